@@ -1,0 +1,49 @@
+#!/usr/bin/env bash
+# build_ref.sh — TEST INFRASTRUCTURE ONLY.
+#
+# Compiles the reference's own host C++ sources, where they lie under
+# /root/reference, into oracle/_ref/libbpref.so (git-ignored; travels to the
+# GPU box as a binary, the sources never do).  Recipe = SURVEY Appendix A:
+#   * g++ -x c++ on curve25519_ops.cu, bulletproof_vectors.cu,
+#     bulletproof_challenge.cu, bulletproof_range_proof.cu (+ -include
+#     cuda_bulletproof.h, the declaration missing at bulletproof_range_proof.cu:724),
+#     complete_bulletproof_test.cu (-Dmain=ref_test_main, for its base-point generator);
+#   * cuda_range_proof_verify.cu exists only inside the notebook (cell at
+#     cudabulletproofoptimized.ipynb:6529); it is extracted to a private temp
+#     dir for the compile and deleted afterwards — nothing lands in the repo;
+#   * oracle/ref/ref_harness.cc (ours): host emulation of the GPU symbols over the
+#     reference's device primitives, deterministic RAND_bytes, flat ctypes API.
+# Links OpenSSL libcrypto (system package) as the reference does.
+set -euo pipefail
+REF=${REF:-/root/reference}
+HERE="$(cd "$(dirname "$0")" && pwd)"
+OUT="$HERE/_ref"
+if [ ! -d "$REF" ]; then
+    echo "build_ref.sh: $REF not present (expected on the GPU box); keeping prebuilt $OUT" >&2
+    exit 0
+fi
+mkdir -p "$OUT"
+TMP="$(mktemp -d)"
+trap 'rm -rf "$TMP"' EXIT
+python3 - "$REF/cudabulletproofoptimized.ipynb" "$TMP" <<'EOF'
+import json, sys
+nb = json.load(open(sys.argv[1]))
+for c in nb["cells"]:
+    src = "".join(c["source"])
+    if src.startswith("%%writefile cuda_range_proof_verify.cu"):
+        open(sys.argv[2] + "/cuda_range_proof_verify.cu", "w").write(src.split("\n", 1)[1])
+        break
+else:
+    sys.exit("notebook cell for cuda_range_proof_verify.cu not found")
+EOF
+F="-O2 -w -x c++ -fPIC -I$REF"
+cd "$TMP"
+g++ $F -c "$REF/curve25519_ops.cu" -o curve25519_ops.o
+g++ $F -c "$REF/bulletproof_vectors.cu" -o bulletproof_vectors.o
+g++ $F -c "$REF/bulletproof_challenge.cu" -o bulletproof_challenge.o
+g++ $F -include cuda_bulletproof.h -c "$REF/bulletproof_range_proof.cu" -o bulletproof_range_proof.o
+g++ $F -D__device__= -c "$TMP/cuda_range_proof_verify.cu" -o cuda_range_proof_verify.o
+g++ $F -Dmain=ref_test_main -c "$REF/complete_bulletproof_test.cu" -o complete_bulletproof_test.o
+g++ -O2 -w -fPIC -I"$REF" -D__device__= -c "$HERE/ref/ref_harness.cc" -o ref_harness.o
+g++ -shared -Wl,-Bsymbolic -o "$OUT/libbpref.so" *.o -lcrypto
+echo "built $OUT/libbpref.so"

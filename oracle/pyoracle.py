@@ -1,0 +1,273 @@
+"""pyoracle — TEST INFRASTRUCTURE ONLY.
+
+ctypes bindings for the CPU restatement (oracle/libbp_oracle.so) and, when it
+has been built, the reference build (oracle/_ref/libbpref.so).  Imported only by
+tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.
+
+Array conventions (the reference's own layouts):
+  fe25519 -> numpy uint64 (..., 4)   little-endian limbs   (curve25519_ops.h:15-17)
+  ge25519 -> numpy uint64 (..., 16)  X|Y|Z|T limbs         (curve25519_ops.h:20-25)
+  head    -> numpy uint64 (100,)     V,A,S,T1,T2 (5x16) then taux,mu,t,c,x (5x4)
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "libbp_oracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libbpref.so")
+
+HEAD_WORDS = 5 * 16 + 5 * 4
+_c = ctypes.c_void_p
+_sz = ctypes.c_size_t
+
+
+def build():
+    """Compile the C restatement (and the reference build when /root/reference exists)."""
+    subprocess.check_call(["make", "-s", "-C", HERE, "libbp_oracle.so"])
+    if os.path.isdir("/root/reference"):
+        subprocess.check_call([os.path.join(HERE, "build_ref.sh")], stdout=subprocess.DEVNULL)
+
+
+def _p(a):
+    return a.ctypes.data_as(_c)
+
+
+def fe(n=None):
+    return np.zeros((4,) if n is None else (n, 4), np.uint64)
+
+
+def ge(n=None):
+    return np.zeros((16,) if n is None else (n, 16), np.uint64)
+
+
+class _Lib:
+    prefix = ""
+
+    def __init__(self, path):
+        self.lib = ctypes.CDLL(path)
+
+    def f(self, name):
+        return getattr(self.lib, self.prefix + name)
+
+
+class Oracle(_Lib):
+    """The C restatement (bp_oracle.c)."""
+
+    prefix = "orc_"
+
+    def __init__(self, path=ORACLE_SO):
+        if not os.path.exists(path):
+            build()
+        super().__init__(path)
+        self.lib.orc_cuda_range_proof_verify.restype = ctypes.c_int
+        self.lib.orc_cuda_inner_product_verify.restype = ctypes.c_int
+
+    # field ------------------------------------------------------------
+    def _fe2(self, name, f, g):
+        h = fe()
+        self.f(name)(_p(h), _p(np.ascontiguousarray(f, np.uint64)), _p(np.ascontiguousarray(g, np.uint64)))
+        return h
+
+    def fe_add(self, f, g):
+        return self._fe2("fe_add", f, g)
+
+    def fe_sub(self, f, g):
+        return self._fe2("fe_sub", f, g)
+
+    def fe_mul(self, f, g):
+        return self._fe2("fe_mul", f, g)
+
+    def fe_invert(self, f):
+        h = fe()
+        self.f("fe_invert")(_p(h), _p(np.ascontiguousarray(f, np.uint64)))
+        return h
+
+    def fe_square_kernel(self, f):
+        h = fe()
+        self.f("fe_square_kernel")(_p(h), _p(np.ascontiguousarray(f, np.uint64)))
+        return h
+
+    def fe_tobytes(self, f):
+        b = np.zeros(32, np.uint8)
+        self.f("fe_tobytes")(_p(b), _p(np.ascontiguousarray(f, np.uint64)))
+        return b
+
+    # points -----------------------------------------------------------
+    def ge_add(self, p, q):
+        r = ge()
+        self.f("ge_add")(_p(r), _p(np.ascontiguousarray(p, np.uint64)), _p(np.ascontiguousarray(q, np.uint64)))
+        return r
+
+    def ge_scalarmult(self, s32, p):
+        r = ge()
+        self.f("ge_scalarmult")(_p(r), _p(np.ascontiguousarray(s32, np.uint8)), _p(np.ascontiguousarray(p, np.uint64)))
+        return r
+
+    def ge_normalize_host(self, p):
+        q = np.array(p, np.uint64)
+        self.f("ge_normalize_host")(_p(q))
+        return q
+
+    def ge_normalize_dev(self, p):
+        q = np.array(p, np.uint64)
+        self.f("ge_normalize_dev")(_p(q))
+        return q
+
+    # vectors ----------------------------------------------------------
+    def msm_canon(self, s, P):
+        r = ge()
+        s = np.ascontiguousarray(s, np.uint64)
+        P = np.ascontiguousarray(P, np.uint64)
+        self.f("msm_canon")(_p(r), _p(s), _p(P), _sz(len(P)))
+        return r
+
+    def msm_cpu(self, s, P):
+        r = ge()
+        s = np.ascontiguousarray(s, np.uint64)
+        P = np.ascontiguousarray(P, np.uint64)
+        self.f("msm_cpu")(_p(r), _p(s), _p(P), _sz(len(P)))
+        return r
+
+    def inner_product(self, a, b):
+        r = fe()
+        a = np.ascontiguousarray(a, np.uint64)
+        b = np.ascontiguousarray(b, np.uint64)
+        self.f("inner_product")(_p(r), _p(a), _p(b), _sz(len(a)))
+        return r
+
+    def base_points(self, n, seed_byte):
+        out = ge(n)
+        seed = np.zeros(32, np.uint8)
+        seed[0] = seed_byte
+        self.f("base_points")(_p(out), _sz(n), _p(seed))
+        return out
+
+    def gh(self):
+        g, h = ge(), ge()
+        self.f("gh")(_p(g), _p(h))
+        return g, h
+
+    def sha256(self, data):
+        buf = np.frombuffer(bytes(data), np.uint8).copy()
+        out = np.zeros(32, np.uint8)
+        self.f("sha256")(_p(out), _p(buf) if len(buf) else None, _sz(len(buf)))
+        return out.tobytes()
+
+    # verify -----------------------------------------------------------
+    def cuda_range_proof_verify(self, head, V, n, a, b, L, R, G, H, g, h, trace=False):
+        """crv:82 semantics. Returns (ok, P, check_point, Gtrace, Htrace)."""
+        head = np.ascontiguousarray(head, np.uint64)
+        a = np.ascontiguousarray(a, np.uint64).reshape(-1, 4)
+        b = np.ascontiguousarray(b, np.uint64).reshape(-1, 4)
+        L = np.ascontiguousarray(L, np.uint64).reshape(-1, 16)
+        R = np.ascontiguousarray(R, np.uint64).reshape(-1, 16)
+        P, chk = ge(), ge()
+        chk[:] = 0
+        Gt = ge(max(n - 1, 1)) if trace else None
+        Ht = ge(max(n - 1, 1)) if trace else None
+        ok = self.f("cuda_range_proof_verify")(
+            _p(head), _p(np.ascontiguousarray(V, np.uint64)), _sz(n), _p(a), _p(b), _sz(len(a)), _p(L), _p(R),
+            _sz(len(L)), _p(np.ascontiguousarray(G, np.uint64)), _p(np.ascontiguousarray(H, np.uint64)),
+            _p(np.ascontiguousarray(g, np.uint64)), _p(np.ascontiguousarray(h, np.uint64)), _p(P), _p(chk),
+            _p(Gt) if trace else None, _p(Ht) if trace else None)
+        return bool(ok), P, chk, Gt, Ht
+
+
+class Reference(_Lib):
+    """The reference's own host code (oracle/_ref/libbpref.so)."""
+
+    prefix = "ref_"
+
+    def __init__(self, path=REF_SO):
+        super().__init__(path)
+        for n in ("prove", "cuda_range_proof_verify", "range_proof_verify"):
+            self.f(n).restype = ctypes.c_int
+
+    def fe_op(self, name, *args):
+        h = fe()
+        self.f(name)(_p(h), *[_p(np.ascontiguousarray(x, np.uint64)) for x in args])
+        return h
+
+    def fe_tobytes(self, f):
+        b = np.zeros(32, np.uint8)
+        self.f("fe_tobytes")(_p(b), _p(np.ascontiguousarray(f, np.uint64)))
+        return b
+
+    def ge_op(self, name, *args):
+        r = ge()
+        self.f(name)(_p(r), *[_p(np.ascontiguousarray(x)) for x in args])
+        return r
+
+    def ge_normalize(self, name, p):
+        q = np.array(p, np.uint64)
+        self.f(name)(_p(q))
+        return q
+
+    def msm(self, name, s, P):
+        r = ge()
+        self.f(name)(_p(r), _p(np.ascontiguousarray(s)), _p(np.ascontiguousarray(P, np.uint64)), _sz(len(P)))
+        return r
+
+    def base_points(self, n, seed_byte):
+        out = ge(n)
+        seed = np.zeros(32, np.uint8)
+        seed[0] = seed_byte
+        self.f("base_points")(_p(out), _sz(n), _p(seed))
+        return out
+
+    def gh(self):
+        g, h = ge(), ge()
+        self.f("gh")(_p(g), _p(h))
+        return g, h
+
+    def prove(self, seed, value32, n, G, H, g, h):
+        """Deterministic reference proof. Returns dict(V, head, a, b, L, R) or None (prover refused)."""
+        V, head = ge(), np.zeros(HEAD_WORDS, np.uint64)
+        a, b, L, R = fe(n), fe(n), ge(n), ge(n)
+        abl, ll = _sz(), _sz()
+        r = self.f("prove")(ctypes.c_uint64(seed), _p(np.ascontiguousarray(value32, np.uint8)), _sz(n), _p(G), _p(H),
+                            _p(g), _p(h), _p(V), _p(head), _p(a), _p(b), _p(L), _p(R), ctypes.byref(abl),
+                            ctypes.byref(ll))
+        if r != 0:
+            return None
+        return dict(V=V, head=head, a=a[:abl.value].copy(), b=b[:abl.value].copy(), L=L[:ll.value].copy(),
+                    R=R[:ll.value].copy())
+
+    def _vargs(self, pr, n, G, H, g, h):
+        return (_p(pr["head"]), _p(pr["V"]), _sz(n), _p(pr["a"]), _p(pr["b"]), _sz(len(pr["a"])), _p(pr["L"]),
+                _p(pr["R"]), _sz(len(pr["L"])), _p(G), _p(H), _p(g), _p(h))
+
+    def cuda_range_proof_verify(self, pr, n, G, H, g, h):
+        return bool(self.f("cuda_range_proof_verify")(*self._vargs(pr, n, G, H, g, h)))
+
+    def range_proof_verify(self, pr, n, G, H, g, h):
+        return bool(self.f("range_proof_verify")(*self._vargs(pr, n, G, H, g, h)))
+
+    def verify_P(self, pr, n, G, H, g, h):
+        P, yzx = ge(), np.zeros(96, np.uint8)
+        self.f("verify_P")(_p(pr["head"]), _p(pr["V"]), _sz(n), _p(G), _p(H), _p(g), _p(h), _p(P), _p(yzx))
+        return P, yzx
+
+    def ipa_fold(self, G, H, n, x, L, R, a0, b0, c, Q):
+        rounds = len(L)
+        Gt, Ht, chk = ge(max(n - 1, 1)), ge(max(n - 1, 1)), ge()
+        self.f("ipa_fold")(_p(G), _p(H), _sz(n), _p(np.ascontiguousarray(x, np.uint64)), _p(L), _p(R), _sz(rounds),
+                           _p(np.ascontiguousarray(a0, np.uint64)), _p(np.ascontiguousarray(b0, np.uint64)),
+                           _p(np.ascontiguousarray(c, np.uint64)), _p(Q), _p(Gt), _p(Ht), _p(chk))
+        return Gt, Ht, chk
+
+
+def have_reference():
+    return os.path.exists(REF_SO)
+
+
+def head_fields(head):
+    """Split a flat head into named views."""
+    head = np.asarray(head)
+    pts = head[:80].reshape(5, 16)
+    fes = head[80:].reshape(5, 4)
+    return dict(V=pts[0], A=pts[1], S=pts[2], T1=pts[3], T2=pts[4], taux=fes[0], mu=fes[1], t=fes[2], c=fes[3],
+                x=fes[4])
