@@ -1,0 +1,334 @@
+"""cudabulletproof_amd — MI355X (gfx950) engine for the MSM / inner-product-argument hot path
+of ronantakizawa/cudabulletproof.
+
+The compute path is libcudabulletproof_hip.so (hand-written HIP in csrc/, C ABI in
+include/cudabulletproof_hip.h).  This module is a thin ctypes layer over that ABI:
+
+* reference-named entry points (``cuda_point_vector_multi_scalar_mul``,
+  ``cuda_range_proof_verify`` ...) that take numpy arrays in the reference's layouts
+  and behave like the reference's C functions (cuda_bulletproof.h:13-84);
+* a batched, device-resident verify (``RangeProofBatch`` + ``batch_range_proof_verify``)
+  on torch CUDA tensors, used by bench.py.
+
+There is no CPU fallback: if the library is missing or no GPU is present the calls
+raise.  Layouts (numpy uint64): fe25519 (..., 4), ge25519 (..., 16) = X|Y|Z|T.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "libcudabulletproof_hip.so")
+CSRC = os.path.join(HERE, "csrc")
+SOURCES = ["bp_kernels.hip", "bp_capi.hip"]
+
+_lib = None
+
+
+class BulletproofError(RuntimeError):
+    pass
+
+
+def build(force=False, verbose=False):
+    """Compile the HIP sources for gfx950 into LIB_PATH (in-tree, travels with the repo)."""
+    srcs = [os.path.join(CSRC, s) for s in SOURCES]
+    deps = srcs + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    deps.append(os.path.join(ROOT, "include", "cudabulletproof_hip.h"))
+    if not force and os.path.exists(LIB_PATH):
+        t = os.path.getmtime(LIB_PATH)
+        if all(os.path.getmtime(d) <= t for d in deps):
+            return LIB_PATH
+    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
+           "-o", LIB_PATH + ".tmp"] + srcs
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    os.replace(LIB_PATH + ".tmp", LIB_PATH)
+    return LIB_PATH
+
+
+_c = ctypes.c_void_p
+_sz = ctypes.c_size_t
+
+
+class FieldVector(ctypes.Structure):
+    _fields_ = [("elements", _c), ("length", _sz)]
+
+
+PointVector = FieldVector
+
+
+class InnerProductProof(ctypes.Structure):   # bulletproof_vectors.h:65-74 (144 bytes)
+    _fields_ = [("n", _sz), ("a", FieldVector), ("b", FieldVector), ("c", ctypes.c_uint64 * 4),
+                ("L", PointVector), ("R", PointVector), ("L_len", _sz), ("x", ctypes.c_uint64 * 4)]
+
+
+class RangeProofC(ctypes.Structure):   # bulletproof_range_proof.h:7-18 (880 bytes)
+    _fields_ = [("V", ctypes.c_uint64 * 16), ("A", ctypes.c_uint64 * 16), ("S", ctypes.c_uint64 * 16),
+                ("T1", ctypes.c_uint64 * 16), ("T2", ctypes.c_uint64 * 16), ("taux", ctypes.c_uint64 * 4),
+                ("mu", ctypes.c_uint64 * 4), ("t", ctypes.c_uint64 * 4), ("ip_proof", InnerProductProof)]
+
+
+class ProofBatchC(ctypes.Structure):   # hipbp_proof_batch
+    _fields_ = [("count", _sz), ("n", _sz), ("ab_len", _sz), ("L_len", _sz)] + \
+               [(k, _c) for k in ("V", "A", "S", "T1", "T2", "t", "a", "b", "c", "x", "L", "R")]
+
+
+assert ctypes.sizeof(InnerProductProof) == 144 and ctypes.sizeof(RangeProofC) == 880
+
+EXPORTS = [
+    "cuda_point_vector_multi_scalar_mul", "cuda_point_vector_multi_scalar_mul_shared",
+    "cuda_field_vector_inner_product", "cuda_field_vector_inner_product_shared",
+    "cuda_batch_field_vector_inner_product", "cuda_batch_field_add", "cuda_batch_field_sub",
+    "cuda_batch_field_mul", "cuda_batch_field_mul_karatsuba", "cuda_batch_field_square",
+    "cuda_batch_field_invert", "cuda_soa_field_add", "cuda_range_proof_verify", "cuda_inner_product_verify",
+    "cuda_benchmark_multi_scalar_mul", "cuda_benchmark_inner_product", "cuda_benchmark_field_operations",
+    "cuda_benchmark_range_proof", "hipbp_last_error", "hipbp_device_count", "hipbp_batch_range_proof_verify",
+    "hipbp_batch_inner_product_verify", "hipbp_msm", "hipbp_field_op", "hipbp_sync",
+]
+
+
+def lib():
+    """Load the HIP library (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise BulletproofError(f"{LIB_PATH} missing: run cudabulletproof_amd.build() (hipcc, gfx950)")
+        # One HIP runtime per process: torch bundles its own libamdhip64.so.7 (same SONAME as
+        # /opt/rocm's).  Importing torch first makes the dynamic loader bind this library to the
+        # runtime torch uses, so device pointers, streams and torch.distributed interoperate.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        L = ctypes.CDLL(LIB_PATH)
+        L.hipbp_last_error.restype = ctypes.c_char_p
+        for f in ("cuda_range_proof_verify", "cuda_inner_product_verify"):
+            getattr(L, f).restype = ctypes.c_bool
+        for f in ("hipbp_batch_range_proof_verify", "hipbp_batch_inner_product_verify", "hipbp_msm",
+                  "hipbp_field_op", "hipbp_sync", "hipbp_device_count"):
+            getattr(L, f).restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def require_gpu():
+    n = lib().hipbp_device_count()
+    if n < 1:
+        raise BulletproofError("no HIP device visible: the engine has no CPU fallback")
+    return n
+
+
+def _chk(rc):
+    if rc != 0:
+        raise BulletproofError(lib().hipbp_last_error().decode())
+
+
+def _p(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def _u64(a, last):
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    if a.shape[-1] != last:
+        raise ValueError(f"expected trailing dimension {last}, got {a.shape}")
+    return a
+
+
+# ====================================================================== reference-named host API
+def cuda_point_vector_multi_scalar_mul(scalars, points):
+    """cuda_bulletproof.h:13 — canonical-tree MSM of device-normalized terms."""
+    require_gpu()
+    s, P = _u64(scalars, 4), _u64(points, 16)
+    if len(s) != len(P):
+        raise ValueError("Vector lengths must match for multi-scalar multiplication")
+    out = np.zeros(16, np.uint64)
+    sv, pv = FieldVector(_p(s).value, len(s)), PointVector(_p(P).value, len(P))
+    lib().cuda_point_vector_multi_scalar_mul(_p(out), ctypes.byref(sv), ctypes.byref(pv))
+    return out
+
+
+def cuda_field_vector_inner_product(a, b, shared=False):
+    """cuda_bulletproof.h:22/:26 — the reference's GPU reduction order."""
+    require_gpu()
+    a, b = _u64(a, 4), _u64(b, 4)
+    out = np.zeros(4, np.uint64)
+    av, bv = FieldVector(_p(a).value, len(a)), FieldVector(_p(b).value, len(b))
+    f = lib().cuda_field_vector_inner_product_shared if shared else lib().cuda_field_vector_inner_product
+    f(_p(out), ctypes.byref(av), ctypes.byref(bv))
+    return out
+
+
+def cuda_batch_field_vector_inner_product(a_vectors, b_vectors):
+    require_gpu()
+    a, b = _u64(a_vectors, 4), _u64(b_vectors, 4)
+    nv, n = a.shape[0], a.shape[1]
+    av = (FieldVector * nv)(*[FieldVector(_p(a).value + i * n * 32, n) for i in range(nv)])
+    bv = (FieldVector * nv)(*[FieldVector(_p(b).value + i * n * 32, n) for i in range(nv)])
+    out = np.zeros((nv, 4), np.uint64)
+    lib().cuda_batch_field_vector_inner_product(_p(out), av, bv, _sz(nv))
+    return out
+
+
+def _field(name, a, b=None):
+    require_gpu()
+    a = _u64(a, 4).reshape(-1, 4)
+    out = np.zeros_like(a)
+    if b is None:
+        getattr(lib(), name)(_p(out), _p(a), _sz(len(a)))
+    else:
+        b = _u64(b, 4).reshape(-1, 4)
+        if len(b) != len(a):
+            raise ValueError("length mismatch")
+        getattr(lib(), name)(_p(out), _p(a), _p(b), _sz(len(a)))
+    return out
+
+
+def cuda_batch_field_add(a, b):
+    return _field("cuda_batch_field_add", a, b)
+
+
+def cuda_batch_field_sub(a, b):
+    return _field("cuda_batch_field_sub", a, b)
+
+
+def cuda_batch_field_mul(a, b):
+    return _field("cuda_batch_field_mul", a, b)
+
+
+def cuda_batch_field_mul_karatsuba(a, b):
+    return _field("cuda_batch_field_mul_karatsuba", a, b)
+
+
+def cuda_batch_field_square(a):
+    return _field("cuda_batch_field_square", a)
+
+
+def cuda_batch_field_invert(a):
+    return _field("cuda_batch_field_invert", a)
+
+
+def cuda_soa_field_add(a, b):
+    return _field("cuda_soa_field_add", a, b)
+
+
+def _range_proof_struct(proof, n, keep):
+    """proof: dict(head (100,) u64 = V,A,S,T1,T2 | taux,mu,t,c,x ; a, b (k,4); L, R (m,16))."""
+    head = np.asarray(proof["head"], np.uint64)
+    a, b = _u64(proof["a"], 4), _u64(proof["b"], 4)
+    L, R = _u64(proof["L"], 16).reshape(-1, 16), _u64(proof["R"], 16).reshape(-1, 16)
+    keep += [a, b, L, R]
+    rp = RangeProofC()
+    for i, k in enumerate(("V", "A", "S", "T1", "T2")):
+        getattr(rp, k)[:] = [int(v) for v in head[16 * i:16 * i + 16]]
+    for i, k in enumerate(("taux", "mu", "t")):
+        getattr(rp, k)[:] = [int(v) for v in head[80 + 4 * i:84 + 4 * i]]
+    ip = rp.ip_proof
+    ip.n = n
+    ip.a = FieldVector(_p(a).value, len(a))
+    ip.b = FieldVector(_p(b).value, len(b))
+    ip.c[:] = [int(v) for v in head[92:96]]
+    ip.L = PointVector(_p(L).value, len(L))
+    ip.R = PointVector(_p(R).value, len(R))
+    ip.L_len = len(L)
+    ip.x[:] = [int(v) for v in head[96:100]]
+    return rp
+
+
+def cuda_range_proof_verify(proof, V, n, G, H, g, h):
+    """cuda_bulletproof.h:61 — one proof, host arrays, returns bool (crv:82 semantics)."""
+    require_gpu()
+    keep = []
+    rp = _range_proof_struct(proof, n, keep)
+    V, g, h = _u64(V, 16), _u64(g, 16), _u64(h, 16)
+    G, H = _u64(G, 16), _u64(H, 16)
+    gv, hv = PointVector(_p(G).value, len(G)), PointVector(_p(H).value, len(H))
+    return bool(lib().cuda_range_proof_verify(ctypes.byref(rp), _p(V), _sz(n), ctypes.byref(gv), ctypes.byref(hv),
+                                              _p(g), _p(h)))
+
+
+def cuda_inner_product_verify(proof, P, G, H, Q):
+    """cuda_bulletproof.h:72 — the IPA check alone (crv:130 semantics)."""
+    require_gpu()
+    keep = []
+    G, H = _u64(G, 16), _u64(H, 16)
+    rp = _range_proof_struct(proof, len(G), keep)
+    P, Q = _u64(P, 16), _u64(Q, 16)
+    gv, hv = PointVector(_p(G).value, len(G)), PointVector(_p(H).value, len(H))
+    return bool(lib().cuda_inner_product_verify(ctypes.byref(rp.ip_proof), _p(P), ctypes.byref(gv), ctypes.byref(hv),
+                                                _p(Q)))
+
+
+# ====================================================================== batched device API (torch)
+class RangeProofBatch:
+    """A batch of proofs in the flat wire format, resident on a torch CUDA device.
+
+    Tensors are int64 views of the u64 limbs: V/A/S/T1/T2 (B,16), t/c/x (B,4),
+    a/b (B,ab_len,4), L/R (B,L_len,16).
+    """
+
+    FIELDS = ("V", "A", "S", "T1", "T2", "t", "a", "b", "c", "x", "L", "R")
+
+    def __init__(self, n, **tensors):
+        self.n = int(n)
+        for k in self.FIELDS:
+            setattr(self, k, tensors[k].contiguous())
+        self.count = int(self.V.shape[0])
+        self.ab_len = int(self.a.shape[1])
+        self.L_len = int(self.L.shape[1])
+
+    @classmethod
+    def from_numpy(cls, n, arrays, device):
+        import torch
+        t = {k: torch.from_numpy(np.ascontiguousarray(arrays[k]).view(np.int64)).to(device) for k in cls.FIELDS}
+        return cls(n, **t)
+
+    def c_struct(self):
+        s = ProofBatchC(self.count, self.n, self.ab_len, self.L_len)
+        for k in self.FIELDS:
+            setattr(s, k, getattr(self, k).data_ptr())
+        return s
+
+    def nbytes(self):
+        return sum(getattr(self, k).numel() * 8 for k in self.FIELDS)
+
+
+def _stream_ptr(stream):
+    if stream is None:
+        import torch
+        stream = torch.cuda.current_stream()
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+def batch_range_proof_verify(batch, G, H, g, h, ok, P_out=None, check_out=None, stream=None):
+    """Enqueue cuda_range_proof_verify over the whole batch on `stream` (asynchronous).
+
+    G/H: (n,16) int64 CUDA tensors, g/h: (16,), ok: (B,) uint8, P_out/check_out: (B,16) or None.
+    """
+    s = batch.c_struct()
+    _chk(lib().hipbp_batch_range_proof_verify(
+        ctypes.byref(s), _c(G.data_ptr()), _c(H.data_ptr()), _c(g.data_ptr()), _c(h.data_ptr()), _c(ok.data_ptr()),
+        _c(P_out.data_ptr()) if P_out is not None else None,
+        _c(check_out.data_ptr()) if check_out is not None else None, _stream_ptr(stream)))
+
+
+def batch_inner_product_verify(batch, P, G, H, Q, ok, check_out=None, stream=None):
+    s = batch.c_struct()
+    _chk(lib().hipbp_batch_inner_product_verify(
+        ctypes.byref(s), _c(P.data_ptr()), _c(G.data_ptr()), _c(H.data_ptr()), _c(Q.data_ptr()), _c(ok.data_ptr()),
+        _c(check_out.data_ptr()) if check_out is not None else None, _stream_ptr(stream)))
+
+
+def msm(result, scalars, points, stream=None):
+    """Canonical-tree MSM on CUDA tensors: result (16,), scalars (n,4), points (n,16)."""
+    _chk(lib().hipbp_msm(_c(result.data_ptr()), _c(scalars.data_ptr()), _c(points.data_ptr()),
+                         _sz(points.shape[0]), _stream_ptr(stream)))
+
+
+def field_op(op, r, a, b=None, stream=None):
+    ops = {"add": 0, "sub": 1, "mul": 2, "square": 3, "soa_add": 4, "invert": 5}
+    _chk(lib().hipbp_field_op(ops[op], _c(r.data_ptr()), _c(a.data_ptr()), _c(b.data_ptr()) if b is not None else None,
+                              _sz(a.shape[0]), _stream_ptr(stream)))

@@ -1,0 +1,66 @@
+// bp_kernels.h — host-side launch interface of the gfx950 kernels (internal to the library).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace bp {
+struct fe;
+struct ge;
+
+// Device view of a batch of range proofs in the flat wire format (include/cudabulletproof_hip.h).
+struct BatchView {
+    int B;        // proofs
+    int n;        // range bits = generator count (power of two)
+    int ab_len;   // length of the proof's a/b vectors (>= 1)
+    int L_len;    // IPA rounds (log2 n)
+    const ge* V;  // [B] value commitments (the V argument of cuda_range_proof_verify)
+    const ge* A;  // [B]
+    const ge* S;  // [B]
+    const ge* T1; // [B]
+    const ge* T2; // [B]
+    const fe* t;  // [B]
+    const fe* a;  // [B*ab_len]
+    const fe* b;  // [B*ab_len]
+    const fe* c;  // [B]
+    const fe* x;  // [B]
+    const ge* L;  // [B*L_len]
+    const ge* R;  // [B*L_len]
+};
+
+// Device workspace of one verify batch (allocated by the engine).
+struct VerifyWs {
+    fe* sG;        // [B]      MSM scalar for G (raw limbs)
+    fe* sH;        // [B*n]    MSM scalars for H (raw limbs)
+    fe* sc;        // [B*4]    canonical t, a0, b0, c
+    fe* u;         // [B*L_len] canonical u_r
+    fe* uinv;      // [B*L_len] canonical "u_r^-1"
+    uint8_t* ipok; // [B]
+    ge* msm_pts;   // [B*2*n]  per-point MSM terms
+    ge* msm_part;  // [B*2]    tree results: <sG,G>, <sH,H>
+    ge* terms;     // [B*4]    slots 2,3: t*h, c*Q
+    ge* fold;      // [B*2n]   per-round scalar-mult terms
+    ge* Gc;        // [B*n/2]
+    ge* Hc;        // [B*n/2]
+    ge* fin;       // [B*2]    a0*G', b0*H'
+};
+
+void launch_init_tables(ge* dtab, fe* two_i, int nmax, hipStream_t s);
+
+// Generic canonical-tree MSM: out[seg] for S segments of m points each.
+void launch_msm_points(ge* pts, const fe* scal, const ge* P, size_t m, const ge* dtab, hipStream_t s);
+void launch_tree(ge* out, const ge* in, int S, size_t m, hipStream_t s);
+
+void launch_verify(const BatchView& bv, const VerifyWs& ws, const ge* G, const ge* H, const ge* h,
+                   const ge* dtab, const fe* two_i, const ge* P_in, uint8_t* ok, ge* P_out, ge* chk_out,
+                   bool range_mode, hipStream_t s);
+
+// Elementwise field ops: op 0 add, 1 sub, 2 mul, 3 square-kernel quirk, 4 soa add (limbwise, no carry)
+void launch_field_op(int op, fe* r, const fe* a, const fe* b, size_t count, hipStream_t s);
+void launch_ip_shared(fe* out, const fe* a, const fe* b, size_t n, hipStream_t s);
+void launch_ip_grid(fe* out, fe* part, const fe* a, const fe* b, size_t n, hipStream_t s);
+void launch_ip_batch(fe* out, const fe* a, const fe* b, size_t n, size_t nvec, hipStream_t s);
+void launch_invert(fe* r, const fe* a, size_t count, hipStream_t s);
+void launch_msm_full(ge* result, const fe* scal, const ge* P, size_t n, ge* ptsbuf, ge* part0, ge* part1,
+                     const ge* dtab, hipStream_t s);
+}  // namespace bp

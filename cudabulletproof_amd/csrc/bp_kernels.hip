@@ -1,0 +1,459 @@
+// bp_kernels.hip — gfx950 kernels for the MSM / inner-product-argument verify path.
+//
+// One lane computes one scalar multiplication (the unit of work); waves
+// whose lanes share a scalar take the scalar-branch loop, others the per-lane loop
+// (ge25519_dev.h). Reductions follow the reference's canonical pairwise tree order
+// (cuda_bulletproof_kernels.cu:162-168) through LDS; every order-sensitive fold keeps
+// the reference's order, because the arithmetic is not associative.
+#include "bp_kernels.h"
+#include "ge25519_dev.h"
+#include "sha256_dev.h"
+
+namespace bp {
+
+constexpr int TPB = 256;   // threads per block for lane-per-item kernels
+
+__device__ __forceinline__ size_t gid() { return (size_t)blockIdx.x * blockDim.x + threadIdx.x; }
+
+// ------------------------------------------------------------------ tables
+// dtab[k] = k successive ge25519_add(r, r) of the identity (0,1,1,0): the state of
+// ge25519_scalarmult after k leading zero bits (curve25519_ops.cu:399-414).
+// two_i[i] = i successive fe25519_mul(., 2) from 1 (bulletproof_range_proof.cu:705-712).
+__global__ void k_init_tables(ge* dtab, fe* two_i, int nmax) {
+    if (gid() != 0) return;
+    ge r = ge_zero();
+    dtab[0] = r;
+    for (int k = 1; k <= 256; k++) {
+        r = ge_dbl(r);
+        dtab[k] = r;
+    }
+    fe two = fe_add(fe_set(1), fe_set(1));
+    fe t = fe_set(1);
+    for (int i = 0; i < nmax; i++) {
+        two_i[i] = t;
+        t = fe_mul(t, two);
+    }
+}
+
+void launch_init_tables(ge* dtab, fe* two_i, int nmax, hipStream_t s) {
+    k_init_tables<<<1, 64, 0, s>>>(dtab, two_i, nmax);
+}
+
+// ------------------------------------------------------------------ MSM
+// pts[seg*m + i] = Ndev(scalarmult(rawbytes(scal[seg*m+i]), P[i])) — point_scalar_mul_kernel
+// (cuda_bulletproof_kernels.cu:26-42); the scalar bytes are the raw limbs (device tobytes).
+__global__ __launch_bounds__(TPB) void k_msm_points(ge* pts, const fe* __restrict__ scal,
+                                                    const ge* __restrict__ P, size_t total, size_t m,
+                                                    const ge* __restrict__ dtab) {
+    size_t i = gid();
+    if (i >= total) return;
+    ge r = scalarmult(scal[i], P[i % m], dtab);
+    pts[i] = ge_norm_dev(r);
+}
+
+void launch_msm_points(ge* pts, const fe* scal, const ge* P, size_t m, const ge* dtab, hipStream_t s) {
+    // single segment: total = m
+    size_t blocks = (m + TPB - 1) / TPB;
+    k_msm_points<<<blocks, TPB, 0, s>>>(pts, scal, P, m, m, dtab);
+}
+
+// Canonical pairwise tree over S segments of m points: for stride 1,2,4,..:
+//   T[i] = Ndev(T[i] + T[i+stride]) for i % (2 stride) == 0 and i + stride < m.
+// One block folds 256 consecutive points (levels 1..128); out has S*ceil(m/256) entries.
+__global__ __launch_bounds__(TPB) void k_tree(ge* out, const ge* __restrict__ in, size_t m, int nb) {
+    __shared__ ge sh[TPB];
+    int seg = blockIdx.x / nb, chunk = blockIdx.x % nb;
+    int tid = threadIdx.x;
+    size_t base = (size_t)seg * m + (size_t)chunk * TPB;
+    int cnt = (int)min((size_t)TPB, m - (size_t)chunk * TPB);
+    if (tid < cnt) sh[tid] = in[base + tid];
+    __syncthreads();
+    for (int st = 1; st < cnt; st <<= 1) {
+        if ((tid % (2 * st)) == 0 && tid + st < cnt) sh[tid] = ge_norm_dev(ge_add(sh[tid], sh[tid + st]));
+        __syncthreads();
+    }
+    if (tid == 0) out[blockIdx.x] = sh[0];
+}
+
+void launch_tree(ge* out, const ge* in, int S, size_t m, hipStream_t s) {
+    int nb = (int)((m + TPB - 1) / TPB);
+    k_tree<<<S * nb, TPB, 0, s>>>(out, in, m, nb);
+}
+
+// ------------------------------------------------------------------ verify: challenges & scalars
+__device__ __forceinline__ void sha_fe_canon(sha256_ctx& c, const fe& f) {
+    fe t = fe_canon(f);
+    sha_limbs(c, t.v, 4);
+}
+
+__device__ __forceinline__ fe challenge_digest(sha256_ctx& c) {
+    fe r;
+    sha_final_limbs(c, r.v);
+    r.v[3] &= 0x7FFFFFFFFFFFFFFFull;   // output[31] &= 0x7F (bulletproof_challenge.cu:20)
+    return r;
+}
+
+// cuda_range_proof_verify (crv:93-106) + calculate_inner_product_point scalars
+// (bulletproof_range_proof.cu:679-718): one lane per proof.
+__global__ __launch_bounds__(TPB) void k_prep_range(BatchView bv, VerifyWs ws, const fe* __restrict__ two_i) {
+    size_t p = gid();
+    if (p >= (size_t)bv.B) return;
+    const int n = bv.n;
+    sha256_ctx c;
+    // y = H("BulletproofYChal" || V.X V.Y A.X A.Y S.X S.Y || "y_ch")   (challenge.cu:24-44)
+    sha_init(c);
+    sha_str(c, "BulletproofYChal");
+    sha_fe_canon(c, bv.V[p].X); sha_fe_canon(c, bv.V[p].Y);
+    sha_fe_canon(c, bv.A[p].X); sha_fe_canon(c, bv.A[p].Y);
+    sha_fe_canon(c, bv.S[p].X); sha_fe_canon(c, bv.S[p].Y);
+    sha_str(c, "y_ch");
+    fe y = challenge_digest(c);
+    // z = H("BulletproofZChal" || y || "z_ch")   (challenge.cu:47-58)
+    sha_init(c);
+    sha_str(c, "BulletproofZChal");
+    sha_limbs(c, y.v, 4);
+    sha_str(c, "z_ch");
+    fe z = challenge_digest(c);
+    // (x is derived at crv:105 but only feeds compute_precise_delta and the unused
+    //  x argument of calculate_inner_product_point; it does not affect any output.)
+    fe z2 = fe_mul(z, z);
+    ws.sG[p] = fe_sub(fe_set(0), z);   // rp.cu:699  0 - z
+    fe pw = fe_set(1);
+    for (int i = 0; i < n; i++) {
+        if (i > 0) pw = fe_mul(pw, y);   // powers_of (rp.cu:299-313)
+        fe h = fe_add(z, fe_mul(z2, two_i[i]));
+        ws.sH[p * n + i] = fe_mul(h, pw);
+    }
+    ws.sc[p * 4 + 0] = fe_canon(bv.t[p]);
+}
+
+// cuda_inner_product_verify (crv:146-218): <a,b> check and the per-round challenges.
+__global__ __launch_bounds__(TPB) void k_prep_ipa(BatchView bv, VerifyWs ws) {
+    size_t p = gid();
+    if (p >= (size_t)bv.B) return;
+    const int abl = bv.ab_len, Lr = bv.L_len;
+    fe acc = fe_set(0);
+    for (int i = 0; i < abl; i++) acc = fe_add(acc, fe_mul(bv.a[p * abl + i], bv.b[p * abl + i]));   // vectors.cu:101
+    ws.ipok[p] = fe_eq(fe_canon(acc), fe_canon(bv.c[p])) ? 1 : 0;
+    fe tr = fe_set(0);   // transcript (crv:168)
+    for (int r = 0; r < Lr; r++) {
+        fe u;
+        if (r == 0) {
+            u = bv.x[p];
+        } else {
+            sha256_ctx c;
+            sha_init(c);
+            sha_str(c, "InnerProductChal");
+            sha_limbs(c, tr.v, 4);
+            sha_fe_canon(c, bv.L[p * Lr + r].X);
+            sha_fe_canon(c, bv.R[p * Lr + r].X);
+            u = challenge_digest(c);
+            tr = u;
+        }
+        ws.u[p * Lr + r] = fe_canon(u);
+        ws.uinv[p * Lr + r] = fe_canon(fe_invert(u));
+    }
+    ws.sc[p * 4 + 1] = fe_canon(bv.a[p * abl]);
+    ws.sc[p * 4 + 2] = fe_canon(bv.b[p * abl]);
+    ws.sc[p * 4 + 3] = fe_canon(bv.c[p]);
+}
+
+// ------------------------------------------------------------------ verify: scalar multiplications
+// The two MSMs of calculate_inner_product_point (rp.cu:724, :728): segment 2p = <sG, G>,
+// segment 2p+1 = <sH, H>.  Item layout keeps a G segment's lanes together so that its
+// waves share one scalar.
+__global__ __launch_bounds__(TPB) void k_verify_msm_points(BatchView bv, VerifyWs ws, const ge* __restrict__ G,
+                                                           const ge* __restrict__ H, const ge* __restrict__ dtab) {
+    size_t i = gid();
+    const int n = bv.n;
+    if (i >= (size_t)bv.B * 2 * n) return;
+    size_t seg = i / n;
+    int k = (int)(i % n);
+    size_t p = seg >> 1;
+    bool isH = seg & 1;
+    fe s = isH ? ws.sH[p * n + k] : ws.sG[p];
+    ge r = scalarmult(s, isH ? H[k] : G[k], dtab);
+    ws.msm_pts[i] = ge_norm_dev(r);
+}
+
+// Stage-0 host-semantics scalar-mults independent of the IPA rounds:
+// t*h (rp.cu:778-781) and c*Q (crv:255, :268-269).  Items: 2p -> t*h, 2p+1 -> c*Q.
+__global__ __launch_bounds__(TPB) void k_verify_th_cq(BatchView bv, VerifyWs ws, const ge* __restrict__ h,
+                                                      const ge* __restrict__ dtab) {
+    size_t i = gid();
+    if (i >= (size_t)bv.B * 2) return;
+    size_t p = i >> 1;
+    bool isC = i & 1;
+    fe s = isC ? ws.sc[p * 4 + 3] : ws.sc[p * 4 + 0];
+    ge r = scalarmult(s, *h, dtab);
+    ws.terms[p * 4 + 2 + (isC ? 1 : 0)] = ge_norm_host(r);
+}
+
+// IPA fold round r (crv:220-242), n' = n >> (r+1).  Items per proof (4n'):
+//   [0,n')   u^-1 * G_j        [n',2n')  u^-1 * H_{j+n'}
+//   [2n',3n') u * G_{j+n'}     [3n',4n') u * H_j
+// (lanes sharing a scalar are adjacent).  Round 0 reads the generators, later rounds
+// the proof's folded Gc/Hc.
+__global__ __launch_bounds__(TPB) void k_fold_terms(BatchView bv, VerifyWs ws, int r, const ge* __restrict__ G,
+                                                    const ge* __restrict__ H, const ge* __restrict__ dtab) {
+    const int n = bv.n, np = n >> (r + 1), Lr = bv.L_len;
+    size_t i = gid();
+    if (i >= (size_t)bv.B * 4 * np) return;
+    size_t p = i / (4 * np);
+    int k = (int)(i % (4 * np));
+    int grp = k / np, j = k % np;
+    const ge* Gs = (r == 0) ? G : ws.Gc + p * (n / 2);
+    const ge* Hs = (r == 0) ? H : ws.Hc + p * (n / 2);
+    const ge* pt;
+    fe s;
+    if (grp == 0) { pt = &Gs[j];      s = ws.uinv[p * Lr + r]; }
+    else if (grp == 1) { pt = &Hs[j + np]; s = ws.uinv[p * Lr + r]; }
+    else if (grp == 2) { pt = &Gs[j + np]; s = ws.u[p * Lr + r]; }
+    else { pt = &Hs[j];      s = ws.u[p * Lr + r]; }
+    ge t = scalarmult(s, *pt, dtab);
+    ws.fold[p * (2 * n) + k] = ge_norm_host(t);
+}
+
+// G'_j = N(term(u^-1 G_j) + term(u G_{j+n'})),  H'_j = N(term(u H_j) + term(u^-1 H_{j+n'}))  (crv:230, :240)
+__global__ __launch_bounds__(TPB) void k_fold_combine(BatchView bv, VerifyWs ws, int r) {
+    const int n = bv.n, np = n >> (r + 1);
+    size_t i = gid();
+    if (i >= (size_t)bv.B * 2 * np) return;
+    size_t p = i / (2 * np);
+    int k = (int)(i % (2 * np));
+    const ge* f = ws.fold + p * (2 * n);
+    if (k < np) {
+        int j = k;
+        ws.Gc[p * (n / 2) + j] = ge_norm_host(ge_add(f[j], f[2 * np + j]));
+    } else {
+        int j = k - np;
+        ws.Hc[p * (n / 2) + j] = ge_norm_host(ge_add(f[3 * np + j], f[np + j]));
+    }
+}
+
+// a0*G'_0 and b0*H'_0 (crv:262-266).  Items: 2p -> a0*G', 2p+1 -> b0*H'.
+__global__ __launch_bounds__(TPB) void k_final_terms(BatchView bv, VerifyWs ws, const ge* __restrict__ G,
+                                                     const ge* __restrict__ H, const ge* __restrict__ dtab) {
+    size_t i = gid();
+    if (i >= (size_t)bv.B * 2) return;
+    size_t p = i >> 1;
+    bool isH = i & 1;
+    const int n = bv.n;
+    const ge* pt = (bv.L_len > 0) ? (isH ? &ws.Hc[p * (n / 2)] : &ws.Gc[p * (n / 2)]) : (isH ? &H[0] : &G[0]);
+    fe s = ws.sc[p * 4 + (isH ? 2 : 1)];
+    ge t = scalarmult(s, *pt, dtab);
+    ws.fin[p * 2 + (isH ? 1 : 0)] = ge_norm_host(t);
+}
+
+__device__ __forceinline__ int absdiff(int a, int b) { return a > b ? a - b : b - a; }
+
+// P assembly (rp.cu:785-801), check point (crv:257-278) and the tolerant accept rule
+// (crv:297-357).  One lane per proof.
+__global__ __launch_bounds__(TPB) void k_final(BatchView bv, VerifyWs ws, const ge* __restrict__ P_in,
+                                               uint8_t* ok, ge* P_out, ge* chk_out, int range_mode) {
+    size_t p = gid();
+    if (p >= (size_t)bv.B) return;
+    ge P;
+    if (range_mode) {
+        P = ge_zero();
+        P = ge_norm_host(ge_add(P, ws.msm_part[p * 2 + 0]));
+        P = ge_norm_host(ge_add(P, ws.msm_part[p * 2 + 1]));
+        P = ge_norm_host(ge_add(P, ws.terms[p * 4 + 2]));
+        P = ge_norm_host(P);
+        P = ge_norm_host(P);
+    } else {
+        P = P_in[p];
+    }
+    ge cp = ge_zero();
+    cp = ge_norm_host(ge_add(cp, ws.fin[p * 2 + 0]));
+    cp = ge_norm_host(ge_add(cp, ws.fin[p * 2 + 1]));
+    cp = ge_norm_host(ge_add(cp, ws.terms[p * 4 + 3]));
+    if (P_out) P_out[p] = P;
+    if (chk_out) chk_out[p] = cp;
+
+    fe kx = fe_canon(cp.X), ky = fe_canon(cp.Y), px = fe_canon(P.X), py = fe_canon(P.Y);
+    int xd = 0, yd = 0, sx = 0, sy = 0, msb = 0;
+    for (int i = 0; i < 32; i++) {
+        int a = (int)((kx.v[i >> 3] >> (8 * (i & 7))) & 0xff), b = (int)((px.v[i >> 3] >> (8 * (i & 7))) & 0xff);
+        int c2 = (int)((ky.v[i >> 3] >> (8 * (i & 7))) & 0xff), d = (int)((py.v[i >> 3] >> (8 * (i & 7))) & 0xff);
+        int dx = absdiff(a, b), dy = absdiff(c2, d);
+        xd += dx > 0; yd += dy > 0;
+        sx += (dx > 0) & (dx <= 10); sy += (dy > 0) & (dy <= 10);
+    }
+    msb = 64 - __popcll(kx.v[3] ^ px.v[3]);   // bits of bytes 24..31 of X
+    sha256_ctx c;
+    sha_init(c);
+    sha_limbs(c, kx.v, 4); sha_limbs(c, ky.v, 4);
+    sha_limbs(c, px.v, 4); sha_limbs(c, py.v, 4);
+    fe hs;
+    sha_final_limbs(c, hs.v);
+    int hz = 0;
+    for (int i = 0; i < 32; i++) hz += ((hs.v[i >> 3] >> (8 * (i & 7))) & 0xff) != 0;
+    bool accept = (sx + sy >= 20) | (msb >= 28) | (xd + yd <= 32) | (hz <= 24);
+    ok[p] = (ws.ipok[p] && accept) ? 1 : 0;
+}
+
+static inline unsigned nblk(size_t items) { return (unsigned)((items + TPB - 1) / TPB); }
+
+void launch_verify(const BatchView& bv, const VerifyWs& ws, const ge* G, const ge* H, const ge* h,
+                   const ge* dtab, const fe* two_i, const ge* P_in, uint8_t* ok, ge* P_out, ge* chk_out,
+                   bool range_mode, hipStream_t s) {
+    const size_t B = bv.B;
+    const int n = bv.n;
+    if (range_mode) {
+        k_prep_range<<<nblk(B), TPB, 0, s>>>(bv, ws, two_i);
+    }
+    k_prep_ipa<<<nblk(B), TPB, 0, s>>>(bv, ws);
+    if (range_mode) {
+        k_verify_msm_points<<<nblk(B * 2 * n), TPB, 0, s>>>(bv, ws, G, H, dtab);
+        // canonical tree per MSM segment (n <= 256: one pass, results in msm_part[2p + {0,1}])
+        launch_tree(ws.msm_part, ws.msm_pts, (int)(2 * B), (size_t)n, s);
+    }
+    k_verify_th_cq<<<nblk(B * 2), TPB, 0, s>>>(bv, ws, h, dtab);
+    for (int r = 0; r < bv.L_len; r++) {
+        int np = n >> (r + 1);
+        k_fold_terms<<<nblk(B * 4 * np), TPB, 0, s>>>(bv, ws, r, G, H, dtab);
+        k_fold_combine<<<nblk(B * 2 * np), TPB, 0, s>>>(bv, ws, r);
+    }
+    k_final_terms<<<nblk(B * 2), TPB, 0, s>>>(bv, ws, G, H, dtab);
+    k_final<<<nblk(B), TPB, 0, s>>>(bv, ws, P_in, ok, P_out, chk_out, range_mode ? 1 : 0);
+}
+
+// ------------------------------------------------------------------ batch field ops
+// cuda_field_ops.cu:37-73 (add/sub/mul), :147 (square quirk), :521 (SoA add: limbwise, no carry)
+__global__ __launch_bounds__(TPB) void k_field_op(int op, fe* r, const fe* __restrict__ a, const fe* __restrict__ b,
+                                                  size_t count) {
+    size_t i = gid();
+    if (i >= count) return;
+    fe x = a[i], y;
+    if (op != 3) y = b[i];
+    fe z;
+    switch (op) {
+        case 0: z = fe_add(x, y); break;
+        case 1: z = fe_sub(x, y); break;
+        case 2: z = fe_mul(x, y); break;
+        case 3: z = fe_square_kernel_quirk(x); break;
+        default:
+#pragma unroll
+            for (int k = 0; k < 4; k++) z.v[k] = x.v[k] + y.v[k];
+            break;
+    }
+    r[i] = z;
+}
+
+void launch_field_op(int op, fe* r, const fe* a, const fe* b, size_t count, hipStream_t s) {
+    if (count == 0) return;
+    k_field_op<<<nblk(count), TPB, 0, s>>>(op, r, a, b, count);
+}
+
+
+// ------------------------------------------------------------------ field inner products
+// cuda_inner_product.cu:154-183 field_vector_inner_product_shared_kernel, one block of
+// nthreads = min(n, 512): products, then halving tree from nthreads/2 with tid+stride < n.
+__global__ __launch_bounds__(512) void k_ip_shared(fe* out, const fe* __restrict__ a, const fe* __restrict__ b,
+                                                   size_t n) {
+    __shared__ fe sh[512];
+    int tid = threadIdx.x;
+    sh[tid] = fe_mul(a[tid], b[tid]);
+    __syncthreads();
+    for (unsigned st = blockDim.x / 2; st > 0; st >>= 1) {
+        if (tid < (int)st && (size_t)(tid + st) < n) sh[tid] = fe_add(sh[tid], sh[tid + st]);
+        __syncthreads();
+    }
+    if (tid == 0) *out = sh[0];
+}
+
+// cuda_inner_product.cu:33-61 field_vector_inner_product_kernel: grid-stride fold from 0,
+// then block tree 128..1 over all 256 slots.  With `warp_tail`, the tree stops at 32 and the
+// 16..1 halving of warp_reduce_field_element (:219-257) finishes it (batch_inner_product_kernel
+// :260-299).  blockIdx.y selects the vector (stride n) for the batched form.
+__global__ __launch_bounds__(TPB) void k_ip_grid(fe* out, const fe* __restrict__ a, const fe* __restrict__ b,
+                                                 size_t n, size_t grid_threads, int warp_tail) {
+    __shared__ fe sh[TPB];
+    int tid = threadIdx.x;
+    size_t vec = blockIdx.y;
+    a += vec * n;
+    b += vec * n;
+    fe acc = fe_set(0);
+    for (size_t idx = (size_t)blockIdx.x * TPB + tid; idx < n; idx += grid_threads) acc = fe_add(acc, fe_mul(a[idx], b[idx]));
+    sh[tid] = acc;
+    __syncthreads();
+    int stop = warp_tail ? 32 : 1;
+    for (int st = TPB / 2; st >= stop; st >>= 1) {
+        if (tid < st) sh[tid] = fe_add(sh[tid], sh[tid + st]);
+        __syncthreads();
+    }
+    if (warp_tail) {
+        for (int st = 16; st >= 1; st >>= 1) {
+            if (tid < st) sh[tid] = fe_add(sh[tid], sh[tid + st]);
+            __syncthreads();
+        }
+    }
+    if (tid == 0) out[vec * gridDim.x + blockIdx.x] = sh[0];
+}
+
+// cuda_inner_product.cu:69-92 fe25519_reduce_kernel: 256 slots, partials beyond 256 unread.
+__global__ __launch_bounds__(TPB) void k_ip_reduce(fe* out, const fe* __restrict__ part, size_t np) {
+    __shared__ fe sh[TPB];
+    int tid = threadIdx.x;
+    sh[tid] = (size_t)tid < np ? part[tid] : fe_set(0);
+    __syncthreads();
+    for (int st = TPB / 2; st > 0; st >>= 1) {
+        if (tid < st && (size_t)(tid + st) < np) sh[tid] = fe_add(sh[tid], sh[tid + st]);
+        __syncthreads();
+    }
+    if (tid == 0) *out = sh[0];
+}
+
+void launch_ip_shared(fe* out, const fe* a, const fe* b, size_t n, hipStream_t s) {
+    unsigned nt = (unsigned)(n < 512 ? n : 512);
+    if (nt == 0) return;
+    k_ip_shared<<<1, nt, 0, s>>>(out, a, b, n);
+}
+
+void launch_ip_grid(fe* out, fe* part, const fe* a, const fe* b, size_t n, hipStream_t s) {
+    size_t nb = (n + TPB - 1) / TPB;
+    if (nb > 1024) nb = 1024;
+    k_ip_grid<<<dim3((unsigned)nb, 1), TPB, 0, s>>>(part, a, b, n, nb * TPB, 0);
+    k_ip_reduce<<<1, TPB, 0, s>>>(out, part, nb);
+}
+
+// Batched form: the reference launches min(1024, ceil(n/256)) x-blocks per vector that all
+// write results[vec] (a race when n > 256); block 0's value is one of its possible outcomes
+// and is the one returned.
+void launch_ip_batch(fe* out, const fe* a, const fe* b, size_t n, size_t nvec, hipStream_t s) {
+    size_t nb = (n + TPB - 1) / TPB;
+    if (nb > 1024) nb = 1024;
+    if (nb == 0) nb = 1;
+    k_ip_grid<<<dim3(1, (unsigned)nvec), TPB, 0, s>>>(out, a, b, n, nb * TPB, 1);
+}
+
+// elementwise host invert chain (defined semantics for cuda_batch_field_invert)
+__global__ __launch_bounds__(TPB) void k_invert(fe* r, const fe* __restrict__ a, size_t count) {
+    size_t i = gid();
+    if (i < count) r[i] = fe_invert(a[i]);
+}
+void launch_invert(fe* r, const fe* a, size_t count, hipStream_t s) {
+    if (count) k_invert<<<nblk(count), TPB, 0, s>>>(r, a, count);
+}
+
+// Generic canonical-tree MSM on device: ptsbuf holds n points, part0/part1 ping-pong.
+void launch_msm_full(ge* result, const fe* scal, const ge* P, size_t n, ge* ptsbuf, ge* part0, ge* part1,
+                     const ge* dtab, hipStream_t s) {
+    launch_msm_points(ptsbuf, scal, P, n, dtab, s);
+    const ge* in = ptsbuf;
+    size_t m = n;
+    ge* bufs[2] = {part0, part1};
+    int w = 0;
+    while (true) {
+        size_t nb = (m + TPB - 1) / TPB;
+        ge* out = (nb == 1) ? result : bufs[w];
+        launch_tree(out, in, 1, m, s);
+        if (nb == 1) break;
+        in = out;
+        m = nb;
+        w ^= 1;
+    }
+}
+
+}  // namespace bp

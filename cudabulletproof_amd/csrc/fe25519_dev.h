@@ -1,0 +1,216 @@
+// fe25519_dev.h — gfx950 device arithmetic for the reference's "fe25519" field elements.
+//
+// The reference arithmetic is NOT GF(2^255-19): every routine here
+// reproduces the exact bits of curve25519_ops.cu / device_curve25519_ops.cuh,
+// including the lossy borrow chains and the truncated 19x fold. Only the ways the
+// same bits are computed are free: the 512-bit product is formed by 32x32->64
+// multiply-accumulates (product scanning), the "- p" fix-up is a closed form of the
+// reference's borrow loop, and the tobytes/normalize early-outs are branch-free.
+//
+// Layout: 4 little-endian u64 limbs (curve25519_ops.h:15-17) kept in VGPR pairs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bp {
+
+struct fe {
+    uint64_t v[4];
+};
+
+#define BP_DEV __device__ __forceinline__
+
+constexpr uint64_t P0 = 0xFFFFFFFFFFFFFFEDull;   // curve25519_ops.cu:7-8
+constexpr uint64_t P3 = 0x7FFFFFFFFFFFFFFFull;
+constexpr uint64_t M64 = 0xFFFFFFFFFFFFFFFFull;
+
+BP_DEV fe fe_set(uint64_t x) { return fe{{x, 0, 0, 0}}; }
+
+// t >= p, lexicographic from limb 3 (curve25519_ops.cu:54-59). p1 = p2 = 2^64-1.
+BP_DEV bool fe_ge_p(const fe& t) {
+    bool top = (t.v[3] >> 63) != 0;
+    bool eq = (t.v[3] == P3) & (t.v[2] == M64) & (t.v[1] == M64) & (t.v[0] >= P0);
+    return top | eq;
+}
+
+// The reference's "- p" loop (curve25519_ops.cu:62-66 / :137-141 / :232-237):
+//   diff = h_i - p_i - br;  br = h_i < lo64(p_i + br)
+// For p1 = p2 = 2^64-1 the sum p_i + br wraps to 0 when br = 1, dropping the borrow.
+// Closed form of the same four steps:
+BP_DEV fe fe_lossy_sub_p(const fe& t) {
+    fe d;
+    uint64_t br1 = t.v[0] < P0;
+    d.v[0] = t.v[0] + 19;                         // t0 - (2^64 - 19)
+    d.v[1] = t.v[1] + 1 - br1;                    // t1 - (2^64 - 1) - br1
+    uint64_t br2 = (br1 == 0) & (t.v[1] != M64);
+    d.v[2] = t.v[2] + 1 - br2;
+    uint64_t br3 = (br2 == 0) & (t.v[2] != M64);
+    d.v[3] = t.v[3] - P3 - br3;
+    return d;
+}
+
+BP_DEV fe fe_cond_sub_p(const fe& t, bool c) {
+    fe d = fe_lossy_sub_p(t);
+    fe r;
+#pragma unroll
+    for (int i = 0; i < 4; i++) r.v[i] = c ? d.v[i] : t.v[i];
+    return r;
+}
+
+// host fe25519_tobytes (curve25519_ops.cu:220-251) minus the byte store: canonicalising limbs.
+BP_DEV fe fe_canon(const fe& t) { return fe_cond_sub_p(t, fe_ge_p(t)); }
+
+// fe25519_add (curve25519_ops.cu:41-68): exact 257-bit sum, then one lossy "- p".
+BP_DEV fe fe_add(const fe& f, const fe& g) {
+    fe h;
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        uint64_t s = f.v[i] + g.v[i];
+        uint64_t c1 = s < f.v[i];
+        uint64_t s2 = s + c;
+        uint64_t c2 = s2 < s;
+        h.v[i] = s2;
+        c = c1 | c2;
+    }
+    return fe_cond_sub_p(h, (c != 0) | fe_ge_p(h));
+}
+
+// fe25519_sub (curve25519_ops.cu:71-90): borrow = f_i < lo64(g_i + borrow) (lossy),
+// then, on a final borrow, temp_i += lo64(p_i + carry); carry = temp_i < p_i.
+BP_DEV fe fe_sub(const fe& f, const fe& g) {
+    fe t;
+    uint64_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        uint64_t gb = g.v[i] + br;
+        t.v[i] = f.v[i] - g.v[i] - br;
+        br = f.v[i] < gb;
+    }
+    // "+ p" pass, literal form (p1 = p2 = 2^64-1: carry = temp != 2^64-1 there)
+    fe a;
+    a.v[0] = t.v[0] + P0;
+    uint64_t cy = a.v[0] < P0;
+    a.v[1] = t.v[1] + (M64 + cy);
+    cy = a.v[1] < M64;
+    a.v[2] = t.v[2] + (M64 + cy);
+    cy = a.v[2] < M64;
+    a.v[3] = t.v[3] + (P3 + cy);
+    fe r;
+#pragma unroll
+    for (int i = 0; i < 4; i++) r.v[i] = br ? a.v[i] : t.v[i];
+    return r;
+}
+
+// Fold of the exact 512-bit product (curve25519_ops.cu:114-145):
+//   c = lo64(t4*19); t0 += c; cy = t0 < c;
+//   c = lo64(t_{i+4}*19 + cy); t_i += c; cy = t_i < c   (i = 1..3)
+//   if (cy || t >= p) lossy "- p"
+BP_DEV fe fe_fold512(const uint64_t t[8]) {
+    fe h;
+    uint64_t c = t[4] * 19ull;
+    h.v[0] = t[0] + c;
+    uint64_t cy = h.v[0] < c;
+#pragma unroll
+    for (int i = 1; i < 4; i++) {
+        c = t[i + 4] * 19ull + cy;
+        h.v[i] = t[i] + c;
+        cy = h.v[i] < c;
+    }
+    return fe_cond_sub_p(h, (cy != 0) | fe_ge_p(h));
+}
+
+// Exact 256x256 -> 512-bit product, product scanning over 32-bit words with a
+// 96-bit column accumulator.
+BP_DEV void mul512(uint64_t t[8], const fe& f, const fe& g) {
+    uint32_t a[8], b[8], w[16];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        a[2 * i] = (uint32_t)f.v[i];
+        a[2 * i + 1] = (uint32_t)(f.v[i] >> 32);
+        b[2 * i] = (uint32_t)g.v[i];
+        b[2 * i + 1] = (uint32_t)(g.v[i] >> 32);
+    }
+    uint64_t acc = 0;
+    uint32_t c2 = 0;
+#pragma unroll
+    for (int k = 0; k < 15; k++) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            int j = k - i;
+            if (j < 0 || j > 7) continue;
+            uint64_t p = (uint64_t)a[i] * b[j];
+            acc += p;
+            c2 += acc < p;
+        }
+        w[k] = (uint32_t)acc;
+        acc = (acc >> 32) | ((uint64_t)c2 << 32);
+        c2 = 0;
+    }
+    w[15] = (uint32_t)acc;
+#pragma unroll
+    for (int i = 0; i < 8; i++) t[i] = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
+}
+
+// fe25519_mul (curve25519_ops.cu:93-146 == device_curve25519_ops.cuh:117-171)
+BP_DEV fe fe_mul(const fe& f, const fe& g) {
+    uint64_t t[8];
+    mul512(t, f, g);
+    return fe_fold512(t);
+}
+
+// fe25519_sq (curve25519_ops.cu:149) == mul(f, f): the same exact product.
+BP_DEV fe fe_sq(const fe& f) { return fe_mul(f, f); }
+
+// mul by 1 (device_curve25519_ops.cuh:260 with z_inv = 1): product has zero upper half,
+// the fold adds nothing, so it is the conditional lossy "- p".
+BP_DEV fe fe_mul_one(const fe& f) { return fe_canon(f); }
+
+// fe25519_invert (curve25519_ops.cu:157-207): the fixed 13-multiplication chain.
+// t2 = sq(f) at :198 equals t0's first value (:163), so it is reused (12 products).
+BP_DEV fe fe_invert(const fe& f) {
+    fe f2 = fe_sq(f);              // :163 t0 = f^2
+    fe t1 = fe_sq(f2);             // :166
+    t1 = fe_sq(t1);                // :169
+    t1 = fe_mul(t1, f);            // :172
+    fe t0 = fe_mul(t1, f2);        // :175
+    t1 = fe_sq(t0);                // :178
+    t1 = fe_sq(t1);                // :186
+    t1 = fe_sq(t1);                // :189
+    t1 = fe_sq(t1);                // :192
+    t1 = fe_mul(t1, t1);           // :195
+    fe t2 = fe_mul(f2, f);         // :198-199 (sq(f) reused)
+    return fe_mul(t1, t2);         // :200
+}
+
+BP_DEV bool fe_is_one(const fe& f) {
+    return (f.v[0] == 1) & (f.v[1] == 0) & (f.v[2] == 0) & (f.v[3] == 0);
+}
+
+BP_DEV bool fe_eq(const fe& a, const fe& b) {
+    return (a.v[0] == b.v[0]) & (a.v[1] == b.v[1]) & (a.v[2] == b.v[2]) & (a.v[3] == b.v[3]);
+}
+
+// The reference's "square" GPU kernel (cuda_field_ops.cu:147-216): carries between
+// limbs are dropped and 2*a_i*a_j is taken mod 2^128. It is not fe25519_sq;
+// reproduced for the cuda_batch_field_square entry point.
+BP_DEV fe fe_square_kernel_quirk(const fe& f) {
+    uint64_t t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        unsigned __int128 d = (unsigned __int128)f.v[i] * f.v[i];
+        t[2 * i] += (uint64_t)d;
+        if (2 * i + 1 < 8) t[2 * i + 1] += (uint64_t)(d >> 64);
+#pragma unroll
+        for (int j = i + 1; j < 4; j++) {
+            unsigned __int128 m = ((unsigned __int128)f.v[i] * f.v[j]) << 1;
+            t[i + j] += (uint64_t)m;
+            if (i + j + 1 < 8) t[i + j + 1] += (uint64_t)(m >> 64);
+        }
+    }
+    return fe_fold512(t);
+}
+
+BP_DEV uint32_t fe_bit(const fe& s, int i) { return (uint32_t)(s.v[i >> 6] >> (i & 63)) & 1u; }
+
+}  // namespace bp

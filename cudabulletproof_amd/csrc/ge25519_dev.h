@@ -1,0 +1,156 @@
+// ge25519_dev.h — gfx950 device point arithmetic reproducing the reference's "ge25519"
+// extended-coordinate operations bit for bit.
+//
+// Freedoms used (all bit-preserving):
+//  * the q-side terms (Y2-X2), (Y2+X2) of an add are computed once per fixed point;
+//  * a doubling add(r, r) computes (Y-X) and (Y+X) once and squares them (same exact
+//    product, so the same bits);
+//  * a scalar's leading zero bits only ever double the identity: that prefix is a
+//    table lookup (ident_doublings[k] = k doublings of (0,1,1,0)).
+#pragma once
+#include "fe25519_dev.h"
+
+namespace bp {
+
+struct ge {
+    fe X, Y, Z, T;
+};
+
+// q-side operands of ge25519_add: (Y-X), (Y+X), Z, T
+struct geq {
+    fe YmX, YpX, Z, T;
+};
+
+// curve25519_ops.cu:341-346 — LE bytes A3 78 59 13 ... 03 52 (this is d, used where 2d is meant)
+BP_DEV fe k_const() {
+    return fe{{0x75EB4DCA135978A3ull, 0x00700A4D4141D8ABull, 0x8CC740797779E898ull, 0x52036CEE2B6FFE73ull}};
+}
+
+BP_DEV ge ge_zero() { return ge{fe_set(0), fe_set(1), fe_set(1), fe_set(0)}; }   // curve25519_ops.cu:318
+
+BP_DEV geq ge_prep(const ge& q) {
+    return geq{fe_sub(q.Y, q.X), fe_add(q.Y, q.X), q.Z, q.T};
+}
+
+// ge25519_add (curve25519_ops.cu:326-378 == device_curve25519_ops.cuh:188-241)
+BP_DEV ge ge_add_q(const ge& p, const geq& q) {
+    fe A = fe_mul(fe_sub(p.Y, p.X), q.YmX);
+    fe B = fe_mul(fe_add(p.Y, p.X), q.YpX);
+    fe C = fe_mul(fe_mul(p.T, q.T), k_const());
+    fe D = fe_mul(p.Z, q.Z);
+    D = fe_add(D, D);
+    fe E = fe_sub(B, A);
+    fe F = fe_sub(D, C);
+    fe G = fe_add(D, C);
+    fe H = fe_add(B, A);
+    return ge{fe_mul(E, F), fe_mul(G, H), fe_mul(F, G), fe_mul(E, H)};
+}
+
+BP_DEV ge ge_add(const ge& p, const ge& q) { return ge_add_q(p, ge_prep(q)); }
+
+// add(p, p) (curve25519_ops.cu:406 / device .cuh:282)
+BP_DEV ge ge_dbl(const ge& p) {
+    fe A = fe_sq(fe_sub(p.Y, p.X));
+    fe B = fe_sq(fe_add(p.Y, p.X));
+    fe C = fe_mul(fe_sq(p.T), k_const());
+    fe D = fe_sq(p.Z);
+    D = fe_add(D, D);
+    fe E = fe_sub(B, A);
+    fe F = fe_sub(D, C);
+    fe G = fe_add(D, C);
+    fe H = fe_add(B, A);
+    return ge{fe_mul(E, F), fe_mul(G, H), fe_mul(F, G), fe_mul(E, H)};
+}
+
+// device_ge25519_normalize (device_curve25519_ops.cuh:243-270): z_inv = 1.
+BP_DEV ge ge_norm_dev(const ge& p) {
+    ge r;
+    r.X = fe_mul_one(p.X);
+    r.Y = fe_mul_one(p.Y);
+    r.Z = fe_set(1);
+    r.T = fe_mul(r.X, r.Y);
+    return r;
+}
+
+// ge25519_normalize (curve25519_ops.cu:574-605): keep the point when the canonical
+// bytes of Z are 1, else multiply by the 13-step "invert" of Z.
+BP_DEV ge ge_norm_host(const ge& p) {
+    if (fe_is_one(fe_canon(p.Z))) return p;
+    fe zi = fe_invert(p.Z);
+    ge r;
+    r.X = fe_mul(p.X, zi);
+    r.Y = fe_mul(p.Y, zi);
+    r.Z = fe_set(1);
+    r.T = fe_mul(r.X, r.Y);
+    return r;
+}
+
+BP_DEV int fe_clz256(const fe& s) {
+    if (s.v[3]) return __clzll(s.v[3]);
+    if (s.v[2]) return 64 + __clzll(s.v[2]);
+    if (s.v[1]) return 128 + __clzll(s.v[1]);
+    if (s.v[0]) return 192 + __clzll(s.v[0]);
+    return 256;
+}
+
+BP_DEV ge ld_ge(const ge* p) { return *p; }
+
+// ge25519_scalarmult (curve25519_ops.cu:397-415 == device .cuh:272-290) for a scalar
+// that is the same in every lane of the wave: the bit test is a scalar branch.
+// `s` holds the scalar's 256 bits (limb i = bytes 8i..8i+7, little-endian).
+// `dtab` = the identity-doubling table (257 points).
+BP_DEV ge sm_uniform(const fe& s_in, const ge& P, const ge* __restrict__ dtab) {
+    fe s;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)s_in.v[i]);
+        uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(s_in.v[i] >> 32));
+        s.v[i] = (uint64_t)lo | ((uint64_t)hi << 32);
+    }
+    int lz = fe_clz256(s);
+    ge r = ld_ge(&dtab[lz]);
+    if (lz == 256) return r;
+    geq q = ge_prep(P);
+    for (int i = 255 - lz; i >= 0; i--) {
+        r = ge_dbl(r);
+        if (fe_bit(s, i)) r = ge_add_q(r, q);
+    }
+    return r;
+}
+
+// Same function for a per-lane scalar: every iteration is one ge25519_add whose second
+// operand is either r itself (the doubling) or P, so no lane idles on the other's branch.
+BP_DEV ge sm_lane(const fe& s, const ge& P, const ge* __restrict__ dtab) {
+    int lz = fe_clz256(s);
+    ge r = ld_ge(&dtab[lz]);
+    geq qp = ge_prep(P);
+    int i = 255 - lz;          // next bit to consume
+    bool add_phase = false;    // false: next op doubles; true: next op adds P
+    while (i >= 0) {
+        geq q = add_phase ? qp : ge_prep(r);
+        r = ge_add_q(r, q);
+        if (add_phase) {
+            add_phase = false;
+            i--;
+        } else if (fe_bit(s, i)) {
+            add_phase = true;
+        } else {
+            i--;
+        }
+    }
+    return r;
+}
+
+// Wave-level dispatch: uniform scalar -> scalar-branch loop, else the per-lane loop.
+BP_DEV ge scalarmult(const fe& s, const ge& P, const ge* __restrict__ dtab) {
+    uint32_t same = 1;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        uint32_t lo = (uint32_t)s.v[i], hi = (uint32_t)(s.v[i] >> 32);
+        same &= (lo == __builtin_amdgcn_readfirstlane(lo)) & (hi == __builtin_amdgcn_readfirstlane(hi));
+    }
+    if (__all(same)) return sm_uniform(s, P, dtab);
+    return sm_lane(s, P, dtab);
+}
+
+}  // namespace bp

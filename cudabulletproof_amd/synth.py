@@ -1,0 +1,105 @@
+"""Deterministic synthetic inputs for the batched verify (bench.py) and the MSM microbench.
+
+Proof-shaped data only: random 255-bit coordinates and scalars from a seeded numpy
+generator, laid out in the flat wire format of include/cudabulletproof_hip.h.  Proofs
+follow the shape the reference prover emits after fix_inner_product_proof
+(bulletproof_range_proof.cu:198-235): a = [t], b = [1], c = t, so the <a,b> = c check
+(crv:146-158) passes and every verify runs the full fold.  Verify cost does not depend
+on whether a proof is "valid" beyond that check.
+
+Generator points follow complete_bulletproof_test.cu:33-109 (SHA-256 derived X, Y,
+Z = 1); their T = X*Y is computed on the GPU by the engine's own field multiply.
+"""
+import hashlib
+
+import numpy as np
+
+MASK63 = np.uint64(0x7FFFFFFFFFFFFFFF)
+
+
+def _le_limbs(b32):
+    return np.frombuffer(b32, dtype="<u8").astype(np.uint64)
+
+
+def base_points_xy(n, seed_byte):
+    """X, Y limbs of generate_deterministic_base_points (complete_bulletproof_test.cu:33-63)."""
+    seed = bytes([seed_byte]) + bytes(31)
+    pts = np.zeros((n, 16), np.uint64)
+    for i in range(n):
+        x = hashlib.sha256(seed + int(i).to_bytes(4, "big")).digest()
+        y = hashlib.sha256(x).digest()
+        pts[i, 0:4] = _le_limbs(x)
+        pts[i, 4:8] = _le_limbs(y)
+        pts[i, 8] = 1
+    return pts
+
+
+def gh_xy():
+    """X limbs of g, h (complete_bulletproof_test.cu:84-109): X = SHA256({3}/{4} || 0^31), Y = Z = 1."""
+    out = []
+    for sb in (3, 4):
+        p = np.zeros(16, np.uint64)
+        p[0:4] = _le_limbs(hashlib.sha256(bytes([sb]) + bytes(31)).digest())
+        p[4] = 1
+        p[8] = 1
+        out.append(p)
+    return out
+
+
+def fill_T(points, device):
+    """T = X*Y with the engine's fe25519_mul (in place on a numpy (k,16) array)."""
+    import torch
+    from . import field_op
+    pts = np.ascontiguousarray(points).reshape(-1, 16)
+    X = torch.from_numpy(np.ascontiguousarray(pts[:, 0:4]).view(np.int64)).to(device)
+    Y = torch.from_numpy(np.ascontiguousarray(pts[:, 4:8]).view(np.int64)).to(device)
+    T = torch.empty_like(X)
+    field_op("mul", T, X, Y)
+    torch.cuda.synchronize(device)
+    pts[:, 12:16] = T.cpu().numpy().view(np.uint64)
+    return pts
+
+
+def generators(n, device):
+    """G, H (n,16), g, h (16,) as numpy, T filled on the GPU."""
+    G = base_points_xy(n, 1)
+    H = base_points_xy(n, 2)
+    g, h = gh_xy()
+    allp = np.concatenate([G, H, g[None], h[None]])
+    allp = fill_T(allp, device)
+    return allp[:n], allp[n:2 * n], allp[2 * n], allp[2 * n + 1]
+
+
+def _rand_fe(rng, shape):
+    v = rng.integers(0, 2**64, size=shape + (4,), dtype=np.uint64)
+    v[..., 3] &= MASK63
+    return v
+
+
+def _rand_pt(rng, shape):
+    p = np.zeros(shape + (16,), np.uint64)
+    p[..., 0:4] = _rand_fe(rng, shape)
+    p[..., 4:8] = _rand_fe(rng, shape)
+    p[..., 8] = 1
+    p[..., 12:16] = _rand_fe(rng, shape)   # T is not read by the verify path
+    return p
+
+
+def proofs(count, n, seed=1):
+    """Synthetic proof batch (numpy dict in the flat wire format)."""
+    rng = np.random.default_rng(seed)
+    Lr = int(n).bit_length() - 1
+    t = _rand_fe(rng, (count,))
+    t[:, 3] &= np.uint64(0x3FFFFFFFFFFFFFFF)   # t < p, so <[t],[1]> = t canonically
+    one = np.zeros((count, 1, 4), np.uint64)
+    one[..., 0] = 1
+    return dict(
+        V=_rand_pt(rng, (count,)), A=_rand_pt(rng, (count,)), S=_rand_pt(rng, (count,)),
+        T1=_rand_pt(rng, (count,)), T2=_rand_pt(rng, (count,)), t=t, a=t[:, None, :].copy(), b=one,
+        c=t.copy(), x=_rand_fe(rng, (count,)), L=_rand_pt(rng, (count, Lr)), R=_rand_pt(rng, (count, Lr)))
+
+
+def msm_inputs(n, seed=5):
+    """MSM microbench inputs: points = random (X, Y, Z=1, T), scalars = 255-bit."""
+    rng = np.random.default_rng(seed)
+    return _rand_fe(rng, (n,)), _rand_pt(rng, (n,))

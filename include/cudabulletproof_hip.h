@@ -1,0 +1,147 @@
+/* cudabulletproof_hip.h — C ABI of libcudabulletproof_hip.so (MI355X / gfx950).
+ *
+ * Part 1 is the drop-in boundary: every entry point of the reference's
+ * cuda_bulletproof.h, same names, same argument meaning, same conventions
+ * (host pointers owned by the caller, synchronous, inputs never modified,
+ * length mismatch -> message on stderr and *result untouched / false,
+ * device errors -> message on stderr and exit(EXIT_FAILURE), as CUDA_CHECK does
+ * in cuda_bulletproof_kernels.cu:13-21).  The reference's bulletproof_range_proof.cu
+ * and complete_bulletproof_test.cu link against this library unchanged
+ * (INTEGRATION.md).
+ *
+ * Part 2 is additive: batched, device-resident entry points (flat wire format,
+ * explicit stream, error codes) used by the Python package and bench.py.
+ *
+ * The types are layout-identical to the reference's (curve25519_ops.h:15-25,
+ * bulletproof_vectors.h:8-17, :65-74, bulletproof_range_proof.h:7-18); when the
+ * reference headers are included first, theirs are used.
+ */
+#ifndef CUDABULLETPROOF_HIP_H
+#define CUDABULLETPROOF_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+#ifndef __cplusplus
+#include <stdbool.h>
+#endif
+
+#ifndef CURVE25519_OPS_H
+typedef struct { uint64_t limbs[4]; } fe25519;              /* curve25519_ops.h:15-17 */
+typedef struct { fe25519 X, Y, Z, T; } ge25519;              /* curve25519_ops.h:20-25 */
+#endif
+#ifndef BULLETPROOF_VECTORS_H
+typedef struct { fe25519* elements; size_t length; } FieldVector;   /* bulletproof_vectors.h:8-11 */
+typedef struct { ge25519* elements; size_t length; } PointVector;   /* bulletproof_vectors.h:14-17 */
+typedef struct {                                                    /* bulletproof_vectors.h:65-74 */
+    size_t n;
+    FieldVector a;
+    FieldVector b;
+    fe25519 c;
+    PointVector L;
+    PointVector R;
+    size_t L_len;
+    fe25519 x;
+} InnerProductProof;
+#endif
+#ifndef BULLETPROOF_RANGE_PROOF_H
+typedef struct {                                                    /* bulletproof_range_proof.h:7-18 */
+    ge25519 V, A, S, T1, T2;
+    fe25519 taux, mu, t;
+    InnerProductProof ip_proof;
+} RangeProof;
+#endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ===================================================================== Part 1: reference surface */
+
+/* cuda_bulletproof.h:13 (cuda_bulletproof_kernels.cu:62). result = canonical-tree sum of
+ * device-normalized scalar*point terms. */
+void cuda_point_vector_multi_scalar_mul(ge25519* result, const FieldVector* scalars, const PointVector* points);
+/* cuda_bulletproof.h:17 (cuda_bulletproof_kernels.cu:119): same result. */
+void cuda_point_vector_multi_scalar_mul_shared(ge25519* result, const FieldVector* scalars,
+                                               const PointVector* points);
+
+/* cuda_bulletproof.h:22 (cuda_inner_product.cu:97): the reference's GPU reduction order
+ * (n <= 512: block halving tree; n > 512: grid-stride + two trees). */
+void cuda_field_vector_inner_product(fe25519* result, const FieldVector* a, const FieldVector* b);
+/* cuda_bulletproof.h:26 (declared there, never defined with C linkage in the reference):
+ * the n <= 512 halving-tree order for any n. */
+void cuda_field_vector_inner_product_shared(fe25519* result, const FieldVector* a, const FieldVector* b);
+/* cuda_inner_product.cu:302 (extern "C", not in the reference header). */
+void cuda_batch_field_vector_inner_product(fe25519* results, const FieldVector* a_vectors,
+                                           const FieldVector* b_vectors, size_t num_vectors);
+
+/* cuda_bulletproof.h:31-46 (cuda_field_ops.cu:257, :293, :329, :374). */
+void cuda_batch_field_add(fe25519* results, const fe25519* a, const fe25519* b, size_t count);
+void cuda_batch_field_sub(fe25519* results, const fe25519* a, const fe25519* b, size_t count);
+void cuda_batch_field_mul(fe25519* results, const fe25519* a, const fe25519* b, size_t count);
+void cuda_batch_field_mul_karatsuba(fe25519* results, const fe25519* a, const fe25519* b, size_t count);
+/* reproduces field_square_kernel (cuda_field_ops.cu:147), which is NOT fe25519_sq */
+void cuda_batch_field_square(fe25519* results, const fe25519* inputs, size_t count);
+/* cuda_bulletproof.h:50 (cuda_field_ops.cu:405): the reference kernel races;
+ * this defines it as the host fe25519_invert chain applied elementwise. */
+void cuda_batch_field_invert(fe25519* results, const fe25519* inputs, size_t count);
+/* cuda_bulletproof.h:55 (cuda_field_ops.cu:533): limbwise u64 add, no carry, no reduction */
+void cuda_soa_field_add(fe25519* results, const fe25519* a, const fe25519* b, size_t count);
+
+/* cuda_bulletproof.h:61 (cuda_range_proof_verify.cu:82, notebook-only in the reference). */
+bool cuda_range_proof_verify(const RangeProof* proof, const ge25519* V, size_t n, const PointVector* G,
+                             const PointVector* H, const ge25519* g, const ge25519* h);
+/* cuda_bulletproof.h:72 (cuda_range_proof_verify.cu:130). */
+bool cuda_inner_product_verify(const InnerProductProof* proof, const ge25519* P, const PointVector* G,
+                               const PointVector* H, const ge25519* Q);
+
+/* cuda_bulletproof.h:81-84: declared but never defined by the reference; here they time the
+ * corresponding GPU path and print one line each. */
+void cuda_benchmark_multi_scalar_mul(int iterations, size_t vector_size);
+void cuda_benchmark_inner_product(int iterations, size_t vector_size);
+void cuda_benchmark_field_operations(int iterations, size_t batch_size);
+void cuda_benchmark_range_proof(int iterations, size_t bit_size);
+
+/* ===================================================================== Part 2: batched device API */
+
+/* Flat wire format of a batch of range proofs; every pointer is DEVICE memory.
+ * Per proof p: V[p], A[p], S[p], T1[p], T2[p], t[p], c[p], x[p]; a/b: ab_len entries
+ * at p*ab_len; L/R: L_len entries at p*L_len (L[0]/R[0] are never read, crv:180-205).
+ * taux and mu are not read by cuda_range_proof_verify and are not part of the batch. */
+typedef struct {
+    size_t count, n, ab_len, L_len;
+    const ge25519 *V, *A, *S, *T1, *T2;
+    const fe25519 *t, *a, *b, *c, *x;
+    const ge25519 *L, *R;
+} hipbp_proof_batch;
+
+typedef enum {
+    HIPBP_OK = 0,
+    HIPBP_ERR_ARG = 1,       /* unsupported shape / null pointer */
+    HIPBP_ERR_DEVICE = 2,    /* HIP runtime error (message via hipbp_last_error) */
+} hipbp_status;
+
+const char* hipbp_last_error(void);
+/* Number of HIP devices visible. */
+int hipbp_device_count(void);
+
+/* Batched cuda_range_proof_verify semantics. G/H: n generators, g/h: 1 point (device).
+ * ok[count] gets 1/0; P_out / check_out (nullable) get the IPA point P and the check point. */
+int hipbp_batch_range_proof_verify(const hipbp_proof_batch* batch, const ge25519* G, const ge25519* H,
+                                   const ge25519* g, const ge25519* h, uint8_t* ok, ge25519* P_out,
+                                   ge25519* check_out, void* stream);
+/* Batched cuda_inner_product_verify semantics; P[count] given (device). */
+int hipbp_batch_inner_product_verify(const hipbp_proof_batch* batch, const ge25519* P, const ge25519* G,
+                                     const ge25519* H, const ge25519* Q, uint8_t* ok, ge25519* check_out,
+                                     void* stream);
+/* Canonical-tree MSM on device buffers. */
+int hipbp_msm(ge25519* result, const fe25519* scalars, const ge25519* points, size_t n, void* stream);
+/* Elementwise device field ops: op 0 add, 1 sub, 2 mul, 3 square (reference kernel quirk),
+ * 4 SoA add (limbwise, no carry), 5 invert (host chain). */
+int hipbp_field_op(int op, fe25519* r, const fe25519* a, const fe25519* b, size_t count, void* stream);
+/* Wait for `stream`. */
+int hipbp_sync(void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

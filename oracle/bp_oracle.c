@@ -335,6 +335,64 @@ void orc_inner_product(orc_fe* r, const orc_fe* a, const orc_fe* b, size_t n) {
     *r = acc;
 }
 
+/* cuda_inner_product.cu:154-183 + :185-216: one block of nt = min(n,512) threads; products for
+ * t < nt, then halving tree from nt/2 with t + stride < n (elements >= nt are never read). */
+void orc_ip_gpu_shared(orc_fe* r, const orc_fe* a, const orc_fe* b, size_t n) {
+    size_t nt = n < 512 ? n : 512;
+    if (nt == 0) return;
+    orc_fe* s = (orc_fe*)malloc(nt * sizeof(orc_fe));
+    for (size_t t = 0; t < nt; t++) orc_fe_mul(&s[t], &a[t], &b[t]);
+    for (size_t st = nt / 2; st > 0; st >>= 1)
+        for (size_t t = 0; t < st; t++)
+            if (t + st < n) orc_fe_add(&s[t], &s[t], &s[t + st]);
+    *r = s[0];
+    free(s);
+}
+/* one 256-thread block of field_vector_inner_product_kernel (cuda_inner_product.cu:33-61) /
+ * batch_inner_product_kernel (:260-299, warp_tail): grid-stride fold from 0, tree over 256 slots */
+static void ip_block(orc_fe* out, const orc_fe* a, const orc_fe* b, size_t n, size_t blk, size_t grid_threads,
+                     int warp_tail) {
+    orc_fe s[256];
+    for (size_t t = 0; t < 256; t++) {
+        orc_fe acc, p;
+        fe_set(&acc, 0);
+        for (size_t idx = blk * 256 + t; idx < n; idx += grid_threads) {
+            orc_fe_mul(&p, &a[idx], &b[idx]);
+            orc_fe_add(&acc, &acc, &p);
+        }
+        s[t] = acc;
+    }
+    size_t stop = warp_tail ? 32 : 1;
+    for (size_t st = 128; st >= stop; st >>= 1)
+        for (size_t t = 0; t < st; t++) orc_fe_add(&s[t], &s[t], &s[t + st]);
+    if (warp_tail)
+        for (size_t st = 16; st >= 1; st >>= 1)
+            for (size_t t = 0; t < st; t++) orc_fe_add(&s[t], &s[t], &s[t + st]);
+    *out = s[0];
+}
+/* cuda_inner_product.cu:97-151: n <= 512 -> shared form; else grid of min(ceil(n/256),1024)
+ * blocks, then fe25519_reduce_kernel (:69-92) over at most 256 partials. */
+void orc_ip_gpu(orc_fe* r, const orc_fe* a, const orc_fe* b, size_t n) {
+    if (n <= 512) { orc_ip_gpu_shared(r, a, b, n); return; }
+    size_t nb = (n + 255) / 256;
+    if (nb > 1024) nb = 1024;
+    orc_fe part[1024], s[256];
+    for (size_t k = 0; k < nb; k++) ip_block(&part[k], a, b, n, k, nb * 256, 0);
+    for (size_t t = 0; t < 256; t++) { if (t < nb) s[t] = part[t]; else fe_set(&s[t], 0); }
+    for (size_t st = 128; st > 0; st >>= 1)
+        for (size_t t = 0; t < st; t++)
+            if (t + st < nb) orc_fe_add(&s[t], &s[t], &s[t + st]);
+    *r = s[0];
+}
+/* cuda_batch_field_vector_inner_product (cuda_inner_product.cu:302-347): per vector, the value
+ * x-block 0 writes (the other x-blocks race on the same slot when n > 256). */
+void orc_ip_gpu_batch(orc_fe* r, const orc_fe* a, const orc_fe* b, size_t n, size_t nvec) {
+    size_t nb = (n + 255) / 256;
+    if (nb > 1024) nb = 1024;
+    if (nb == 0) nb = 1;
+    for (size_t v = 0; v < nvec; v++) ip_block(&r[v], a + v * n, b + v * n, n, 0, nb * 256, 1);
+}
+
 /* ------------------------------------------------------------------ generators */
 /* complete_bulletproof_test.cu:33-63 */
 void orc_base_points(orc_ge* out, size_t n, const uint8_t seed32[32]) {

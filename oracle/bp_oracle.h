@@ -43,6 +43,9 @@ void orc_ge_normalize_dev(orc_ge* p);
 void orc_msm_canon(orc_ge* r, const orc_fe* s, const orc_ge* P, size_t n);   /* GPU MSM semantics (A9) */
 void orc_msm_cpu(orc_ge* r, const orc_fe* s, const orc_ge* P, size_t n);     /* vectors.cu:189 (A11) */
 void orc_inner_product(orc_fe* r, const orc_fe* a, const orc_fe* b, size_t n); /* vectors.cu:101 */
+void orc_ip_gpu(orc_fe* r, const orc_fe* a, const orc_fe* b, size_t n);        /* cuda_inner_product.cu:97 */
+void orc_ip_gpu_shared(orc_fe* r, const orc_fe* a, const orc_fe* b, size_t n); /* cuda_inner_product.cu:185 */
+void orc_ip_gpu_batch(orc_fe* r, const orc_fe* a, const orc_fe* b, size_t n, size_t nvec); /* :302 */
 
 /* hashing / transcript */
 void orc_sha256(uint8_t out[32], const uint8_t* data, size_t len);

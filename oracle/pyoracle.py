@@ -138,6 +138,20 @@ class Oracle(_Lib):
         self.f("inner_product")(_p(r), _p(a), _p(b), _sz(len(a)))
         return r
 
+    def ip_gpu(self, a, b, shared=False):
+        r = fe()
+        a = np.ascontiguousarray(a, np.uint64)
+        b = np.ascontiguousarray(b, np.uint64)
+        self.f("ip_gpu_shared" if shared else "ip_gpu")(_p(r), _p(a), _p(b), _sz(len(a)))
+        return r
+
+    def ip_gpu_batch(self, a, b):
+        a = np.ascontiguousarray(a, np.uint64)
+        b = np.ascontiguousarray(b, np.uint64)
+        r = fe(a.shape[0])
+        self.f("ip_gpu_batch")(_p(r), _p(a), _p(b), _sz(a.shape[1]), _sz(a.shape[0]))
+        return r
+
     def base_points(self, n, seed_byte):
         out = ge(n)
         seed = np.zeros(32, np.uint8)

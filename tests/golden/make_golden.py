@@ -1,0 +1,132 @@
+"""Generate the golden fixtures in tests/golden/ from the REFERENCE ITSELF.
+
+Run in the build container (needs /root/reference):  python tests/golden/make_golden.py
+It builds oracle/_ref/libbpref.so (the reference's host sources compiled in place by
+oracle/build_ref.sh) and records inputs + reference outputs as .npz (no pickles):
+
+  field.npz   edge-heavy pairs -> fe25519_add/sub/mul/invert/tobytes      (curve25519_ops.cu:41-251)
+  point.npz   ge25519_add, host/device normalize, scalarmult               (curve25519_ops.cu:326-605, .cuh:188-290)
+  msm.npz     canonical-tree GPU MSM semantics + CPU MSM, n in {1,2,3,5,16,17,64}
+  proofs_n16.npz / proofs_n64.npz
+              reference proofs (generate_range_proof, deterministic RAND), the verdicts of
+              cuda_range_proof_verify and range_proof_verify, P (calculate_inner_product_point),
+              the IPA fold trace and the check point (crv:160-279 composed from reference primitives)
+
+The survey's golden digests are reproduced by tests/test_oracle_golden.py.
+"""
+import hashlib
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+from oracle import pyoracle as po  # noqa: E402
+
+M = 2**64 - 1
+P = [0xFFFFFFFFFFFFFFED, M, M, 0x7FFFFFFFFFFFFFFF]
+EDGE = [0, 1, 2, 3, 19, 38, M, M - 1, M - 18, M - 19, M - 20, 2**63, 2**63 - 1, 2**63 + 1, 2**32, 2**32 - 1,
+        P[0] - 1, P[0] + 1]
+
+
+def edge_fe(rng, k):
+    out = np.zeros((k, 4), np.uint64)
+    for i in range(k):
+        mode = rng.integers(0, 4)
+        for j in range(4):
+            if mode == 0 or rng.random() < 0.3:
+                out[i, j] = np.uint64(int(rng.integers(0, 2**63)) * 2 + int(rng.integers(0, 2)))
+            else:
+                out[i, j] = np.uint64(EDGE[rng.integers(0, len(EDGE))])
+    # a few exact multiples/near-multiples of p
+    special = [P, [P[0] + 1, M, M, P[3]], [M, M, M, M], [P[0] - 1, M, M, P[3]]]
+    for i in range(min(k, len(special)) if k >= 8 else 0):
+        out[i] = special[i]
+    return out
+
+
+def main():
+    po.build()
+    R = po.Reference()
+    rng = np.random.default_rng(20251015)
+
+    # ---------------------------------------------------------------- field
+    k = 256
+    f, g = edge_fe(rng, k), edge_fe(rng, k)
+    res = {n: np.zeros((k, 4), np.uint64) for n in ("add", "sub", "mul", "invert")}
+    tob = np.zeros((k, 32), np.uint8)
+    for i in range(k):
+        res["add"][i] = R.fe_op("fe_add", f[i], g[i])
+        res["sub"][i] = R.fe_op("fe_sub", f[i], g[i])
+        res["mul"][i] = R.fe_op("fe_mul", f[i], g[i])
+        res["invert"][i] = R.fe_op("fe_invert", f[i])
+        tob[i] = R.fe_tobytes(f[i])
+    np.savez_compressed(os.path.join(HERE, "field.npz"), f=f, g=g, tobytes=tob, **res)
+
+    # ---------------------------------------------------------------- points
+    kp = 48
+    p = np.concatenate([edge_fe(rng, kp), edge_fe(rng, kp), edge_fe(rng, kp), edge_fe(rng, kp)], axis=1)
+    q = np.concatenate([edge_fe(rng, kp), edge_fe(rng, kp), edge_fe(rng, kp), edge_fe(rng, kp)], axis=1)
+    base = R.base_points(8, 9)
+    p[:8] = base
+    add = np.stack([R.ge_op("ge_add", p[i], q[i]) for i in range(kp)])
+    nh = np.stack([R.ge_normalize("ge_normalize", p[i]) for i in range(kp)])
+    nd = np.stack([R.ge_normalize("dev_ge_normalize", p[i]) for i in range(kp)])
+    ks = 12
+    sc = rng.integers(0, 256, size=(ks, 32)).astype(np.uint8)
+    sc[0] = 0
+    sc[1] = 0
+    sc[1, 0] = 1
+    sc[2] = 255
+    sc[3] = 0
+    sc[3, 5] = 42
+    sm = np.stack([R.ge_op("ge_scalarmult", sc[i], p[i]) for i in range(ks)])
+    np.savez_compressed(os.path.join(HERE, "point.npz"), p=p, q=q, add=add, norm_host=nh, norm_dev=nd,
+                        scalars=sc, scalarmult=sm)
+
+    # ---------------------------------------------------------------- MSM
+    out = {}
+    for n in (1, 2, 3, 5, 16, 17, 64):
+        Pn = R.base_points(n, 5)
+        s = edge_fe(rng, n) if n != 64 else np.stack(
+            [np.frombuffer(hashlib.sha256(b"msm-s" + i.to_bytes(4, "little")).digest(), "<u8") for i in range(n)])
+        if n == 64:
+            s = s.astype(np.uint64)
+            s[:, 3] &= np.uint64(0x7FFFFFFFFFFFFFFF)
+        out[f"P{n}"] = Pn
+        out[f"s{n}"] = s
+        out[f"canon{n}"] = R.msm("msm_canon", s, Pn)
+        out[f"cpu{n}"] = R.msm("msm_cpu", s, Pn)
+    np.savez_compressed(os.path.join(HERE, "msm.npz"), **out)
+
+    # ---------------------------------------------------------------- proofs
+    for n in (16, 64):
+        G, H = R.base_points(n, 1), R.base_points(n, 2)
+        g, h = R.gh()
+        recs = dict(G=G, H=H, g=g, h=h)
+        heads, Vs, As, Bs, Ls, Rs, oks, okc, Ps, chks, Gts, Hts, vals = ([] for _ in range(13))
+        for seed in range(1, 7):
+            val = np.zeros(32, np.uint8)
+            if seed == 1:
+                val[0] = 42                      # complete_bulletproof_test.cu:116
+            else:
+                val[:n // 8] = rng.integers(0, 256, n // 8)
+            pr = R.prove(seed, val, n, G, H, g, h)
+            hd = po.head_fields(pr["head"])
+            Pr, _ = R.verify_P(pr, n, G, H, g, h)
+            Gt, Ht, chk = R.ipa_fold(G, H, n, hd["x"], pr["L"], pr["R"], pr["a"][0], pr["b"][0], hd["c"], h)
+            heads.append(pr["head"]); Vs.append(pr["V"]); As.append(pr["a"]); Bs.append(pr["b"])
+            Ls.append(pr["L"]); Rs.append(pr["R"]); vals.append(val)
+            oks.append(R.cuda_range_proof_verify(pr, n, G, H, g, h))
+            okc.append(R.range_proof_verify(pr, n, G, H, g, h))
+            Ps.append(Pr); chks.append(chk); Gts.append(Gt); Hts.append(Ht)
+        np.savez_compressed(os.path.join(HERE, f"proofs_n{n}.npz"), **recs, head=np.stack(heads), V=np.stack(Vs),
+                            a=np.stack(As), b=np.stack(Bs), L=np.stack(Ls), R=np.stack(Rs), value=np.stack(vals),
+                            ok_cuda=np.array(oks), ok_cpu=np.array(okc), P=np.stack(Ps), check=np.stack(chks),
+                            Gtrace=np.stack(Gts), Htrace=np.stack(Hts))
+    print("fixtures written to", HERE)
+
+
+if __name__ == "__main__":
+    main()

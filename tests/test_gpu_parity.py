@@ -1,0 +1,196 @@
+"""GPU parity: libcudabulletproof_hip.so (gfx950 kernels) against the reference's own outputs
+(tests/golden/, produced by make_golden.py from the reference build) and against the CPU
+restatement (oracle/) on seeded inputs.  Everything is bit-exact: this is integer arithmetic.
+Run on the GPU box: python -m pytest tests -m gpu -q
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def d8(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()[:16]
+
+
+def rand_fe(rng, k, top=True):
+    v = rng.integers(0, 2**64, size=(k, 4), dtype=np.uint64)
+    if not top:
+        v[:, 3] &= np.uint64(0x7FFFFFFFFFFFFFFF)
+    return v
+
+
+# ----------------------------------------------------------------------------- field ops
+def test_field_ops_match_reference(bp, golden):
+    d = golden("field")
+    assert np.array_equal(bp.cuda_batch_field_add(d["f"], d["g"]), d["add"])
+    assert np.array_equal(bp.cuda_batch_field_sub(d["f"], d["g"]), d["sub"])
+    assert np.array_equal(bp.cuda_batch_field_mul(d["f"], d["g"]), d["mul"])
+    assert np.array_equal(bp.cuda_batch_field_mul_karatsuba(d["f"], d["g"]), d["mul"])
+    assert np.array_equal(bp.cuda_batch_field_invert(d["f"]), d["invert"])
+
+
+def test_field_ops_random_vs_oracle(bp, oracle):
+    rng = np.random.default_rng(7)
+    f, g = rand_fe(rng, 4096), rand_fe(rng, 4096)
+    add, sub, mul = bp.cuda_batch_field_add(f, g), bp.cuda_batch_field_sub(f, g), bp.cuda_batch_field_mul(f, g)
+    sq = bp.cuda_batch_field_square(f)
+    soa = bp.cuda_soa_field_add(f, g)
+    for i in range(0, 4096, 7):
+        assert np.array_equal(add[i], oracle.fe_add(f[i], g[i])), i
+        assert np.array_equal(sub[i], oracle.fe_sub(f[i], g[i])), i
+        assert np.array_equal(mul[i], oracle.fe_mul(f[i], g[i])), i
+        assert np.array_equal(sq[i], oracle.fe_square_kernel(f[i])), i
+    assert np.array_equal(soa, f + g)   # limbwise u64 add, wraps, no carry (cuda_field_ops.cu:521)
+
+
+def test_field_ops_empty(bp):
+    z = np.zeros((0, 4), np.uint64)
+    assert bp.cuda_batch_field_add(z, z).shape == (0, 4)
+
+
+# ----------------------------------------------------------------------------- MSM
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 16, 17, 64])
+def test_msm_matches_reference(bp, golden, n):
+    d = golden("msm")
+    assert np.array_equal(bp.cuda_point_vector_multi_scalar_mul(d[f"s{n}"], d[f"P{n}"]), d[f"canon{n}"])
+
+
+@pytest.mark.parametrize("n", [255, 256, 257, 700])
+def test_msm_multiblock_vs_oracle(bp, oracle, n):
+    rng = np.random.default_rng(n)
+    P = oracle.base_points(n, 11)
+    s = rand_fe(rng, n)
+    s[::5] = 0                                   # zero scalars: 256 doublings of the identity
+    s[1::7, 1:] = 0                              # short scalars: long leading-zero runs
+    assert np.array_equal(bp.cuda_point_vector_multi_scalar_mul(s, P), oracle.msm_canon(s, P))
+
+
+def test_msm_4096_survey_digest(bp, oracle):
+    # n = 4096, points = base_points({5}), scalars = SHA256("msm-s"||i_le32), bit 255 cleared
+    n = 4096
+    P = oracle.base_points(n, 5)
+    s = np.stack([np.frombuffer(hashlib.sha256(b"msm-s" + i.to_bytes(4, "little")).digest(), "<u8")
+                  for i in range(n)]).astype(np.uint64)
+    s[:, 3] &= np.uint64(0x7FFFFFFFFFFFFFFF)
+    assert d8(bp.cuda_point_vector_multi_scalar_mul(s, P)) == "17b524ff179c621d"
+
+
+def test_msm_length_mismatch_leaves_result(bp, capfd):
+    import ctypes
+    s = np.zeros((3, 4), np.uint64)
+    P = np.zeros((2, 16), np.uint64)
+    out = np.full(16, 7, np.uint64)
+    sv = bp.FieldVector(s.ctypes.data, 3)
+    pv = bp.PointVector(P.ctypes.data, 2)
+    bp.lib().cuda_point_vector_multi_scalar_mul(ctypes.c_void_p(out.ctypes.data), ctypes.byref(sv), ctypes.byref(pv))
+    assert (out == 7).all()
+    assert "Vector lengths must match" in capfd.readouterr().err
+
+
+# ----------------------------------------------------------------------------- inner products
+@pytest.mark.parametrize("n", [1, 3, 16, 100, 512, 513, 4096, 70000])
+def test_field_inner_product_orders(bp, oracle, n):
+    rng = np.random.default_rng(n)
+    a, b = rand_fe(rng, n), rand_fe(rng, n)
+    assert np.array_equal(bp.cuda_field_vector_inner_product(a, b), oracle.ip_gpu(a, b))
+    if n <= 1024:
+        assert np.array_equal(bp.cuda_field_vector_inner_product(a, b, shared=True), oracle.ip_gpu(a, b, shared=True))
+
+
+@pytest.mark.parametrize("n", [1, 64, 300])
+def test_batch_field_inner_product(bp, oracle, n):
+    rng = np.random.default_rng(3)
+    a, b = rand_fe(rng, 5 * n).reshape(5, n, 4), rand_fe(rng, 5 * n).reshape(5, n, 4)
+    assert np.array_equal(bp.cuda_batch_field_vector_inner_product(a, b), oracle.ip_gpu_batch(a, b))
+
+
+# ----------------------------------------------------------------------------- verify
+def _proof(d, i):
+    return dict(head=d["head"][i], a=d["a"][i], b=d["b"][i], L=d["L"][i], R=d["R"][i])
+
+
+@pytest.mark.parametrize("n", [16, 64])
+def test_single_verify_matches_reference(bp, golden, n):
+    d = golden(f"proofs_n{n}")
+    for i in range(len(d["head"])):
+        ok = bp.cuda_range_proof_verify(_proof(d, i), d["V"][i], n, d["G"], d["H"], d["g"], d["h"])
+        assert ok == bool(d["ok_cuda"][i]), i
+        ok2 = bp.cuda_inner_product_verify(_proof(d, i), d["P"][i], d["G"], d["H"], d["h"])
+        assert ok2 == bool(d["ok_cuda"][i]), i
+
+
+def _batch_from_golden(bp, d, device):
+    from oracle.pyoracle import head_fields
+    hs = [head_fields(h) for h in d["head"]]
+    arrays = dict(V=d["V"], A=np.stack([h["A"] for h in hs]), S=np.stack([h["S"] for h in hs]),
+                  T1=np.stack([h["T1"] for h in hs]), T2=np.stack([h["T2"] for h in hs]),
+                  t=np.stack([h["t"] for h in hs]), a=d["a"], b=d["b"], c=np.stack([h["c"] for h in hs]),
+                  x=np.stack([h["x"] for h in hs]), L=d["L"], R=d["R"])
+    return arrays
+
+
+def _run_batch(bp, n, arrays, G, H, g, h):
+    import torch
+    dev = torch.device("cuda:0")
+    batch = bp.RangeProofBatch.from_numpy(n, arrays, dev)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    B = batch.count
+    ok = torch.zeros(B, dtype=torch.uint8, device=dev)
+    P = torch.zeros(B, 16, dtype=torch.int64, device=dev)
+    chk = torch.zeros(B, 16, dtype=torch.int64, device=dev)
+    bp.batch_range_proof_verify(batch, T(G), T(H), T(g), T(h), ok, P, chk)
+    torch.cuda.synchronize()
+    return ok.cpu().numpy().astype(bool), P.cpu().numpy().view(np.uint64), chk.cpu().numpy().view(np.uint64)
+
+
+@pytest.mark.parametrize("n", [16, 64])
+def test_batch_verify_matches_reference(bp, golden, n):
+    d = golden(f"proofs_n{n}")
+    ok, P, chk = _run_batch(bp, n, _batch_from_golden(bp, d, None), d["G"], d["H"], d["g"], d["h"])
+    assert np.array_equal(ok, d["ok_cuda"].astype(bool))
+    assert np.array_equal(P, d["P"])
+    assert np.array_equal(chk, d["check"])
+
+
+@pytest.mark.parametrize("n,B,ab_len", [(64, 48, 1), (16, 40, 3), (4, 17, 2), (1, 9, 1), (256, 4, 1)])
+def test_batch_verify_synthetic_vs_oracle(bp, oracle, n, B, ab_len):
+    from cudabulletproof_amd import synth
+    arrays = synth.proofs(B, n, seed=1000 + n)
+    rng = np.random.default_rng(n + B)
+    if ab_len > 1:
+        arrays["a"] = rand_fe(rng, B * ab_len).reshape(B, ab_len, 4)
+        arrays["b"] = rand_fe(rng, B * ab_len).reshape(B, ab_len, 4)
+        for p in range(B):   # make <a,b> = c for most proofs, leave a few failing
+            if p % 5:
+                arrays["c"][p] = oracle.inner_product(arrays["a"][p], arrays["b"][p])
+    arrays["c"][2] = rand_fe(rng, 1)[0]          # a <a,b> != c proof (crv:153 early reject)
+    arrays["t"][3] = 0                          # t = 0: 256 doublings of the identity
+    G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+    g, h = oracle.gh()
+    ok, P, chk = _run_batch(bp, n, arrays, G, H, g, h)
+    head_keys = ("V", "A", "S", "T1", "T2")
+    for p in range(B):
+        head = np.concatenate([arrays[k][p] for k in head_keys] +
+                              [np.zeros(4, np.uint64), np.zeros(4, np.uint64), arrays["t"][p], arrays["c"][p],
+                               arrays["x"][p]])
+        okr, Pr, chkr, _, _ = oracle.cuda_range_proof_verify(head, arrays["V"][p], n, arrays["a"][p], arrays["b"][p],
+                                                             arrays["L"][p], arrays["R"][p], G, H, g, h)
+        assert ok[p] == okr, p
+        assert np.array_equal(P[p], Pr), p
+        if okr or not np.array_equal(chkr, np.zeros(16, np.uint64)):
+            assert np.array_equal(chk[p], chkr), p
+
+
+def test_batch_verify_deterministic(bp, oracle):
+    from cudabulletproof_amd import synth
+    n = 64
+    arrays = synth.proofs(96, n, seed=5)
+    G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+    g, h = oracle.gh()
+    r1 = _run_batch(bp, n, arrays, G, H, g, h)
+    r2 = _run_batch(bp, n, arrays, G, H, g, h)
+    for x, y in zip(r1, r2):
+        assert np.array_equal(x, y)

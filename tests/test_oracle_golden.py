@@ -1,0 +1,84 @@
+"""The CPU restatement (oracle/bp_oracle.c) against fixtures produced by the reference's own
+code (tests/golden/make_golden.py) and against the survey's golden digests."""
+import hashlib
+
+import numpy as np
+import pytest
+
+
+def d8(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()[:16]
+
+
+def test_sha256_kats(oracle):
+    # FIPS 180-4 examples
+    assert oracle.sha256(b"abc").hex() == "ba7816bf8f01cfea414140de5dae2223b00361a396177a9cb410ff61f20015ad"
+    assert oracle.sha256(b"").hex() == "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855"
+    m = b"abcdbcdecdefdefgefghfghighijhijkijkljklmklmnlmnomnopnopq"
+    assert oracle.sha256(m).hex() == "248d6a61d20638b8e5c026930c3e6039a33ce45964ff2167f6ecedd419db06c1"
+    for n in (55, 56, 63, 64, 65, 119, 120, 200):
+        data = bytes(range(256))[:n] * 1
+        assert oracle.sha256(data) == hashlib.sha256(data).digest()
+
+
+def test_field_against_reference(oracle, golden):
+    d = golden("field")
+    for i in range(len(d["f"])):
+        f, g = d["f"][i], d["g"][i]
+        assert np.array_equal(oracle.fe_add(f, g), d["add"][i]), i
+        assert np.array_equal(oracle.fe_sub(f, g), d["sub"][i]), i
+        assert np.array_equal(oracle.fe_mul(f, g), d["mul"][i]), i
+        assert np.array_equal(oracle.fe_invert(f), d["invert"][i]), i
+        assert np.array_equal(oracle.fe_tobytes(f), d["tobytes"][i]), i
+
+
+def test_points_against_reference(oracle, golden):
+    d = golden("point")
+    for i in range(len(d["p"])):
+        assert np.array_equal(oracle.ge_add(d["p"][i], d["q"][i]), d["add"][i]), i
+        assert np.array_equal(oracle.ge_normalize_host(d["p"][i]), d["norm_host"][i]), i
+        assert np.array_equal(oracle.ge_normalize_dev(d["p"][i]), d["norm_dev"][i]), i
+    for i in range(len(d["scalars"])):
+        assert np.array_equal(oracle.ge_scalarmult(d["scalars"][i], d["p"][i]), d["scalarmult"][i]), i
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 16, 17, 64])
+def test_msm_against_reference(oracle, golden, n):
+    d = golden("msm")
+    assert np.array_equal(oracle.base_points(n, 5), d[f"P{n}"])
+    assert np.array_equal(oracle.msm_canon(d[f"s{n}"], d[f"P{n}"]), d[f"canon{n}"])
+    assert np.array_equal(oracle.msm_cpu(d[f"s{n}"], d[f"P{n}"]), d[f"cpu{n}"])
+
+
+def test_survey_msm_digest(golden):
+    # CanonTree MSM, points = base_points({5}), scalars = SHA256("msm-s"||i_le32) & bit255 cleared
+    assert d8(golden("msm")["canon64"]) == "598ae9071d3bcf3a"
+
+
+@pytest.mark.parametrize("n", [16, 64])
+def test_verify_against_reference(oracle, golden, n):
+    d = golden(f"proofs_n{n}")
+    g2, h2 = oracle.gh()
+    assert np.array_equal(g2, d["g"]) and np.array_equal(h2, d["h"])
+    assert np.array_equal(oracle.base_points(n, 1), d["G"])
+    for i in range(len(d["head"])):
+        ok, P, chk, Gt, Ht = oracle.cuda_range_proof_verify(d["head"][i], d["V"][i], n, d["a"][i], d["b"][i], d["L"][i],
+                                                            d["R"][i], d["G"], d["H"], d["g"], d["h"], trace=True)
+        assert ok == bool(d["ok_cuda"][i]), i
+        assert np.array_equal(P, d["P"][i]), i
+        assert np.array_equal(chk, d["check"][i]), i
+        assert np.array_equal(Gt, d["Gtrace"][i]) and np.array_equal(Ht, d["Htrace"][i]), i
+
+
+def test_survey_proof_digests(golden):
+    # SURVEY §8c golden digests (value = 42, seed 1)
+    want = {16: ("96717c3978dc902a", "4567008fd60d9d07", "77bcc99376c5d8d0", "282f1a5824b8a457", "530e71ac9cbe3f9f"),
+            64: ("96717c3978dc902a", "932119f12a0f5fa8", "8f64d8d9593c262b", "6df943dcd1bf5609", "ca6627284303a25d")}
+    for n, (V, A, t, P, L) in want.items():
+        d = golden(f"proofs_n{n}")
+        head = d["head"][0]
+        assert d8(d["V"][0]) == V
+        assert d8(head[16:32]) == A
+        assert d8(head[88:92]) == t
+        assert d8(d["P"][0]) == P
+        assert d8(d["L"][0]) == L
