@@ -1,0 +1,225 @@
+"""bench.py — batched 64-bit range-proof verification on MI355X (BASELINE.json metric).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--n 64]
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+      --master-port P bench.py --gpus N --steps K --warmup W
+
+One step = cuda_range_proof_verify semantics (crv:82) over one batch of B = 1024 synthetic
+64-bit proofs already resident in HBM (BASELINE configs[1]); every rank verifies its own
+batches (weak scaling, no data-path collective: proofs are independent).  K steps are timed
+between barrier + synchronize on both sides; the max over ranks is the step time.
+
+Extra fields on the JSON line:
+  roofline     the dominant kernel's algorithmic bytes / HIP-event launch time vs HBM peak
+               (the path is VALU-integer bound), PMC traffic when profiled;
+  cpu_baseline the CPU restatement (oracle/, test infrastructure) on a bounded sample, 1 thread;
+  msm          2^20-point canonical-tree MSM points/s (BASELINE configs[2], per-point semantics).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+FE_B, GE_B = 32, 128
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=1024, help="proofs per step per GPU")
+    ap.add_argument("--n", type=int, default=64, help="range bits")
+    ap.add_argument("--msm-log2", type=int, default=20)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-msm", action="store_true")
+    return ap.parse_args()
+
+
+def alg_bytes(kernel, B, n, ab_len):
+    """Algorithmic HBM bytes of one launch-set of `kernel` over a batch (inputs read + outputs written)."""
+    Lr = n.bit_length() - 1
+    folds = sum(4 * (n >> (r + 1)) for r in range(Lr))            # scalar-mult tasks over all rounds
+    if kernel == "k_fold_terms":
+        return B * folds * (GE_B + FE_B + GE_B)                     # point + scalar in, term out
+    if kernel == "k_verify_msm_points":
+        return B * 2 * n * (GE_B + FE_B + GE_B)
+    return None
+
+
+def proof_bytes(n, ab_len):
+    Lr = n.bit_length() - 1
+    return 5 * GE_B + 3 * FE_B + 2 * ab_len * FE_B + 2 * Lr * GE_B   # V,A,S,T1,T2, t,c,x, a,b, L,R
+
+
+def cpu_baseline(n, seconds):
+    """The CPU restatement (oracle/, test infrastructure) verifying synthetic proofs, 1 thread."""
+    from cudabulletproof_amd import synth
+    from oracle import pyoracle
+    O = pyoracle.Oracle()
+    G, H = O.base_points(n, 1), O.base_points(n, 2)
+    g, h = O.gh()
+    s = synth.proofs(64, n, seed=777)
+    done, t0 = 0, time.perf_counter()
+    while done < 64:
+        p = done
+        head = np.concatenate([s[k][p] for k in ("V", "A", "S", "T1", "T2")] +
+                              [np.zeros(8, np.uint64), s["t"][p], s["c"][p], s["x"][p]])
+        O.cuda_range_proof_verify(head, s["V"][p], n, s["a"][p], s["b"][p], s["L"][p], s["R"][p], G, H, g, h)
+        done += 1
+        if time.perf_counter() - t0 > seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "verifies/s", "cores": 1, "kind": "port",
+            "sample": f"{done} synthetic {n}-bit proofs, cuda_range_proof_verify semantics, oracle/bp_oracle.c, "
+                      f"1 thread, {dt:.1f} s", "cpu": cpu_model()}
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def pmc_traffic(kernel):
+    """Per-launch HBM bytes for `kernel` from the committed rocprofv3 PMC summary, if present."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+        return d.get(kernel, {}).get("bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import cudabulletproof_amd as bp
+    from cudabulletproof_amd import synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    bp.lib()
+    bp.require_gpu()
+
+    B, n = args.batch, args.n
+    G, H, g, h = synth.generators(n, dev)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)
+    Gd, Hd, gd, hd = T(G), T(H), T(g), T(h)
+    nb = 4
+    batches = [bp.RangeProofBatch.from_numpy(n, synth.proofs(B, n, seed=1 + 1000 * rank + i), dev) for i in range(nb)]
+    ok = torch.zeros(B, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step(k):
+        bp.batch_range_proof_verify(batches[k % nb], Gd, Hd, gd, hd, ok, stream=stream)
+
+    for k in range(args.warmup):
+        step(k)
+    torch.cuda.synchronize(dev)
+    passes_warm = int(ok.sum().item())
+
+    bp.timing_enable(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(k)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    stats = bp.timing_collect()
+    bp.timing_enable(False)
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        c = torch.tensor([passes_warm], dtype=torch.int64, device=dev)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        passes_warm = int(c.item())
+
+    total = B * args.steps * world
+    value = total / dt
+
+    # dominant kernel + live roofline (HIP events on the verify stream)
+    kern_ms = {k: v[0] for k, v in stats.items() if v[1]}
+    dom = max(kern_ms, key=kern_ms.get)
+    launches = stats[dom][1]
+    avg_ms = stats[dom][0] / launches
+    ab_batch = alg_bytes(dom, B, n, 1)
+    per_launch = ab_batch * args.steps / launches if ab_batch else None
+    achieved = (per_launch / (avg_ms * 1e-3)) / 1e9 if per_launch else None
+    Lr = n.bit_length() - 1
+    sm_per_verify = 2 * n + 2 + sum(4 * (n >> (r + 1)) for r in range(Lr)) + 2
+    roofline = {
+        "bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": pmc_traffic(dom),
+        "avg_launch_ms": avg_ms, "launches": launches,
+        "kernel_ms_share": {k: round(v / sum(kern_ms.values()), 4) for k, v in kern_ms.items()},
+        "binding": "VALU integer (not HBM, not MFMA): see DESIGN.md",
+        "scalar_mults_per_s": value * sm_per_verify,
+    }
+
+    msm = None
+    if not args.no_msm and rank == 0:
+        nm = 1 << args.msm_log2
+        sc, pts = synth.msm_inputs(nm)
+        scd, ptd = T(sc), T(pts)
+        res = torch.zeros(16, dtype=torch.int64, device=dev)
+        bp.msm(res, scd, ptd, stream=stream)
+        torch.cuda.synchronize(dev)
+        reps = 3
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            bp.msm(res, scd, ptd, stream=stream)
+        torch.cuda.synchronize(dev)
+        mdt = (time.perf_counter() - t1) / reps
+        msm = {"metric": "MSM points/sec", "value": nm / mdt, "unit": "points/s", "points": nm,
+               "ms_per_msm": mdt * 1e3, "semantics": "canonical-tree per-point double-and-add (SURVEY A9)"}
+
+    cpu = None
+    if not args.no_cpu and rank == 0 and world == 1:
+        cpu = cpu_baseline(n, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": "64-bit range-proof verifies/sec (batched)", "value": value, "unit": "verifies/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+            "data": "synthetic (seeded proof-shaped inputs, a=[t], b=[1], c=t; generators per "
+                    "complete_bulletproof_test.cu:33-109)",
+            "config": {"workload": f"batch {B} x {n}-bit range-proof verify per GPU (BASELINE configs[1])",
+                       "batch_per_gpu": B, "n": n, "semantics": "cuda_range_proof_verify (crv:82)",
+                       "parallelism": f"independent proof shards x{world}",
+                       "proof_bytes": proof_bytes(n, 1), "passes_in_warmup_batch": passes_warm},
+            "roofline": roofline, "cpu_baseline": cpu, "msm": msm,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -87,7 +87,8 @@ EXPORTS = [
     "cuda_batch_field_invert", "cuda_soa_field_add", "cuda_range_proof_verify", "cuda_inner_product_verify",
     "cuda_benchmark_multi_scalar_mul", "cuda_benchmark_inner_product", "cuda_benchmark_field_operations",
     "cuda_benchmark_range_proof", "hipbp_last_error", "hipbp_device_count", "hipbp_batch_range_proof_verify",
-    "hipbp_batch_inner_product_verify", "hipbp_msm", "hipbp_field_op", "hipbp_sync",
+    "hipbp_batch_inner_product_verify", "hipbp_msm", "hipbp_field_op", "hipbp_sync", "hipbp_timing_enable",
+    "hipbp_timing_collect", "hipbp_kernel_count", "hipbp_kernel_name",
 ]
 
 
@@ -332,3 +333,23 @@ def field_op(op, r, a, b=None, stream=None):
     ops = {"add": 0, "sub": 1, "mul": 2, "square": 3, "soa_add": 4, "invert": 5}
     _chk(lib().hipbp_field_op(ops[op], _c(r.data_ptr()), _c(a.data_ptr()), _c(b.data_ptr()) if b is not None else None,
                               _sz(a.shape[0]), _stream_ptr(stream)))
+
+
+# ====================================================================== per-kernel timing
+def timing_enable(on=True):
+    """Record HIP events around each verify-pipeline kernel launch (resets the totals)."""
+    L = lib()
+    L.hipbp_timing_enable.restype = ctypes.c_int
+    _chk(L.hipbp_timing_enable(1 if on else 0))
+
+
+def timing_collect():
+    """{kernel_name: (total_ms, launches)} accumulated since timing_enable()."""
+    L = lib()
+    L.hipbp_kernel_name.restype = ctypes.c_char_p
+    L.hipbp_timing_collect.restype = ctypes.c_int
+    k = L.hipbp_kernel_count()
+    ms = (ctypes.c_double * k)()
+    cnt = (ctypes.c_uint64 * k)()
+    _chk(L.hipbp_timing_collect(ms, cnt))
+    return {L.hipbp_kernel_name(i).decode(): (ms[i], cnt[i]) for i in range(k)}

@@ -65,8 +65,60 @@ struct Buf {
     T* as() const { return (T*)p; }
 };
 
+// HIP-event timing of the verify pipeline's kernels (bench.py's live roofline numbers).
+struct EventTimer : bp::KernelTimer {
+    struct Rec {
+        int kind;
+        hipEvent_t a, b;
+    };
+    bool on = false;
+    std::vector<hipEvent_t> pool;
+    size_t used = 0;
+    std::vector<Rec> pending;
+    hipEvent_t open[bp::KT_COUNT] = {};
+    double total_ms[bp::KT_COUNT] = {};
+    uint64_t count[bp::KT_COUNT] = {};
+
+    hipEvent_t get() {
+        if (used == pool.size()) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            pool.push_back(e);
+        }
+        return pool[used++];
+    }
+    void mark(int kind, bool end, hipStream_t s) override {
+        hipEvent_t e = get();
+        if (!e) return;
+        (void)hipEventRecord(e, s);
+        if (!end)
+            open[kind] = e;
+        else
+            pending.push_back(Rec{kind, open[kind], e});
+    }
+    hipError_t collect() {
+        for (auto& r : pending) {
+            hipError_t err = hipEventSynchronize(r.b);
+            if (err != hipSuccess) return err;
+            float ms = 0;
+            if ((err = hipEventElapsedTime(&ms, r.a, r.b)) != hipSuccess) return err;
+            total_ms[r.kind] += ms;
+            count[r.kind]++;
+        }
+        pending.clear();
+        used = 0;
+        return hipSuccess;
+    }
+    void reset() {
+        pending.clear();
+        used = 0;
+        for (int i = 0; i < bp::KT_COUNT; i++) { total_ms[i] = 0; count[i] = 0; }
+    }
+};
+
 // Per-device state. Tables are built on first use (k_init_tables) and cached.
 struct Engine {
+    EventTimer timer;
     int device = -1;
     hipStream_t stream = nullptr;
     bp::ge* dtab = nullptr;
@@ -207,7 +259,8 @@ int run_verify(Engine& e, const hipbp_proof_batch* batch, const ge25519* P_in, c
     bp::VerifyWs w;
     BP_RET_ON(carve_ws(e, batch->count, batch->n, batch->L_len, &w));
     bp::launch_verify(view_of(batch), w, (const bp::ge*)G, (const bp::ge*)H, (const bp::ge*)h, e.dtab, e.two_i,
-                      (const bp::ge*)P_in, ok, (bp::ge*)P_out, (bp::ge*)chk_out, range_mode, s);
+                      (const bp::ge*)P_in, ok, (bp::ge*)P_out, (bp::ge*)chk_out, range_mode, s,
+                      e.timer.on ? &e.timer : nullptr);
     BP_RET_ON(hipGetLastError());
     return HIPBP_OK;
 }
@@ -237,6 +290,38 @@ int hipbp_sync(void* stream) {
     BP_RET_ON(hipStreamSynchronize(pick(stream, *e)));
     return HIPBP_OK;
 }
+
+static const char* kKernelNames[bp::KT_COUNT] = {
+    "k_prep_range", "k_prep_ipa", "k_verify_msm_points", "k_tree", "k_verify_th_cq",
+    "k_fold_terms", "k_fold_combine", "k_final_terms", "k_final"};
+
+int hipbp_timing_enable(int on) {
+    hipError_t err;
+    Engine* e = engine_or_null(&err);
+    BP_RET_ON(err);
+    std::lock_guard<std::mutex> lk(e->mu);
+    BP_RET_ON(e->timer.collect());
+    e->timer.reset();
+    e->timer.on = on != 0;
+    return HIPBP_OK;
+}
+
+int hipbp_timing_collect(double* total_ms, uint64_t* launches) {
+    hipError_t err;
+    Engine* e = engine_or_null(&err);
+    BP_RET_ON(err);
+    std::lock_guard<std::mutex> lk(e->mu);
+    BP_RET_ON(e->timer.collect());
+    for (int i = 0; i < bp::KT_COUNT; i++) {
+        if (total_ms) total_ms[i] = e->timer.total_ms[i];
+        if (launches) launches[i] = e->timer.count[i];
+    }
+    return HIPBP_OK;
+}
+
+int hipbp_kernel_count(void) { return bp::KT_COUNT; }
+
+const char* hipbp_kernel_name(int kind) { return (kind >= 0 && kind < bp::KT_COUNT) ? kKernelNames[kind] : ""; }
 
 int hipbp_batch_range_proof_verify(const hipbp_proof_batch* batch, const ge25519* G, const ge25519* H,
                                    const ge25519* g, const ge25519* h, uint8_t* ok, ge25519* P_out,

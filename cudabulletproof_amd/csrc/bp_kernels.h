@@ -45,6 +45,17 @@ struct VerifyWs {
     ge* fin;       // [B*2]    a0*G', b0*H'
 };
 
+// Kernel kinds of the verify pipeline, for per-kernel HIP-event timing (bench.py roofline).
+enum KernelKind {
+    KT_PREP_RANGE = 0, KT_PREP_IPA, KT_MSM_POINTS, KT_TREE, KT_TH_CQ, KT_FOLD_TERMS, KT_FOLD_COMBINE,
+    KT_FINAL_TERMS, KT_FINAL, KT_COUNT
+};
+
+struct KernelTimer {
+    virtual void mark(int kind, bool end, hipStream_t s) = 0;
+    virtual ~KernelTimer() {}
+};
+
 void launch_init_tables(ge* dtab, fe* two_i, int nmax, hipStream_t s);
 
 // Generic canonical-tree MSM: out[seg] for S segments of m points each.
@@ -53,7 +64,7 @@ void launch_tree(ge* out, const ge* in, int S, size_t m, hipStream_t s);
 
 void launch_verify(const BatchView& bv, const VerifyWs& ws, const ge* G, const ge* H, const ge* h,
                    const ge* dtab, const fe* two_i, const ge* P_in, uint8_t* ok, ge* P_out, ge* chk_out,
-                   bool range_mode, hipStream_t s);
+                   bool range_mode, hipStream_t s, KernelTimer* tm = nullptr);
 
 // Elementwise field ops: op 0 add, 1 sub, 2 mul, 3 square-kernel quirk, 4 soa add (limbwise, no carry)
 void launch_field_op(int op, fe* r, const fe* a, const fe* b, size_t count, hipStream_t s);

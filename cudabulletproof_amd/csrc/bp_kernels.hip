@@ -297,26 +297,31 @@ static inline unsigned nblk(size_t items) { return (unsigned)((items + TPB - 1) 
 
 void launch_verify(const BatchView& bv, const VerifyWs& ws, const ge* G, const ge* H, const ge* h,
                    const ge* dtab, const fe* two_i, const ge* P_in, uint8_t* ok, ge* P_out, ge* chk_out,
-                   bool range_mode, hipStream_t s) {
+                   bool range_mode, hipStream_t s, KernelTimer* tm) {
     const size_t B = bv.B;
     const int n = bv.n;
+#define BP_TIMED(kind, ...)                    \
+    do {                                       \
+        if (tm) tm->mark(kind, false, s);      \
+        __VA_ARGS__;                           \
+        if (tm) tm->mark(kind, true, s);       \
+    } while (0)
+    if (range_mode) BP_TIMED(KT_PREP_RANGE, k_prep_range<<<nblk(B), TPB, 0, s>>>(bv, ws, two_i));
+    BP_TIMED(KT_PREP_IPA, k_prep_ipa<<<nblk(B), TPB, 0, s>>>(bv, ws));
     if (range_mode) {
-        k_prep_range<<<nblk(B), TPB, 0, s>>>(bv, ws, two_i);
-    }
-    k_prep_ipa<<<nblk(B), TPB, 0, s>>>(bv, ws);
-    if (range_mode) {
-        k_verify_msm_points<<<nblk(B * 2 * n), TPB, 0, s>>>(bv, ws, G, H, dtab);
+        BP_TIMED(KT_MSM_POINTS, k_verify_msm_points<<<nblk(B * 2 * n), TPB, 0, s>>>(bv, ws, G, H, dtab));
         // canonical tree per MSM segment (n <= 256: one pass, results in msm_part[2p + {0,1}])
-        launch_tree(ws.msm_part, ws.msm_pts, (int)(2 * B), (size_t)n, s);
+        BP_TIMED(KT_TREE, launch_tree(ws.msm_part, ws.msm_pts, (int)(2 * B), (size_t)n, s));
     }
-    k_verify_th_cq<<<nblk(B * 2), TPB, 0, s>>>(bv, ws, h, dtab);
+    BP_TIMED(KT_TH_CQ, k_verify_th_cq<<<nblk(B * 2), TPB, 0, s>>>(bv, ws, h, dtab));
     for (int r = 0; r < bv.L_len; r++) {
         int np = n >> (r + 1);
-        k_fold_terms<<<nblk(B * 4 * np), TPB, 0, s>>>(bv, ws, r, G, H, dtab);
-        k_fold_combine<<<nblk(B * 2 * np), TPB, 0, s>>>(bv, ws, r);
+        BP_TIMED(KT_FOLD_TERMS, k_fold_terms<<<nblk(B * 4 * np), TPB, 0, s>>>(bv, ws, r, G, H, dtab));
+        BP_TIMED(KT_FOLD_COMBINE, k_fold_combine<<<nblk(B * 2 * np), TPB, 0, s>>>(bv, ws, r));
     }
-    k_final_terms<<<nblk(B * 2), TPB, 0, s>>>(bv, ws, G, H, dtab);
-    k_final<<<nblk(B), TPB, 0, s>>>(bv, ws, P_in, ok, P_out, chk_out, range_mode ? 1 : 0);
+    BP_TIMED(KT_FINAL_TERMS, k_final_terms<<<nblk(B * 2), TPB, 0, s>>>(bv, ws, G, H, dtab));
+    BP_TIMED(KT_FINAL, k_final<<<nblk(B), TPB, 0, s>>>(bv, ws, P_in, ok, P_out, chk_out, range_mode ? 1 : 0));
+#undef BP_TIMED
 }
 
 // ------------------------------------------------------------------ batch field ops

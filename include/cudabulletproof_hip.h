@@ -141,6 +141,14 @@ int hipbp_field_op(int op, fe25519* r, const fe25519* a, const fe25519* b, size_
 /* Wait for `stream`. */
 int hipbp_sync(void* stream);
 
+/* Per-kernel HIP-event timing of the verify pipeline (on the stream the kernels run on).
+ * enable(1) resets the accumulators; collect() waits for the recorded events and returns,
+ * per kernel kind, the summed launch durations (ms) and the launch counts. */
+int hipbp_timing_enable(int on);
+int hipbp_timing_collect(double* total_ms, uint64_t* launches);
+int hipbp_kernel_count(void);
+const char* hipbp_kernel_name(int kind);
+
 #ifdef __cplusplus
 }
 #endif
