@@ -37,6 +37,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=1024, help="proofs per step per GPU")
     ap.add_argument("--n", type=int, default=64, help="range bits")
+    ap.add_argument("--streams", type=int, default=2, help="HIP streams batches rotate over (overlap)")
     ap.add_argument("--msm-log2", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -44,14 +45,18 @@ def parse():
     return ap.parse_args()
 
 
+TASK_B = GE_B + FE_B + GE_B   # one scalar-mult task: point + scalar in, term out
+
+
 def alg_bytes(kernel, B, n, ab_len):
-    """Algorithmic HBM bytes of one launch-set of `kernel` over a batch (inputs read + outputs written)."""
+    """Algorithmic HBM bytes of all launches of `kernel` for one batch (inputs read + outputs written)."""
     Lr = n.bit_length() - 1
-    folds = sum(4 * (n >> (r + 1)) for r in range(Lr))            # scalar-mult tasks over all rounds
-    if kernel == "k_fold_terms":
-        return B * folds * (GE_B + FE_B + GE_B)                     # point + scalar in, term out
-    if kernel == "k_verify_msm_points":
-        return B * 2 * n * (GE_B + FE_B + GE_B)
+    if kernel == "k_stage0":          # 2 MSMs (2n) + fold round 0 (2n) + t*h, c*Q
+        return B * (2 * n + 2 * n + 2) * TASK_B
+    if kernel == "k_fold_terms":      # rounds 1 .. Lr-1
+        return B * sum(4 * (n >> (r + 1)) for r in range(1, Lr)) * TASK_B
+    if kernel == "k_final_terms":
+        return B * 2 * TASK_B
     return None
 
 
@@ -128,16 +133,19 @@ def main():
     Gd, Hd, gd, hd = T(G), T(H), T(g), T(h)
     nb = 4
     batches = [bp.RangeProofBatch.from_numpy(n, synth.proofs(B, n, seed=1 + 1000 * rank + i), dev) for i in range(nb)]
-    ok = torch.zeros(B, dtype=torch.uint8, device=dev)
+    ns = max(1, args.streams)
+    streams = [torch.cuda.Stream(dev) for _ in range(ns)]
+    oks = [torch.zeros(B, dtype=torch.uint8, device=dev) for _ in range(ns)]
     stream = torch.cuda.current_stream(dev)
+    torch.cuda.synchronize(dev)
 
     def step(k):
-        bp.batch_range_proof_verify(batches[k % nb], Gd, Hd, gd, hd, ok, stream=stream)
+        bp.batch_range_proof_verify(batches[k % nb], Gd, Hd, gd, hd, oks[k % ns], stream=streams[k % ns])
 
-    for k in range(args.warmup):
+    for k in range(max(args.warmup, 1)):
         step(k)
     torch.cuda.synchronize(dev)
-    passes_warm = int(ok.sum().item())
+    passes_warm = int(oks[0].sum().item())
 
     bp.timing_enable(True)
     if world > 1:
@@ -212,7 +220,7 @@ def main():
                     "complete_bulletproof_test.cu:33-109)",
             "config": {"workload": f"batch {B} x {n}-bit range-proof verify per GPU (BASELINE configs[1])",
                        "batch_per_gpu": B, "n": n, "semantics": "cuda_range_proof_verify (crv:82)",
-                       "parallelism": f"independent proof shards x{world}",
+                       "parallelism": f"independent proof shards x{world}", "streams": ns,
                        "proof_bytes": proof_bytes(n, 1), "passes_in_warmup_batch": passes_warm},
             "roofline": roofline, "cpu_baseline": cpu, "msm": msm,
         }

@@ -6,6 +6,7 @@
 // Unlike the reference it does not cudaMalloc/cudaFree per call: a per-process engine
 // keeps grow-only device buffers, the identity-doubling and 2^i tables, and one stream.
 #include <hip/hip_runtime.h>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -126,8 +127,11 @@ struct Engine {
     int two_cap = 0;
     // single-call staging
     Buf h2d[8], scratch[8];
-    // batch-verify workspace
-    Buf ws[16];
+    // batch-verify workspaces, one set per stream so batches on different streams overlap
+    struct WsSet {
+        Buf b[16];
+    };
+    std::map<hipStream_t, WsSet*> ws;
     std::mutex mu;
 
     hipError_t init() {
@@ -193,36 +197,39 @@ int log2i(size_t n) {
 }
 
 // Workspace carve-out for a verify batch.
-hipError_t carve_ws(Engine& e, size_t B, size_t n, size_t Lr, bp::VerifyWs* w) {
+hipError_t carve_ws(Engine& e, hipStream_t s, size_t B, size_t n, size_t Lr, bp::VerifyWs* w) {
     hipError_t r;
+    Engine::WsSet*& set = e.ws[s];
+    if (!set) set = new Engine::WsSet();
+    Buf* wb = set->b;
     size_t nh = n / 2 ? n / 2 : 1;
     size_t Lc = Lr ? Lr : 1;
-    if ((r = e.ws[0].need(B * sizeof(bp::fe))) != hipSuccess) return r;
-    if ((r = e.ws[1].need(B * n * sizeof(bp::fe))) != hipSuccess) return r;
-    if ((r = e.ws[2].need(B * 4 * sizeof(bp::fe))) != hipSuccess) return r;
-    if ((r = e.ws[3].need(B * Lc * sizeof(bp::fe))) != hipSuccess) return r;
-    if ((r = e.ws[4].need(B * Lc * sizeof(bp::fe))) != hipSuccess) return r;
-    if ((r = e.ws[5].need(B)) != hipSuccess) return r;
-    if ((r = e.ws[6].need(B * 2 * n * sizeof(bp::ge))) != hipSuccess) return r;
-    if ((r = e.ws[7].need(B * 2 * sizeof(bp::ge))) != hipSuccess) return r;
-    if ((r = e.ws[8].need(B * 4 * sizeof(bp::ge))) != hipSuccess) return r;
-    if ((r = e.ws[9].need(B * 2 * n * sizeof(bp::ge))) != hipSuccess) return r;
-    if ((r = e.ws[10].need(B * nh * sizeof(bp::ge))) != hipSuccess) return r;
-    if ((r = e.ws[11].need(B * nh * sizeof(bp::ge))) != hipSuccess) return r;
-    if ((r = e.ws[12].need(B * 2 * sizeof(bp::ge))) != hipSuccess) return r;
-    w->sG = e.ws[0].as<bp::fe>();
-    w->sH = e.ws[1].as<bp::fe>();
-    w->sc = e.ws[2].as<bp::fe>();
-    w->u = e.ws[3].as<bp::fe>();
-    w->uinv = e.ws[4].as<bp::fe>();
-    w->ipok = e.ws[5].as<uint8_t>();
-    w->msm_pts = e.ws[6].as<bp::ge>();
-    w->msm_part = e.ws[7].as<bp::ge>();
-    w->terms = e.ws[8].as<bp::ge>();
-    w->fold = e.ws[9].as<bp::ge>();
-    w->Gc = e.ws[10].as<bp::ge>();
-    w->Hc = e.ws[11].as<bp::ge>();
-    w->fin = e.ws[12].as<bp::ge>();
+    if ((r = wb[0].need(B * sizeof(bp::fe))) != hipSuccess) return r;
+    if ((r = wb[1].need(B * n * sizeof(bp::fe))) != hipSuccess) return r;
+    if ((r = wb[2].need(B * 4 * sizeof(bp::fe))) != hipSuccess) return r;
+    if ((r = wb[3].need(B * Lc * sizeof(bp::fe))) != hipSuccess) return r;
+    if ((r = wb[4].need(B * Lc * sizeof(bp::fe))) != hipSuccess) return r;
+    if ((r = wb[5].need(B)) != hipSuccess) return r;
+    if ((r = wb[6].need(B * 2 * n * sizeof(bp::ge))) != hipSuccess) return r;
+    if ((r = wb[7].need(B * 2 * sizeof(bp::ge))) != hipSuccess) return r;
+    if ((r = wb[8].need(B * 4 * sizeof(bp::ge))) != hipSuccess) return r;
+    if ((r = wb[9].need(B * 2 * n * sizeof(bp::ge))) != hipSuccess) return r;
+    if ((r = wb[10].need(B * nh * sizeof(bp::ge))) != hipSuccess) return r;
+    if ((r = wb[11].need(B * nh * sizeof(bp::ge))) != hipSuccess) return r;
+    if ((r = wb[12].need(B * 2 * sizeof(bp::ge))) != hipSuccess) return r;
+    w->sG = wb[0].as<bp::fe>();
+    w->sH = wb[1].as<bp::fe>();
+    w->sc = wb[2].as<bp::fe>();
+    w->u = wb[3].as<bp::fe>();
+    w->uinv = wb[4].as<bp::fe>();
+    w->ipok = wb[5].as<uint8_t>();
+    w->msm_pts = wb[6].as<bp::ge>();
+    w->msm_part = wb[7].as<bp::ge>();
+    w->terms = wb[8].as<bp::ge>();
+    w->fold = wb[9].as<bp::ge>();
+    w->Gc = wb[10].as<bp::ge>();
+    w->Hc = wb[11].as<bp::ge>();
+    w->fin = wb[12].as<bp::ge>();
     return hipSuccess;
 }
 
@@ -257,7 +264,7 @@ int run_verify(Engine& e, const hipbp_proof_batch* batch, const ge25519* P_in, c
     int rc = check_batch(batch, range_mode);
     if (rc != HIPBP_OK || batch->count == 0) return rc;
     bp::VerifyWs w;
-    BP_RET_ON(carve_ws(e, batch->count, batch->n, batch->L_len, &w));
+    BP_RET_ON(carve_ws(e, s, batch->count, batch->n, batch->L_len, &w));
     bp::launch_verify(view_of(batch), w, (const bp::ge*)G, (const bp::ge*)H, (const bp::ge*)h, e.dtab, e.two_i,
                       (const bp::ge*)P_in, ok, (bp::ge*)P_out, (bp::ge*)chk_out, range_mode, s,
                       e.timer.on ? &e.timer : nullptr);
@@ -292,8 +299,8 @@ int hipbp_sync(void* stream) {
 }
 
 static const char* kKernelNames[bp::KT_COUNT] = {
-    "k_prep_range", "k_prep_ipa", "k_verify_msm_points", "k_tree", "k_verify_th_cq",
-    "k_fold_terms", "k_fold_combine", "k_final_terms", "k_final"};
+    "k_prep_range", "k_prep_ipa", "k_stage0", "k_tree", "k_fold_terms", "k_fold_combine", "k_final_terms",
+    "k_final"};
 
 int hipbp_timing_enable(int on) {
     hipError_t err;

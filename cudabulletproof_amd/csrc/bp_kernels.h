@@ -47,7 +47,7 @@ struct VerifyWs {
 
 // Kernel kinds of the verify pipeline, for per-kernel HIP-event timing (bench.py roofline).
 enum KernelKind {
-    KT_PREP_RANGE = 0, KT_PREP_IPA, KT_MSM_POINTS, KT_TREE, KT_TH_CQ, KT_FOLD_TERMS, KT_FOLD_COMBINE,
+    KT_PREP_RANGE = 0, KT_PREP_IPA, KT_STAGE0, KT_TREE, KT_FOLD_TERMS, KT_FOLD_COMBINE,
     KT_FINAL_TERMS, KT_FINAL, KT_COUNT
 };
 

@@ -159,48 +159,15 @@ __global__ __launch_bounds__(TPB) void k_prep_ipa(BatchView bv, VerifyWs ws) {
 }
 
 // ------------------------------------------------------------------ verify: scalar multiplications
-// The two MSMs of calculate_inner_product_point (rp.cu:724, :728): segment 2p = <sG, G>,
-// segment 2p+1 = <sH, H>.  Item layout keeps a G segment's lanes together so that its
-// waves share one scalar.
-__global__ __launch_bounds__(TPB) void k_verify_msm_points(BatchView bv, VerifyWs ws, const ge* __restrict__ G,
-                                                           const ge* __restrict__ H, const ge* __restrict__ dtab) {
-    size_t i = gid();
-    const int n = bv.n;
-    if (i >= (size_t)bv.B * 2 * n) return;
-    size_t seg = i / n;
-    int k = (int)(i % n);
-    size_t p = seg >> 1;
-    bool isH = seg & 1;
-    fe s = isH ? ws.sH[p * n + k] : ws.sG[p];
-    ge r = scalarmult(s, isH ? H[k] : G[k], dtab);
-    ws.msm_pts[i] = ge_norm_dev(r);
-}
-
-// Stage-0 host-semantics scalar-mults independent of the IPA rounds:
-// t*h (rp.cu:778-781) and c*Q (crv:255, :268-269).  Items: 2p -> t*h, 2p+1 -> c*Q.
-__global__ __launch_bounds__(TPB) void k_verify_th_cq(BatchView bv, VerifyWs ws, const ge* __restrict__ h,
-                                                      const ge* __restrict__ dtab) {
-    size_t i = gid();
-    if (i >= (size_t)bv.B * 2) return;
-    size_t p = i >> 1;
-    bool isC = i & 1;
-    fe s = isC ? ws.sc[p * 4 + 3] : ws.sc[p * 4 + 0];
-    ge r = scalarmult(s, *h, dtab);
-    ws.terms[p * 4 + 2 + (isC ? 1 : 0)] = ge_norm_host(r);
-}
-
 // IPA fold round r (crv:220-242), n' = n >> (r+1).  Items per proof (4n'):
 //   [0,n')   u^-1 * G_j        [n',2n')  u^-1 * H_{j+n'}
 //   [2n',3n') u * G_{j+n'}     [3n',4n') u * H_j
 // (lanes sharing a scalar are adjacent).  Round 0 reads the generators, later rounds
 // the proof's folded Gc/Hc.
-__global__ __launch_bounds__(TPB) void k_fold_terms(BatchView bv, VerifyWs ws, int r, const ge* __restrict__ G,
-                                                    const ge* __restrict__ H, const ge* __restrict__ dtab) {
+__device__ __forceinline__ void fold_task(const BatchView& bv, const VerifyWs& ws, int r, size_t p, int k,
+                                          const ge* __restrict__ G, const ge* __restrict__ H,
+                                          const ge* __restrict__ dtab) {
     const int n = bv.n, np = n >> (r + 1), Lr = bv.L_len;
-    size_t i = gid();
-    if (i >= (size_t)bv.B * 4 * np) return;
-    size_t p = i / (4 * np);
-    int k = (int)(i % (4 * np));
     int grp = k / np, j = k % np;
     const ge* Gs = (r == 0) ? G : ws.Gc + p * (n / 2);
     const ge* Hs = (r == 0) ? H : ws.Hc + p * (n / 2);
@@ -212,6 +179,54 @@ __global__ __launch_bounds__(TPB) void k_fold_terms(BatchView bv, VerifyWs ws, i
     else { pt = &Hs[j];      s = ws.u[p * Lr + r]; }
     ge t = scalarmult(s, *pt, dtab);
     ws.fold[p * (2 * n) + k] = ge_norm_host(t);
+}
+
+// Stage 0: every scalar multiplication that depends only on the proof, in one launch so
+// that none of them waits behind another (task regions are contiguous per kind, so a
+// wave's lanes mostly share a scalar):
+//   region A  [0, 2nB)      the two MSMs of calculate_inner_product_point (rp.cu:724, :728):
+//                           segment 2p = <sG, G>, 2p+1 = <sH, H>; Ndev (kernels.cu:26-42)
+//   region B  [.., +2nB)    IPA fold round 0 terms (fold_task, r = 0)
+//   region C  [.., +2B)     t*h (rp.cu:778-781) and c*Q (crv:255, :268-269), host normalize
+__global__ __launch_bounds__(TPB) void k_stage0(BatchView bv, VerifyWs ws, const ge* __restrict__ G,
+                                                const ge* __restrict__ H, const ge* __restrict__ h,
+                                                const ge* __restrict__ dtab, int range_mode) {
+    size_t i = gid();
+    const size_t B = bv.B;
+    const int n = bv.n;
+    const size_t nA = range_mode ? B * 2 * n : 0;
+    const size_t nB = bv.L_len > 0 ? B * 2 * n : 0;
+    if (i < nA) {
+        size_t seg = i / n;
+        int k = (int)(i % n);
+        size_t p = seg >> 1;
+        bool isH = seg & 1;
+        fe s = isH ? ws.sH[p * n + k] : ws.sG[p];
+        ge r = scalarmult(s, isH ? H[k] : G[k], dtab);
+        ws.msm_pts[i] = ge_norm_dev(r);
+        return;
+    }
+    i -= nA;
+    if (i < nB) {
+        fold_task(bv, ws, 0, i / (2 * n), (int)(i % (2 * n)), G, H, dtab);
+        return;
+    }
+    i -= nB;
+    if (i >= B * 2) return;
+    size_t p = i >> 1;
+    bool isC = i & 1;
+    if (!isC && !range_mode) return;
+    fe s = isC ? ws.sc[p * 4 + 3] : ws.sc[p * 4 + 0];
+    ge r = scalarmult(s, *h, dtab);
+    ws.terms[p * 4 + 2 + (isC ? 1 : 0)] = ge_norm_host(r);
+}
+
+__global__ __launch_bounds__(TPB) void k_fold_terms(BatchView bv, VerifyWs ws, int r, const ge* __restrict__ G,
+                                                    const ge* __restrict__ H, const ge* __restrict__ dtab) {
+    const int np = bv.n >> (r + 1);
+    size_t i = gid();
+    if (i >= (size_t)bv.B * 4 * np) return;
+    fold_task(bv, ws, r, i / (4 * np), (int)(i % (4 * np)), G, H, dtab);
 }
 
 // G'_j = N(term(u^-1 G_j) + term(u G_{j+n'})),  H'_j = N(term(u H_j) + term(u^-1 H_{j+n'}))  (crv:230, :240)
@@ -308,15 +323,15 @@ void launch_verify(const BatchView& bv, const VerifyWs& ws, const ge* G, const g
     } while (0)
     if (range_mode) BP_TIMED(KT_PREP_RANGE, k_prep_range<<<nblk(B), TPB, 0, s>>>(bv, ws, two_i));
     BP_TIMED(KT_PREP_IPA, k_prep_ipa<<<nblk(B), TPB, 0, s>>>(bv, ws));
-    if (range_mode) {
-        BP_TIMED(KT_MSM_POINTS, k_verify_msm_points<<<nblk(B * 2 * n), TPB, 0, s>>>(bv, ws, G, H, dtab));
-        // canonical tree per MSM segment (n <= 256: one pass, results in msm_part[2p + {0,1}])
-        BP_TIMED(KT_TREE, launch_tree(ws.msm_part, ws.msm_pts, (int)(2 * B), (size_t)n, s));
+    {
+        size_t items = (range_mode ? B * 2 * n : 0) + (bv.L_len > 0 ? B * 2 * n : 0) + B * 2;
+        BP_TIMED(KT_STAGE0, k_stage0<<<nblk(items), TPB, 0, s>>>(bv, ws, G, H, h, dtab, range_mode ? 1 : 0));
     }
-    BP_TIMED(KT_TH_CQ, k_verify_th_cq<<<nblk(B * 2), TPB, 0, s>>>(bv, ws, h, dtab));
+    // canonical tree per MSM segment (n <= 256: one pass, results in msm_part[2p + {0,1}])
+    if (range_mode) BP_TIMED(KT_TREE, launch_tree(ws.msm_part, ws.msm_pts, (int)(2 * B), (size_t)n, s));
     for (int r = 0; r < bv.L_len; r++) {
         int np = n >> (r + 1);
-        BP_TIMED(KT_FOLD_TERMS, k_fold_terms<<<nblk(B * 4 * np), TPB, 0, s>>>(bv, ws, r, G, H, dtab));
+        if (r > 0) BP_TIMED(KT_FOLD_TERMS, k_fold_terms<<<nblk(B * 4 * np), TPB, 0, s>>>(bv, ws, r, G, H, dtab));
         BP_TIMED(KT_FOLD_COMBINE, k_fold_combine<<<nblk(B * 2 * np), TPB, 0, s>>>(bv, ws, r));
     }
     BP_TIMED(KT_FINAL_TERMS, k_final_terms<<<nblk(B * 2), TPB, 0, s>>>(bv, ws, G, H, dtab));

@@ -12,6 +12,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#ifndef BP_MUL_ASM
+#define BP_MUL_ASM 1
+#endif
+#include "mul512_asm.h"
+
 namespace bp {
 
 struct fe {
@@ -121,7 +126,9 @@ BP_DEV fe fe_fold512(const uint64_t t[8]) {
 }
 
 // Exact 256x256 -> 512-bit product, product scanning over 32-bit words with a
-// 96-bit column accumulator.
+// 96-bit column accumulator.  BP_MUL_ASM selects the generated gfx950 column kernels
+// (mul512_asm.h: v_mad_u64_u32 carry-out + v_addc_co_u32, 2 VALU per 32x32 product);
+// the plain-C form below is the reference formulation of the same product.
 BP_DEV void mul512(uint64_t t[8], const fe& f, const fe& g) {
     uint32_t a[8], b[8], w[16];
 #pragma unroll
@@ -131,6 +138,9 @@ BP_DEV void mul512(uint64_t t[8], const fe& f, const fe& g) {
         b[2 * i] = (uint32_t)g.v[i];
         b[2 * i + 1] = (uint32_t)(g.v[i] >> 32);
     }
+#if BP_MUL_ASM
+    mul512_asm(w, a, b);
+#else
     uint64_t acc = 0;
     uint32_t c2 = 0;
 #pragma unroll
@@ -148,6 +158,7 @@ BP_DEV void mul512(uint64_t t[8], const fe& f, const fe& g) {
         c2 = 0;
     }
     w[15] = (uint32_t)acc;
+#endif
 #pragma unroll
     for (int i = 0; i < 8; i++) t[i] = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
 }
