@@ -37,7 +37,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=1024, help="proofs per step per GPU")
     ap.add_argument("--n", type=int, default=64, help="range bits")
-    ap.add_argument("--streams", type=int, default=2, help="HIP streams batches rotate over (overlap)")
+    ap.add_argument("--mode", choices=["pipeline", "oneshot"], default="pipeline",
+                    help="pipeline: streaming verify pipeline, one tick (= one batch of work) per step; "
+                         "oneshot: each step verifies one batch start to finish")
+    ap.add_argument("--streams", type=int, default=2, help="oneshot mode: HIP streams batches rotate over")
     ap.add_argument("--msm-log2", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -50,14 +53,14 @@ TASK_B = GE_B + FE_B + GE_B   # one scalar-mult task: point + scalar in, term ou
 
 def alg_bytes(kernel, B, n, ab_len):
     """Algorithmic HBM bytes of all launches of `kernel` for one batch (inputs read + outputs written)."""
-    Lr = n.bit_length() - 1
-    if kernel == "k_stage0":          # 2 MSMs (2n) + fold round 0 (2n) + t*h, c*Q
-        return B * (2 * n + 2 * n + 2) * TASK_B
-    if kernel == "k_fold_terms":      # rounds 1 .. Lr-1
-        return B * sum(4 * (n >> (r + 1)) for r in range(1, Lr)) * TASK_B
-    if kernel == "k_final_terms":
-        return B * 2 * TASK_B
+    if kernel == "k_terms":   # every scalar multiplication of a verify: 2 MSMs, all fold rounds, t*h, c*Q, a0*G', b0*H'
+        return B * sm_per_verify(n) * TASK_B
     return None
+
+
+def sm_per_verify(n):
+    Lr = n.bit_length() - 1
+    return 2 * n + sum(4 * (n >> (r + 1)) for r in range(Lr)) + 4
 
 
 def proof_bytes(n, ab_len):
@@ -135,18 +138,32 @@ def main():
     batches = [bp.RangeProofBatch.from_numpy(n, synth.proofs(B, n, seed=1 + 1000 * rank + i), dev) for i in range(nb)]
     ns = max(1, args.streams)
     streams = [torch.cuda.Stream(dev) for _ in range(ns)]
-    oks = [torch.zeros(B, dtype=torch.uint8, device=dev) for _ in range(ns)]
+    oks = [torch.zeros(B, dtype=torch.uint8, device=dev) for _ in range(max(ns, nb))]
     stream = torch.cuda.current_stream(dev)
     torch.cuda.synchronize(dev)
+    pipe = None
+    if args.mode == "pipeline":
+        pipe = bp.VerifyPipeline(B, n, Gd, Hd, hd, stream=streams[0])
 
-    def step(k):
-        bp.batch_range_proof_verify(batches[k % nb], Gd, Hd, gd, hd, oks[k % ns], stream=streams[k % ns])
+        def step(k):   # one tick: stage s of the batch pushed s ticks earlier, for every s
+            pipe.push(batches[k % nb], oks[k % nb])
+        warm = max(args.warmup, pipe.depth)   # fill the pipeline before timing
+    else:
+        def step(k):
+            bp.batch_range_proof_verify(batches[k % nb], Gd, Hd, gd, hd, oks[k % ns], stream=streams[k % ns])
+        warm = max(args.warmup, 1)
 
-    for k in range(max(args.warmup, 1)):
+    for k in range(warm):
         step(k)
+    if pipe:
+        pipe.flush()
     torch.cuda.synchronize(dev)
     passes_warm = int(oks[0].sum().item())
 
+    if pipe:   # refill (flush drained it) so every timed tick carries a full batch of work
+        for k in range(pipe.depth - 1):
+            step(k)
+        torch.cuda.synchronize(dev)
     bp.timing_enable(True)
     if world > 1:
         dist.barrier()
@@ -160,6 +177,10 @@ def main():
     dt = time.perf_counter() - t0
     stats = bp.timing_collect()
     bp.timing_enable(False)
+    if pipe:
+        pipe.flush()
+        torch.cuda.synchronize(dev)
+        pipe.close()
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -179,15 +200,13 @@ def main():
     ab_batch = alg_bytes(dom, B, n, 1)
     per_launch = ab_batch * args.steps / launches if ab_batch else None
     achieved = (per_launch / (avg_ms * 1e-3)) / 1e9 if per_launch else None
-    Lr = n.bit_length() - 1
-    sm_per_verify = 2 * n + 2 + sum(4 * (n >> (r + 1)) for r in range(Lr)) + 2
     roofline = {
         "bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": pmc_traffic(dom),
         "avg_launch_ms": avg_ms, "launches": launches,
         "kernel_ms_share": {k: round(v / sum(kern_ms.values()), 4) for k, v in kern_ms.items()},
         "binding": "VALU integer (not HBM, not MFMA): see DESIGN.md",
-        "scalar_mults_per_s": value * sm_per_verify,
+        "scalar_mults_per_s": value * sm_per_verify(n),
     }
 
     msm = None
@@ -220,7 +239,8 @@ def main():
                     "complete_bulletproof_test.cu:33-109)",
             "config": {"workload": f"batch {B} x {n}-bit range-proof verify per GPU (BASELINE configs[1])",
                        "batch_per_gpu": B, "n": n, "semantics": "cuda_range_proof_verify (crv:82)",
-                       "parallelism": f"independent proof shards x{world}", "streams": ns,
+                       "parallelism": f"independent proof shards x{world}", "mode": args.mode,
+                       "pipeline_depth": pipe.depth if pipe else None,
                        "proof_bytes": proof_bytes(n, 1), "passes_in_warmup_batch": passes_warm},
             "roofline": roofline, "cpu_baseline": cpu, "msm": msm,
         }

@@ -88,7 +88,8 @@ EXPORTS = [
     "cuda_benchmark_multi_scalar_mul", "cuda_benchmark_inner_product", "cuda_benchmark_field_operations",
     "cuda_benchmark_range_proof", "hipbp_last_error", "hipbp_device_count", "hipbp_batch_range_proof_verify",
     "hipbp_batch_inner_product_verify", "hipbp_msm", "hipbp_field_op", "hipbp_sync", "hipbp_timing_enable",
-    "hipbp_timing_collect", "hipbp_kernel_count", "hipbp_kernel_name",
+    "hipbp_timing_collect", "hipbp_kernel_count", "hipbp_kernel_name", "hipbp_pipeline_create",
+    "hipbp_pipeline_push", "hipbp_pipeline_flush", "hipbp_pipeline_depth", "hipbp_pipeline_destroy",
 ]
 
 
@@ -353,3 +354,45 @@ def timing_collect():
     cnt = (ctypes.c_uint64 * k)()
     _chk(L.hipbp_timing_collect(ms, cnt))
     return {L.hipbp_kernel_name(i).decode(): (ms[i], cnt[i]) for i in range(k)}
+
+
+# ====================================================================== streaming verify pipeline
+class VerifyPipeline:
+    """hipbp_pipeline_*: up to `depth` batches in flight; each push runs one tick in which
+    every in-flight batch advances one stage (stage 0 / fold round r / final).  A batch's
+    outputs are complete after depth-1 further pushes or flush()."""
+
+    def __init__(self, max_batch, n, G, H, h, range_mode=True, stream=None):
+        L = lib()
+        L.hipbp_pipeline_create.restype = ctypes.c_void_p
+        L.hipbp_pipeline_push.restype = ctypes.c_int
+        L.hipbp_pipeline_flush.restype = ctypes.c_int
+        L.hipbp_pipeline_depth.restype = ctypes.c_int
+        self._keep = (G, H, h)
+        self.h = L.hipbp_pipeline_create(_sz(max_batch), _sz(n), 1 if range_mode else 0, _c(G.data_ptr()),
+                                         _c(H.data_ptr()), _c(h.data_ptr()), _stream_ptr(stream))
+        if not self.h:
+            raise BulletproofError(L.hipbp_last_error().decode())
+        self.depth = L.hipbp_pipeline_depth(_c(self.h))
+
+    def push(self, batch, ok=None, P_out=None, check_out=None, P_in=None):
+        s = batch.c_struct() if batch is not None else None
+        _chk(lib().hipbp_pipeline_push(
+            _c(self.h), ctypes.byref(s) if s is not None else None,
+            _c(P_in.data_ptr()) if P_in is not None else None, _c(ok.data_ptr()) if ok is not None else None,
+            _c(P_out.data_ptr()) if P_out is not None else None,
+            _c(check_out.data_ptr()) if check_out is not None else None))
+
+    def flush(self):
+        _chk(lib().hipbp_pipeline_flush(_c(self.h)))
+
+    def close(self):
+        if self.h:
+            lib().hipbp_pipeline_destroy(_c(self.h))
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -7,6 +7,7 @@
 // keeps grow-only device buffers, the identity-doubling and 2^i tables, and one stream.
 #include <hip/hip_runtime.h>
 #include <map>
+#include <tuple>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -67,7 +68,7 @@ struct Buf {
 };
 
 // HIP-event timing of the verify pipeline's kernels (bench.py's live roofline numbers).
-struct EventTimer : bp::KernelTimer {
+struct EventTimer {
     struct Rec {
         int kind;
         hipEvent_t a, b;
@@ -88,7 +89,7 @@ struct EventTimer : bp::KernelTimer {
         }
         return pool[used++];
     }
-    void mark(int kind, bool end, hipStream_t s) override {
+    void mark(int kind, bool end, hipStream_t s) {
         hipEvent_t e = get();
         if (!e) return;
         (void)hipEventRecord(e, s);
@@ -127,11 +128,23 @@ struct Engine {
     int two_cap = 0;
     // single-call staging
     Buf h2d[8], scratch[8];
-    // batch-verify workspaces, one set per stream so batches on different streams overlap
-    struct WsSet {
-        Buf b[16];
-    };
-    std::map<hipStream_t, WsSet*> ws;
+    // pinned host staging for the single-proof entry points (a pageable source of an
+    // async copy must outlive the copy; this one does, and the stream is synced after use)
+    uint8_t* pinned = nullptr;
+    size_t pinned_cap = 0;
+    hipError_t need_pinned(size_t bytes) {
+        if (bytes <= pinned_cap) return hipSuccess;
+        hipError_t r;
+        if (pinned && (r = hipStreamSynchronize(stream)) != hipSuccess) return r;
+        if (pinned && (r = hipHostFree(pinned)) != hipSuccess) return r;
+        pinned = nullptr;
+        pinned_cap = 0;
+        if ((r = hipHostMalloc(&pinned, bytes)) != hipSuccess) return r;
+        pinned_cap = bytes;
+        return hipSuccess;
+    }
+    // one-shot verify pipelines, per (stream, n, mode), so batches on different streams overlap
+    std::map<std::tuple<hipStream_t, int, bool>, struct Pipeline*> pipes;
     std::mutex mu;
 
     hipError_t init() {
@@ -196,43 +209,6 @@ int log2i(size_t n) {
     return k;
 }
 
-// Workspace carve-out for a verify batch.
-hipError_t carve_ws(Engine& e, hipStream_t s, size_t B, size_t n, size_t Lr, bp::VerifyWs* w) {
-    hipError_t r;
-    Engine::WsSet*& set = e.ws[s];
-    if (!set) set = new Engine::WsSet();
-    Buf* wb = set->b;
-    size_t nh = n / 2 ? n / 2 : 1;
-    size_t Lc = Lr ? Lr : 1;
-    if ((r = wb[0].need(B * sizeof(bp::fe))) != hipSuccess) return r;
-    if ((r = wb[1].need(B * n * sizeof(bp::fe))) != hipSuccess) return r;
-    if ((r = wb[2].need(B * 4 * sizeof(bp::fe))) != hipSuccess) return r;
-    if ((r = wb[3].need(B * Lc * sizeof(bp::fe))) != hipSuccess) return r;
-    if ((r = wb[4].need(B * Lc * sizeof(bp::fe))) != hipSuccess) return r;
-    if ((r = wb[5].need(B)) != hipSuccess) return r;
-    if ((r = wb[6].need(B * 2 * n * sizeof(bp::ge))) != hipSuccess) return r;
-    if ((r = wb[7].need(B * 2 * sizeof(bp::ge))) != hipSuccess) return r;
-    if ((r = wb[8].need(B * 4 * sizeof(bp::ge))) != hipSuccess) return r;
-    if ((r = wb[9].need(B * 2 * n * sizeof(bp::ge))) != hipSuccess) return r;
-    if ((r = wb[10].need(B * nh * sizeof(bp::ge))) != hipSuccess) return r;
-    if ((r = wb[11].need(B * nh * sizeof(bp::ge))) != hipSuccess) return r;
-    if ((r = wb[12].need(B * 2 * sizeof(bp::ge))) != hipSuccess) return r;
-    w->sG = wb[0].as<bp::fe>();
-    w->sH = wb[1].as<bp::fe>();
-    w->sc = wb[2].as<bp::fe>();
-    w->u = wb[3].as<bp::fe>();
-    w->uinv = wb[4].as<bp::fe>();
-    w->ipok = wb[5].as<uint8_t>();
-    w->msm_pts = wb[6].as<bp::ge>();
-    w->msm_part = wb[7].as<bp::ge>();
-    w->terms = wb[8].as<bp::ge>();
-    w->fold = wb[9].as<bp::ge>();
-    w->Gc = wb[10].as<bp::ge>();
-    w->Hc = wb[11].as<bp::ge>();
-    w->fin = wb[12].as<bp::ge>();
-    return hipSuccess;
-}
-
 int check_batch(const hipbp_proof_batch* b, bool range_mode) {
     if (!b) { g_err = "null batch"; return HIPBP_ERR_ARG; }
     if (b->count == 0) return HIPBP_OK;
@@ -259,17 +235,169 @@ bp::BatchView view_of(const hipbp_proof_batch* b) {
     return v;
 }
 
+// The verify pipeline: a ring of D = L_len + 1 batch slots.  Every tick launches ONE
+// k_terms over all in-flight batches (stage 0 of the newest, fold round r of the batch
+// pushed r ticks earlier, the final terms of the oldest), then the newest batch's MSM
+// tree, then ONE k_combine (fold combinations + final assembly).  Within a batch the
+// reference's order is kept exactly; across batches nothing depends on anything.
+struct Pipeline {
+    Engine* e = nullptr;
+    hipStream_t s = nullptr;
+    int n = 0, Lr = 0, D = 0;
+    size_t maxB = 0;
+    bool range_mode = true;
+    const bp::ge *G = nullptr, *H = nullptr, *h = nullptr;
+    struct Slot {
+        Buf b[16];
+        bp::SlotDev dev{};
+        bool active = false;
+        int stage = 0;
+        size_t B = 0;
+        hipEvent_t copied = nullptr;
+    };
+    std::vector<Slot> slots;
+    bp::SlotDev* slots_dev = nullptr;   // device copies [D]
+    bp::SlotDev* host_dev = nullptr;    // pinned staging [D]
+    int head = 0;
+
+    hipError_t init(Engine* eng, hipStream_t st, size_t mb, int nn, bool range) {
+        e = eng; s = st; maxB = mb; n = nn; range_mode = range;
+        Lr = log2i((size_t)n);
+        D = Lr + 1;
+        slots.resize(D);
+        hipError_t r;
+        if ((r = hipMalloc(&slots_dev, D * sizeof(bp::SlotDev))) != hipSuccess) return r;
+        if ((r = hipHostMalloc(&host_dev, D * sizeof(bp::SlotDev))) != hipSuccess) return r;
+        for (auto& sl : slots)
+            if ((r = hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming)) != hipSuccess) return r;
+        return hipSuccess;
+    }
+    void release() {
+        if (s) (void)hipStreamSynchronize(s);
+        for (auto& sl : slots) {
+            for (auto& b : sl.b) if (b.p) (void)hipFree(b.p);
+            if (sl.copied) (void)hipEventDestroy(sl.copied);
+        }
+        if (slots_dev) (void)hipFree(slots_dev);
+        if (host_dev) (void)hipHostFree(host_dev);
+    }
+    bool busy() const {
+        for (auto& sl : slots) if (sl.active) return true;
+        return false;
+    }
+    hipError_t carve(Slot& sl, size_t B, size_t Lb) {
+        hipError_t r;
+        size_t nh = n / 2 ? n / 2 : 1, Lc = Lb ? Lb : 1;
+        size_t sz[14] = {B * 32, B * n * 32, B * 4 * 32, B * Lc * 32, B * Lc * 32, B, B * 2 * n * 128, B * 2 * 128,
+                         B * 4 * 128, B * 2 * n * 128, B * nh * 128, B * nh * 128, B * 2 * 128, B * 128};
+        for (int i = 0; i < 14; i++)
+            if ((r = sl.b[i].need(sz[i])) != hipSuccess) return r;
+        bp::VerifyWs& w = sl.dev.ws;
+        w.sG = sl.b[0].as<bp::fe>(); w.sH = sl.b[1].as<bp::fe>(); w.sc = sl.b[2].as<bp::fe>();
+        w.u = sl.b[3].as<bp::fe>(); w.uinv = sl.b[4].as<bp::fe>(); w.ipok = sl.b[5].as<uint8_t>();
+        w.msm_pts = sl.b[6].as<bp::ge>(); w.msm_part = sl.b[7].as<bp::ge>(); w.terms = sl.b[8].as<bp::ge>();
+        w.fold = sl.b[9].as<bp::ge>(); w.Gc = sl.b[10].as<bp::ge>(); w.Hc = sl.b[11].as<bp::ge>();
+        w.fin = sl.b[12].as<bp::ge>(); w.Pin = sl.b[13].as<bp::ge>();
+        return hipSuccess;
+    }
+
+    // One tick; `b` may be null (drain).  Outputs of `b` are written when it completes.
+    int push(const hipbp_proof_batch* b, const ge25519* P_in, uint8_t* ok, ge25519* P_out, ge25519* chk) {
+        EventTimer* tm = e->timer.on ? &e->timer : nullptr;
+        bool has = b && b->count > 0;
+        Slot& nw = slots[head];
+        if (has) {
+            int rc = check_batch(b, range_mode);
+            if (rc != HIPBP_OK) return rc;
+            if ((int)b->n != n) { g_err = "batch n differs from the pipeline's"; return HIPBP_ERR_ARG; }
+            if (nw.active) { g_err = "pipeline slot busy (internal)"; return HIPBP_ERR_ARG; }
+            BP_RET_ON(carve(nw, b->count, b->L_len));
+            nw.dev.bv = view_of(b);
+            nw.dev.ok = ok;
+            nw.dev.P_out = (bp::ge*)P_out;
+            nw.dev.chk_out = (bp::ge*)chk;
+            nw.dev.range_mode = range_mode ? 1 : 0;
+            BP_RET_ON(hipEventSynchronize(nw.copied));   // staging slot free again
+            host_dev[head] = nw.dev;
+            BP_RET_ON(hipMemcpyAsync(slots_dev + head, host_dev + head, sizeof(bp::SlotDev), hipMemcpyHostToDevice, s));
+            BP_RET_ON(hipEventRecord(nw.copied, s));
+            if (!range_mode)
+                BP_RET_ON(hipMemcpyAsync(nw.dev.ws.Pin, P_in, b->count * sizeof(ge25519), hipMemcpyDeviceToDevice, s));
+            if (tm) tm->mark(bp::KT_PREP, false, s);
+            bp::launch_prep(nw.dev.bv, nw.dev.ws, e->two_i, range_mode, s);
+            if (tm) tm->mark(bp::KT_PREP, true, s);
+            nw.active = true;
+            nw.stage = 0;
+            nw.B = b->count;
+        }
+        bp::RegionList tr{}, cr{};
+        auto add = [](bp::RegionList& rl, int kind, int slot, int r, unsigned long long items) {
+            if (!items) return;
+            bp::Region& g = rl.reg[rl.count++];
+            g.kind = kind; g.slot = slot; g.r = r; g.begin = rl.total; g.items = items;
+            rl.total += (items + 63) & ~63ull;   // regions start on wave boundaries
+        };
+        for (int k = 0; k < D; k++) {
+            int idx = (head - k + D) % D;   // newest first
+            Slot& sl = slots[idx];
+            if (!sl.active) continue;
+            const bp::BatchView& bv = sl.dev.bv;
+            unsigned long long B = bv.B;
+            int L = bv.L_len, st = sl.stage;
+            if (st == 0) {
+                unsigned long long it = (range_mode ? B * 2 * n : 0) + (L > 0 ? B * 2 * n : 0) + B * 2;
+                add(tr, bp::RK_STAGE0, idx, 0, it);
+            }
+            if (st >= 1 && st <= L - 1) add(tr, bp::RK_ROUND, idx, st, B * 4 * (n >> (st + 1)));
+            if (st == L) add(tr, bp::RK_FINAL_TERMS, idx, 0, B * 2);
+            if (st <= L - 1) add(cr, bp::RK_COMBINE, idx, st, B * 2 * (n >> (st + 1)));
+            if (st == L) add(cr, bp::RK_FINAL, idx, 0, B);
+        }
+        if (tm) tm->mark(bp::KT_TERMS, false, s);
+        bp::launch_terms(tr, slots_dev, G, H, h, e->dtab, s);
+        if (tm) tm->mark(bp::KT_TERMS, true, s);
+        if (has && range_mode) {
+            if (tm) tm->mark(bp::KT_TREE, false, s);
+            bp::launch_tree(nw.dev.ws.msm_part, nw.dev.ws.msm_pts, (int)(2 * nw.B), (size_t)n, s);
+            if (tm) tm->mark(bp::KT_TREE, true, s);
+        }
+        if (tm) tm->mark(bp::KT_COMBINE, false, s);
+        bp::launch_combine(cr, slots_dev, s);
+        if (tm) tm->mark(bp::KT_COMBINE, true, s);
+        BP_RET_ON(hipGetLastError());
+        for (auto& sl : slots) {
+            if (!sl.active) continue;
+            if (sl.stage == sl.dev.bv.L_len) sl.active = false;
+            else sl.stage++;
+        }
+        head = (head + 1) % D;
+        return HIPBP_OK;
+    }
+    int flush() {
+        while (busy()) {
+            int rc = push(nullptr, nullptr, nullptr, nullptr, nullptr);
+            if (rc != HIPBP_OK) return rc;
+        }
+        return HIPBP_OK;
+    }
+};
+
+// One-shot verify of a whole batch on `s` (push + drain of a cached pipeline).
 int run_verify(Engine& e, const hipbp_proof_batch* batch, const ge25519* P_in, const ge25519* G, const ge25519* H,
                const ge25519* h, uint8_t* ok, ge25519* P_out, ge25519* chk_out, bool range_mode, hipStream_t s) {
     int rc = check_batch(batch, range_mode);
     if (rc != HIPBP_OK || batch->count == 0) return rc;
-    bp::VerifyWs w;
-    BP_RET_ON(carve_ws(e, s, batch->count, batch->n, batch->L_len, &w));
-    bp::launch_verify(view_of(batch), w, (const bp::ge*)G, (const bp::ge*)H, (const bp::ge*)h, e.dtab, e.two_i,
-                      (const bp::ge*)P_in, ok, (bp::ge*)P_out, (bp::ge*)chk_out, range_mode, s,
-                      e.timer.on ? &e.timer : nullptr);
-    BP_RET_ON(hipGetLastError());
-    return HIPBP_OK;
+    auto key = std::make_tuple(s, (int)batch->n, range_mode);
+    Pipeline*& pl = e.pipes[key];
+    if (!pl) {
+        pl = new Pipeline();
+        BP_RET_ON(pl->init(&e, s, batch->count, (int)batch->n, range_mode));
+    }
+    pl->G = (const bp::ge*)G;
+    pl->H = (const bp::ge*)H;
+    pl->h = (const bp::ge*)h;
+    if ((rc = pl->push(batch, P_in, ok, P_out, chk_out)) != HIPBP_OK) return rc;
+    return pl->flush();
 }
 
 // ---- host staging for the single-proof reference entry points
@@ -298,9 +426,7 @@ int hipbp_sync(void* stream) {
     return HIPBP_OK;
 }
 
-static const char* kKernelNames[bp::KT_COUNT] = {
-    "k_prep_range", "k_prep_ipa", "k_stage0", "k_tree", "k_fold_terms", "k_fold_combine", "k_final_terms",
-    "k_final"};
+static const char* kKernelNames[bp::KT_COUNT] = {"k_prep", "k_terms", "k_tree", "k_combine"};
 
 int hipbp_timing_enable(int on) {
     hipError_t err;
@@ -351,6 +477,51 @@ int hipbp_batch_inner_product_verify(const hipbp_proof_batch* batch, const ge255
     if (!P || !G || !H || !Q || !ok) { g_err = "null argument"; return HIPBP_ERR_ARG; }
     std::lock_guard<std::mutex> lk(e->mu);
     return run_verify(*e, batch, P, G, H, Q, ok, nullptr, check_out, false, pick(stream, *e));
+}
+
+void* hipbp_pipeline_create(size_t max_batch, size_t n, int range_mode, const ge25519* G, const ge25519* H,
+                            const ge25519* h, void* stream) {
+    hipError_t err;
+    Engine* e = engine_or_null(&err);
+    if (!e) { g_err = std::string("engine: ") + hipGetErrorString(err); return nullptr; }
+    if (!is_pow2(n) || n > 256 || !G || !H || !h) { g_err = "pipeline: bad n or null generator"; return nullptr; }
+    Pipeline* pl = new Pipeline();
+    err = pl->init(e, pick(stream, *e), max_batch, (int)n, range_mode != 0);
+    if (err != hipSuccess) {
+        g_err = std::string("pipeline init: ") + hipGetErrorString(err);
+        pl->release();
+        delete pl;
+        return nullptr;
+    }
+    pl->G = (const bp::ge*)G;
+    pl->H = (const bp::ge*)H;
+    pl->h = (const bp::ge*)h;
+    return pl;
+}
+
+int hipbp_pipeline_push(void* handle, const hipbp_proof_batch* batch, const ge25519* P_in, uint8_t* ok,
+                        ge25519* P_out, ge25519* check_out) {
+    Pipeline* pl = (Pipeline*)handle;
+    if (!pl) { g_err = "null pipeline"; return HIPBP_ERR_ARG; }
+    if (batch && batch->count && (!ok || (!pl->range_mode && !P_in))) { g_err = "null output/P"; return HIPBP_ERR_ARG; }
+    std::lock_guard<std::mutex> lk(pl->e->mu);
+    return pl->push(batch, P_in, ok, P_out, check_out);
+}
+
+int hipbp_pipeline_flush(void* handle) {
+    Pipeline* pl = (Pipeline*)handle;
+    if (!pl) { g_err = "null pipeline"; return HIPBP_ERR_ARG; }
+    std::lock_guard<std::mutex> lk(pl->e->mu);
+    return pl->flush();
+}
+
+int hipbp_pipeline_depth(void* handle) { return handle ? ((Pipeline*)handle)->D : 0; }
+
+void hipbp_pipeline_destroy(void* handle) {
+    Pipeline* pl = (Pipeline*)handle;
+    if (!pl) return;
+    pl->release();
+    delete pl;
 }
 
 int hipbp_msm(ge25519* result, const fe25519* scalars, const ge25519* points, size_t n, void* stream) {
@@ -511,8 +682,9 @@ static bool stage_single(Engine& e, const InnerProductProof* ip, const RangeProo
     // head: V,A,S,T1,T2 | t,c,x ; then a,b ; then L,R
     size_t bytes = 5 * sizeof(ge25519) + 3 * sizeof(fe25519) + 2 * abl * sizeof(fe25519) + 2 * Lr * sizeof(ge25519);
     BP_EXIT_ON(e.h2d[3].need(bytes));
-    std::vector<uint8_t> host(bytes);
-    uint8_t* q = host.data();
+    BP_EXIT_ON(e.need_pinned(bytes));
+    BP_EXIT_ON(hipStreamSynchronize(e.stream));   // previous user of the staging buffer is done
+    uint8_t* q = e.pinned;
     auto put = [&](const void* src, size_t len) {
         if (src) memcpy(q, src, len);
         else memset(q, 0, len);
@@ -533,7 +705,7 @@ static bool stage_single(Engine& e, const InnerProductProof* ip, const RangeProo
         put(ip->L.elements, Lr * sizeof(ge25519));
         put(ip->R.elements, Lr * sizeof(ge25519));
     }
-    BP_EXIT_ON(hipMemcpyAsync(e.h2d[3].p, host.data(), bytes, hipMemcpyHostToDevice, e.stream));
+    BP_EXIT_ON(hipMemcpyAsync(e.h2d[3].p, e.pinned, bytes, hipMemcpyHostToDevice, e.stream));
     uint8_t* d = e.h2d[3].as<uint8_t>();
     const ge25519* pts = (const ge25519*)d;
     const fe25519* fes = (const fe25519*)(d + 5 * sizeof(ge25519));

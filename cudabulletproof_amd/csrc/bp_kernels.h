@@ -43,28 +43,51 @@ struct VerifyWs {
     ge* Gc;        // [B*n/2]
     ge* Hc;        // [B*n/2]
     ge* fin;       // [B*2]    a0*G', b0*H'
+    ge* Pin;       // [B]      given P (inner-product-only verify)
 };
 
-// Kernel kinds of the verify pipeline, for per-kernel HIP-event timing (bench.py roofline).
-enum KernelKind {
-    KT_PREP_RANGE = 0, KT_PREP_IPA, KT_STAGE0, KT_TREE, KT_FOLD_TERMS, KT_FOLD_COMBINE,
-    KT_FINAL_TERMS, KT_FINAL, KT_COUNT
+// One batch in flight in the verify pipeline (device-resident copy, read by the tick kernels).
+struct SlotDev {
+    BatchView bv;
+    VerifyWs ws;
+    uint8_t* ok;
+    ge* P_out;
+    ge* chk_out;
+    int range_mode;
 };
 
-struct KernelTimer {
-    virtual void mark(int kind, bool end, hipStream_t s) = 0;
-    virtual ~KernelTimer() {}
+// A tick's work list: region k covers items [begin_k, begin_{k+1}) of one slot at one stage.
+enum RegionKind { RK_STAGE0 = 0, RK_ROUND = 1, RK_FINAL_TERMS = 2, RK_COMBINE = 3, RK_FINAL = 4 };
+struct Region {
+    int kind;
+    int slot;
+    int r;
+    int pad;
+    unsigned long long begin;
+    unsigned long long items;   // lanes [begin+items, next begin) are wave-alignment padding
 };
+constexpr int MAX_REGIONS = 12;
+struct RegionList {
+    int count;
+    int pad;
+    unsigned long long total;
+    Region reg[MAX_REGIONS];
+};
+
+// Kernel groups of the verify pipeline, for per-kernel HIP-event timing (bench.py roofline).
+enum KernelKind { KT_PREP = 0, KT_TERMS, KT_TREE, KT_COMBINE, KT_COUNT };
 
 void launch_init_tables(ge* dtab, fe* two_i, int nmax, hipStream_t s);
+void launch_prep(const BatchView& bv, const VerifyWs& ws, const fe* two_i, bool range_mode, hipStream_t s);
+void launch_terms(const RegionList& rl, const SlotDev* slots, const ge* G, const ge* H, const ge* h,
+                  const ge* dtab, hipStream_t s);
+void launch_combine(const RegionList& rl, const SlotDev* slots, hipStream_t s);
 
 // Generic canonical-tree MSM: out[seg] for S segments of m points each.
 void launch_msm_points(ge* pts, const fe* scal, const ge* P, size_t m, const ge* dtab, hipStream_t s);
 void launch_tree(ge* out, const ge* in, int S, size_t m, hipStream_t s);
 
-void launch_verify(const BatchView& bv, const VerifyWs& ws, const ge* G, const ge* H, const ge* h,
-                   const ge* dtab, const fe* two_i, const ge* P_in, uint8_t* ok, ge* P_out, ge* chk_out,
-                   bool range_mode, hipStream_t s, KernelTimer* tm = nullptr);
+
 
 // Elementwise field ops: op 0 add, 1 sub, 2 mul, 3 square-kernel quirk, 4 soa add (limbwise, no carry)
 void launch_field_op(int op, fe* r, const fe* a, const fe* b, size_t count, hipStream_t s);

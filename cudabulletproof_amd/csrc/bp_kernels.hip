@@ -13,6 +13,7 @@ namespace bp {
 
 constexpr int TPB = 256;   // threads per block for lane-per-item kernels
 
+
 __device__ __forceinline__ size_t gid() { return (size_t)blockIdx.x * blockDim.x + threadIdx.x; }
 
 // ------------------------------------------------------------------ tables
@@ -45,9 +46,10 @@ void launch_init_tables(ge* dtab, fe* two_i, int nmax, hipStream_t s) {
 __global__ __launch_bounds__(TPB) void k_msm_points(ge* pts, const fe* __restrict__ scal,
                                                     const ge* __restrict__ P, size_t total, size_t m,
                                                     const ge* __restrict__ dtab) {
+    __shared__ geq qs[TPB];
     size_t i = gid();
     if (i >= total) return;
-    ge r = scalarmult(scal[i], P[i % m], dtab);
+    ge r = scalarmult<true>(scal[i], P[i % m], &qs[threadIdx.x], dtab);
     pts[i] = ge_norm_dev(r);
 }
 
@@ -165,7 +167,7 @@ __global__ __launch_bounds__(TPB) void k_prep_ipa(BatchView bv, VerifyWs ws) {
 // (lanes sharing a scalar are adjacent).  Round 0 reads the generators, later rounds
 // the proof's folded Gc/Hc.
 __device__ __forceinline__ void fold_task(const BatchView& bv, const VerifyWs& ws, int r, size_t p, int k,
-                                          const ge* __restrict__ G, const ge* __restrict__ H,
+                                          geq* qslot, const ge* __restrict__ G, const ge* __restrict__ H,
                                           const ge* __restrict__ dtab) {
     const int n = bv.n, np = n >> (r + 1), Lr = bv.L_len;
     int grp = k / np, j = k % np;
@@ -177,24 +179,29 @@ __device__ __forceinline__ void fold_task(const BatchView& bv, const VerifyWs& w
     else if (grp == 1) { pt = &Hs[j + np]; s = ws.uinv[p * Lr + r]; }
     else if (grp == 2) { pt = &Gs[j + np]; s = ws.u[p * Lr + r]; }
     else { pt = &Hs[j];      s = ws.u[p * Lr + r]; }
-    ge t = scalarmult(s, *pt, dtab);
+    ge t = scalarmult<true>(s, *pt, qslot, dtab);
     ws.fold[p * (2 * n) + k] = ge_norm_host(t);
 }
 
-// Stage 0: every scalar multiplication that depends only on the proof, in one launch so
-// that none of them waits behind another (task regions are contiguous per kind, so a
-// wave's lanes mostly share a scalar):
-//   region A  [0, 2nB)      the two MSMs of calculate_inner_product_point (rp.cu:724, :728):
-//                           segment 2p = <sG, G>, 2p+1 = <sH, H>; Ndev (kernels.cu:26-42)
-//   region B  [.., +2nB)    IPA fold round 0 terms (fold_task, r = 0)
-//   region C  [.., +2B)     t*h (rp.cu:778-781) and c*Q (crv:255, :268-269), host normalize
-__global__ __launch_bounds__(TPB) void k_stage0(BatchView bv, VerifyWs ws, const ge* __restrict__ G,
-                                                const ge* __restrict__ H, const ge* __restrict__ h,
-                                                const ge* __restrict__ dtab, int range_mode) {
-    size_t i = gid();
+// Stage 0: every scalar multiplication that depends only on the proof (contiguous per kind,
+// so a wave's lanes mostly share a scalar):
+//   [0, 2nB)      the two MSMs of calculate_inner_product_point (rp.cu:724, :728):
+//                 segment 2p = <sG, G>, 2p+1 = <sH, H>; Ndev (kernels.cu:26-42)
+//   [.., +2nB)    IPA fold round 0 terms
+//   [.., +2B)     t*h (rp.cu:778-781) and c*Q (crv:255, :268-269), host normalize
+__device__ __forceinline__ size_t stage0_items(const SlotDev& sd) {
+    const size_t B = sd.bv.B;
+    return (sd.range_mode ? B * 2 * sd.bv.n : 0) + (sd.bv.L_len > 0 ? B * 2 * sd.bv.n : 0) + B * 2;
+}
+
+__device__ __forceinline__ void stage0_task(const SlotDev& sd, size_t i, geq* qslot, const ge* __restrict__ G,
+                                            const ge* __restrict__ H, const ge* __restrict__ h,
+                                            const ge* __restrict__ dtab) {
+    const BatchView& bv = sd.bv;
+    const VerifyWs& ws = sd.ws;
     const size_t B = bv.B;
     const int n = bv.n;
-    const size_t nA = range_mode ? B * 2 * n : 0;
+    const size_t nA = sd.range_mode ? B * 2 * n : 0;
     const size_t nB = bv.L_len > 0 ? B * 2 * n : 0;
     if (i < nA) {
         size_t seg = i / n;
@@ -202,74 +209,75 @@ __global__ __launch_bounds__(TPB) void k_stage0(BatchView bv, VerifyWs ws, const
         size_t p = seg >> 1;
         bool isH = seg & 1;
         fe s = isH ? ws.sH[p * n + k] : ws.sG[p];
-        ge r = scalarmult(s, isH ? H[k] : G[k], dtab);
+        ge r = scalarmult<true>(s, isH ? H[k] : G[k], qslot, dtab);
         ws.msm_pts[i] = ge_norm_dev(r);
         return;
     }
     i -= nA;
     if (i < nB) {
-        fold_task(bv, ws, 0, i / (2 * n), (int)(i % (2 * n)), G, H, dtab);
+        fold_task(bv, ws, 0, i / (2 * n), (int)(i % (2 * n)), qslot, G, H, dtab);
         return;
     }
     i -= nB;
-    if (i >= B * 2) return;
     size_t p = i >> 1;
     bool isC = i & 1;
-    if (!isC && !range_mode) return;
+    if (!isC && !sd.range_mode) return;
     fe s = isC ? ws.sc[p * 4 + 3] : ws.sc[p * 4 + 0];
-    ge r = scalarmult(s, *h, dtab);
+    ge r = scalarmult<true>(s, *h, qslot, dtab);
     ws.terms[p * 4 + 2 + (isC ? 1 : 0)] = ge_norm_host(r);
 }
 
-__global__ __launch_bounds__(TPB) void k_fold_terms(BatchView bv, VerifyWs ws, int r, const ge* __restrict__ G,
-                                                    const ge* __restrict__ H, const ge* __restrict__ dtab) {
-    const int np = bv.n >> (r + 1);
-    size_t i = gid();
-    if (i >= (size_t)bv.B * 4 * np) return;
-    fold_task(bv, ws, r, i / (4 * np), (int)(i % (4 * np)), G, H, dtab);
-}
-
-// G'_j = N(term(u^-1 G_j) + term(u G_{j+n'})),  H'_j = N(term(u H_j) + term(u^-1 H_{j+n'}))  (crv:230, :240)
-__global__ __launch_bounds__(TPB) void k_fold_combine(BatchView bv, VerifyWs ws, int r) {
-    const int n = bv.n, np = n >> (r + 1);
-    size_t i = gid();
-    if (i >= (size_t)bv.B * 2 * np) return;
-    size_t p = i / (2 * np);
-    int k = (int)(i % (2 * np));
-    const ge* f = ws.fold + p * (2 * n);
-    if (k < np) {
-        int j = k;
-        ws.Gc[p * (n / 2) + j] = ge_norm_host(ge_add(f[j], f[2 * np + j]));
-    } else {
-        int j = k - np;
-        ws.Hc[p * (n / 2) + j] = ge_norm_host(ge_add(f[3 * np + j], f[np + j]));
-    }
-}
-
 // a0*G'_0 and b0*H'_0 (crv:262-266).  Items: 2p -> a0*G', 2p+1 -> b0*H'.
-__global__ __launch_bounds__(TPB) void k_final_terms(BatchView bv, VerifyWs ws, const ge* __restrict__ G,
-                                                     const ge* __restrict__ H, const ge* __restrict__ dtab) {
-    size_t i = gid();
-    if (i >= (size_t)bv.B * 2) return;
+__device__ __forceinline__ void final_terms_task(const SlotDev& sd, size_t i, geq* qslot, const ge* __restrict__ G,
+                                                 const ge* __restrict__ H, const ge* __restrict__ dtab) {
+    const BatchView& bv = sd.bv;
+    const VerifyWs& ws = sd.ws;
     size_t p = i >> 1;
     bool isH = i & 1;
     const int n = bv.n;
     const ge* pt = (bv.L_len > 0) ? (isH ? &ws.Hc[p * (n / 2)] : &ws.Gc[p * (n / 2)]) : (isH ? &H[0] : &G[0]);
     fe s = ws.sc[p * 4 + (isH ? 2 : 1)];
-    ge t = scalarmult(s, *pt, dtab);
+    ge t = scalarmult<true>(s, *pt, qslot, dtab);
     ws.fin[p * 2 + (isH ? 1 : 0)] = ge_norm_host(t);
+}
+
+__device__ __forceinline__ int find_region(const RegionList& rl, size_t i) {
+    int k = 0;
+    while (k + 1 < rl.count && i >= rl.reg[k + 1].begin) k++;
+    return k;
+}
+
+// One pipeline tick's scalar multiplications: every region is one in-flight batch at its
+// own stage (stage 0 / fold round r / final terms), so a launch carries a whole batch's
+// worth of independent work however deep the batch-level dependency chain is.
+__global__ __launch_bounds__(TPB) void k_terms(RegionList rl, const SlotDev* __restrict__ slots,
+                                               const ge* __restrict__ G, const ge* __restrict__ H,
+                                               const ge* __restrict__ h, const ge* __restrict__ dtab) {
+    __shared__ geq qs[TPB];
+    size_t i = gid();
+    if (i >= rl.total) return;
+    const Region& rg = rl.reg[find_region(rl, i)];
+    size_t l = i - rg.begin;
+    if (l >= rg.items) return;
+    const SlotDev& sd = slots[rg.slot];
+    if (rg.kind == RK_STAGE0) {
+        stage0_task(sd, l, &qs[threadIdx.x], G, H, h, dtab);
+    } else if (rg.kind == RK_ROUND) {
+        const int np = sd.bv.n >> (rg.r + 1);
+        fold_task(sd.bv, sd.ws, rg.r, l / (4 * np), (int)(l % (4 * np)), &qs[threadIdx.x], G, H, dtab);
+    } else {
+        final_terms_task(sd, l, &qs[threadIdx.x], G, H, dtab);
+    }
 }
 
 __device__ __forceinline__ int absdiff(int a, int b) { return a > b ? a - b : b - a; }
 
 // P assembly (rp.cu:785-801), check point (crv:257-278) and the tolerant accept rule
 // (crv:297-357).  One lane per proof.
-__global__ __launch_bounds__(TPB) void k_final(BatchView bv, VerifyWs ws, const ge* __restrict__ P_in,
-                                               uint8_t* ok, ge* P_out, ge* chk_out, int range_mode) {
-    size_t p = gid();
-    if (p >= (size_t)bv.B) return;
+__device__ __forceinline__ void final_task(const SlotDev& sd, size_t p) {
+    const VerifyWs& ws = sd.ws;
     ge P;
-    if (range_mode) {
+    if (sd.range_mode) {
         P = ge_zero();
         P = ge_norm_host(ge_add(P, ws.msm_part[p * 2 + 0]));
         P = ge_norm_host(ge_add(P, ws.msm_part[p * 2 + 1]));
@@ -277,14 +285,14 @@ __global__ __launch_bounds__(TPB) void k_final(BatchView bv, VerifyWs ws, const 
         P = ge_norm_host(P);
         P = ge_norm_host(P);
     } else {
-        P = P_in[p];
+        P = ws.Pin[p];
     }
     ge cp = ge_zero();
     cp = ge_norm_host(ge_add(cp, ws.fin[p * 2 + 0]));
     cp = ge_norm_host(ge_add(cp, ws.fin[p * 2 + 1]));
     cp = ge_norm_host(ge_add(cp, ws.terms[p * 4 + 3]));
-    if (P_out) P_out[p] = P;
-    if (chk_out) chk_out[p] = cp;
+    if (sd.P_out) sd.P_out[p] = P;
+    if (sd.chk_out) sd.chk_out[p] = cp;
 
     fe kx = fe_canon(cp.X), ky = fe_canon(cp.Y), px = fe_canon(P.X), py = fe_canon(P.Y);
     int xd = 0, yd = 0, sx = 0, sy = 0, msb = 0;
@@ -305,38 +313,46 @@ __global__ __launch_bounds__(TPB) void k_final(BatchView bv, VerifyWs ws, const 
     int hz = 0;
     for (int i = 0; i < 32; i++) hz += ((hs.v[i >> 3] >> (8 * (i & 7))) & 0xff) != 0;
     bool accept = (sx + sy >= 20) | (msb >= 28) | (xd + yd <= 32) | (hz <= 24);
-    ok[p] = (ws.ipok[p] && accept) ? 1 : 0;
+    sd.ok[p] = (ws.ipok[p] && accept) ? 1 : 0;
+}
+
+// One pipeline tick's point combinations: fold round r  G'_j = N(term(u^-1 G_j) + term(u G_{j+n'})),
+// H'_j = N(term(u H_j) + term(u^-1 H_{j+n'}))  (crv:230, :240), or the final assembly.
+__global__ __launch_bounds__(TPB) void k_combine(RegionList rl, const SlotDev* __restrict__ slots) {
+    size_t i = gid();
+    if (i >= rl.total) return;
+    const Region& rg = rl.reg[find_region(rl, i)];
+    size_t l = i - rg.begin;
+    if (l >= rg.items) return;
+    const SlotDev& sd = slots[rg.slot];
+    if (rg.kind == RK_COMBINE) {
+        const int n = sd.bv.n, np = n >> (rg.r + 1);
+        size_t p = l / (2 * np);
+        int k = (int)(l % (2 * np));
+        const ge* f = sd.ws.fold + p * (2 * n);
+        if (k < np)
+            sd.ws.Gc[p * (n / 2) + k] = ge_norm_host(ge_add(f[k], f[2 * np + k]));
+        else
+            sd.ws.Hc[p * (n / 2) + (k - np)] = ge_norm_host(ge_add(f[3 * np + (k - np)], f[np + (k - np)]));
+    } else {
+        final_task(sd, l);
+    }
 }
 
 static inline unsigned nblk(size_t items) { return (unsigned)((items + TPB - 1) / TPB); }
 
-void launch_verify(const BatchView& bv, const VerifyWs& ws, const ge* G, const ge* H, const ge* h,
-                   const ge* dtab, const fe* two_i, const ge* P_in, uint8_t* ok, ge* P_out, ge* chk_out,
-                   bool range_mode, hipStream_t s, KernelTimer* tm) {
-    const size_t B = bv.B;
-    const int n = bv.n;
-#define BP_TIMED(kind, ...)                    \
-    do {                                       \
-        if (tm) tm->mark(kind, false, s);      \
-        __VA_ARGS__;                           \
-        if (tm) tm->mark(kind, true, s);       \
-    } while (0)
-    if (range_mode) BP_TIMED(KT_PREP_RANGE, k_prep_range<<<nblk(B), TPB, 0, s>>>(bv, ws, two_i));
-    BP_TIMED(KT_PREP_IPA, k_prep_ipa<<<nblk(B), TPB, 0, s>>>(bv, ws));
-    {
-        size_t items = (range_mode ? B * 2 * n : 0) + (bv.L_len > 0 ? B * 2 * n : 0) + B * 2;
-        BP_TIMED(KT_STAGE0, k_stage0<<<nblk(items), TPB, 0, s>>>(bv, ws, G, H, h, dtab, range_mode ? 1 : 0));
-    }
-    // canonical tree per MSM segment (n <= 256: one pass, results in msm_part[2p + {0,1}])
-    if (range_mode) BP_TIMED(KT_TREE, launch_tree(ws.msm_part, ws.msm_pts, (int)(2 * B), (size_t)n, s));
-    for (int r = 0; r < bv.L_len; r++) {
-        int np = n >> (r + 1);
-        if (r > 0) BP_TIMED(KT_FOLD_TERMS, k_fold_terms<<<nblk(B * 4 * np), TPB, 0, s>>>(bv, ws, r, G, H, dtab));
-        BP_TIMED(KT_FOLD_COMBINE, k_fold_combine<<<nblk(B * 2 * np), TPB, 0, s>>>(bv, ws, r));
-    }
-    BP_TIMED(KT_FINAL_TERMS, k_final_terms<<<nblk(B * 2), TPB, 0, s>>>(bv, ws, G, H, dtab));
-    BP_TIMED(KT_FINAL, k_final<<<nblk(B), TPB, 0, s>>>(bv, ws, P_in, ok, P_out, chk_out, range_mode ? 1 : 0));
-#undef BP_TIMED
+void launch_prep(const BatchView& bv, const VerifyWs& ws, const fe* two_i, bool range_mode, hipStream_t s) {
+    if (range_mode) k_prep_range<<<nblk(bv.B), TPB, 0, s>>>(bv, ws, two_i);
+    k_prep_ipa<<<nblk(bv.B), TPB, 0, s>>>(bv, ws);
+}
+
+void launch_terms(const RegionList& rl, const SlotDev* slots, const ge* G, const ge* H, const ge* h,
+                  const ge* dtab, hipStream_t s) {
+    if (rl.total) k_terms<<<nblk(rl.total), TPB, 0, s>>>(rl, slots, G, H, h, dtab);
+}
+
+void launch_combine(const RegionList& rl, const SlotDev* slots, hipStream_t s) {
+    if (rl.total) k_combine<<<nblk(rl.total), TPB, 0, s>>>(rl, slots);
 }
 
 // ------------------------------------------------------------------ batch field ops

@@ -95,11 +95,55 @@ BP_DEV int fe_clz256(const fe& s) {
 
 BP_DEV ge ld_ge(const ge* p) { return *p; }
 
+// q-side operand access.  QLDS = true: this lane's LDS slot, read at the point of use (the
+// empty asm with a memory clobber stops the compiler from hoisting the loads and keeping all
+// of q in VGPRs, which would cost occupancy in the throughput kernels).  QLDS = false: a
+// register copy (latency-bound kernels run one wave per SIMD, registers are free there).
+template <bool QLDS>
+BP_DEV fe qget(const fe* p) {
+    if (QLDS) asm volatile("" ::: "memory");
+    return *p;
+}
+
+// ge25519_add(p, q) with q's prepared operands (same operation order as ge_add_q).
+template <bool QLDS>
+BP_DEV ge ge_add_qp(const ge& p, const geq* q) {
+    fe A = fe_mul(fe_sub(p.Y, p.X), qget<QLDS>(&q->YmX));
+    fe B = fe_mul(fe_add(p.Y, p.X), qget<QLDS>(&q->YpX));
+    fe C = fe_mul(fe_mul(p.T, qget<QLDS>(&q->T)), k_const());
+    fe D = fe_mul(p.Z, qget<QLDS>(&q->Z));
+    D = fe_add(D, D);
+    fe E = fe_sub(B, A);
+    fe F = fe_sub(D, C);
+    fe G = fe_add(D, C);
+    fe H = fe_add(B, A);
+    return ge{fe_mul(E, F), fe_mul(G, H), fe_mul(F, G), fe_mul(E, H)};
+}
+
+// One step of the per-lane loop: add(r, r) when !use_q, add(r, q) when use_q; the
+// select is per lane, the operation order is ge25519_add's in both cases.
+template <bool QLDS>
+BP_DEV ge ge_add_sel(const ge& p, const geq* q, bool use_q) {
+    fe ymx = fe_sub(p.Y, p.X);
+    fe A = fe_mul(ymx, use_q ? qget<QLDS>(&q->YmX) : ymx);
+    fe ypx = fe_add(p.Y, p.X);
+    fe B = fe_mul(ypx, use_q ? qget<QLDS>(&q->YpX) : ypx);
+    fe C = fe_mul(fe_mul(p.T, use_q ? qget<QLDS>(&q->T) : p.T), k_const());
+    fe D = fe_mul(p.Z, use_q ? qget<QLDS>(&q->Z) : p.Z);
+    D = fe_add(D, D);
+    fe E = fe_sub(B, A);
+    fe F = fe_sub(D, C);
+    fe G = fe_add(D, C);
+    fe H = fe_add(B, A);
+    return ge{fe_mul(E, F), fe_mul(G, H), fe_mul(F, G), fe_mul(E, H)};
+}
+
 // ge25519_scalarmult (curve25519_ops.cu:397-415 == device .cuh:272-290) for a scalar
 // that is the same in every lane of the wave: the bit test is a scalar branch.
-// `s` holds the scalar's 256 bits (limb i = bytes 8i..8i+7, little-endian).
-// `dtab` = the identity-doubling table (257 points).
-BP_DEV ge sm_uniform(const fe& s_in, const ge& P, const ge* __restrict__ dtab) {
+// `s` holds the scalar's 256 bits (limb i = bytes 8i..8i+7, little-endian); `q` holds
+// ge_prep(P); `dtab` = the identity-doubling table (257 points).
+template <bool QLDS>
+BP_DEV ge sm_uniform(const fe& s_in, const geq* q, const ge* __restrict__ dtab) {
     fe s;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
@@ -109,26 +153,23 @@ BP_DEV ge sm_uniform(const fe& s_in, const ge& P, const ge* __restrict__ dtab) {
     }
     int lz = fe_clz256(s);
     ge r = ld_ge(&dtab[lz]);
-    if (lz == 256) return r;
-    geq q = ge_prep(P);
     for (int i = 255 - lz; i >= 0; i--) {
         r = ge_dbl(r);
-        if (fe_bit(s, i)) r = ge_add_q(r, q);
+        if (fe_bit(s, i)) r = ge_add_qp<QLDS>(r, q);
     }
     return r;
 }
 
 // Same function for a per-lane scalar: every iteration is one ge25519_add whose second
 // operand is either r itself (the doubling) or P, so no lane idles on the other's branch.
-BP_DEV ge sm_lane(const fe& s, const ge& P, const ge* __restrict__ dtab) {
+template <bool QLDS>
+BP_DEV ge sm_lane(const fe& s, const geq* q, const ge* __restrict__ dtab) {
     int lz = fe_clz256(s);
     ge r = ld_ge(&dtab[lz]);
-    geq qp = ge_prep(P);
     int i = 255 - lz;          // next bit to consume
     bool add_phase = false;    // false: next op doubles; true: next op adds P
     while (i >= 0) {
-        geq q = add_phase ? qp : ge_prep(r);
-        r = ge_add_q(r, q);
+        r = ge_add_sel<QLDS>(r, q, add_phase);
         if (add_phase) {
             add_phase = false;
             i--;
@@ -142,15 +183,26 @@ BP_DEV ge sm_lane(const fe& s, const ge& P, const ge* __restrict__ dtab) {
 }
 
 // Wave-level dispatch: uniform scalar -> scalar-branch loop, else the per-lane loop.
-BP_DEV ge scalarmult(const fe& s, const ge& P, const ge* __restrict__ dtab) {
+// QLDS: `slot` is this lane's LDS slot and receives ge_prep(P); otherwise q stays in VGPRs.
+template <bool QLDS>
+BP_DEV ge scalarmult(const fe& s, const ge& P, geq* slot, const ge* __restrict__ dtab) {
+    geq qreg;
+    const geq* q;
+    if (QLDS) {
+        *slot = ge_prep(P);
+        q = slot;
+    } else {
+        qreg = ge_prep(P);
+        q = &qreg;
+    }
     uint32_t same = 1;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         uint32_t lo = (uint32_t)s.v[i], hi = (uint32_t)(s.v[i] >> 32);
         same &= (lo == __builtin_amdgcn_readfirstlane(lo)) & (hi == __builtin_amdgcn_readfirstlane(hi));
     }
-    if (__all(same)) return sm_uniform(s, P, dtab);
-    return sm_lane(s, P, dtab);
+    if (__all(same)) return sm_uniform<QLDS>(s, q, dtab);
+    return sm_lane<QLDS>(s, q, dtab);
 }
 
 }  // namespace bp

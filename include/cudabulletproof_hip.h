@@ -133,6 +133,23 @@ int hipbp_batch_range_proof_verify(const hipbp_proof_batch* batch, const ge25519
 int hipbp_batch_inner_product_verify(const hipbp_proof_batch* batch, const ge25519* P, const ge25519* G,
                                      const ge25519* H, const ge25519* Q, uint8_t* ok, ge25519* check_out,
                                      void* stream);
+/* Streaming verify pipeline.  A verify has a log2(n)+1-deep chain of dependent stages
+ * (stage 0, IPA fold rounds 1..L-1, final); the pipeline keeps up to log2(n)+1 batches in
+ * flight and each push runs ONE tick: stage 0 of the pushed batch, round r of the batch
+ * pushed r ticks earlier, the final stage of the oldest, all in one kernel launch.
+ * A batch's outputs (ok / P_out / check_out, device memory) are complete after
+ * depth-1 further pushes or a flush; its inputs (and P_in) are consumed by its own push.
+ * range_mode 1: cuda_range_proof_verify semantics (h = the generator h);
+ * range_mode 0: cuda_inner_product_verify semantics (h = Q, P_in required).
+ * Returns NULL on error (see hipbp_last_error). */
+void* hipbp_pipeline_create(size_t max_batch, size_t n, int range_mode, const ge25519* G, const ge25519* H,
+                            const ge25519* h, void* stream);
+int hipbp_pipeline_push(void* pipeline, const hipbp_proof_batch* batch /* NULL = drain tick */,
+                        const ge25519* P_in, uint8_t* ok, ge25519* P_out, ge25519* check_out);
+int hipbp_pipeline_flush(void* pipeline);
+int hipbp_pipeline_depth(void* pipeline);
+void hipbp_pipeline_destroy(void* pipeline);
+
 /* Canonical-tree MSM on device buffers. */
 int hipbp_msm(ge25519* result, const fe25519* scalars, const ge25519* points, size_t n, void* stream);
 /* Elementwise device field ops: op 0 add, 1 sub, 2 mul, 3 square (reference kernel quirk),

@@ -194,3 +194,54 @@ def test_batch_verify_deterministic(bp, oracle):
     r2 = _run_batch(bp, n, arrays, G, H, g, h)
     for x, y in zip(r1, r2):
         assert np.array_equal(x, y)
+
+
+# ----------------------------------------------------------------------------- streaming pipeline
+@pytest.mark.parametrize("n", [16, 64])
+def test_pipeline_matches_reference(bp, golden, n):
+    """Batches of different sizes in flight together (hipbp_pipeline_*): each batch's verdicts,
+    P and check points equal the reference's, whatever shares its ticks."""
+    import torch
+    d = golden(f"proofs_n{n}")
+    arrays = _batch_from_golden(bp, d, None)
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    pipe = bp.VerifyPipeline(8, n, T(d["G"]), T(d["H"]), T(d["h"]))
+    splits = [(0, 2), (2, 3), (3, 6), (0, 6), (5, 6)]
+    outs = []
+    for lo, hi in splits:
+        sub = {k: v[lo:hi] for k, v in arrays.items()}
+        batch = bp.RangeProofBatch.from_numpy(n, sub, dev)
+        ok = torch.zeros(hi - lo, dtype=torch.uint8, device=dev)
+        P = torch.zeros(hi - lo, 16, dtype=torch.int64, device=dev)
+        chk = torch.zeros(hi - lo, 16, dtype=torch.int64, device=dev)
+        pipe.push(batch, ok, P, chk)
+        outs.append((lo, hi, ok, P, chk, batch))
+        pipe.push(None)                      # a drain tick in between
+    pipe.flush()
+    torch.cuda.synchronize()
+    for lo, hi, ok, P, chk, _ in outs:
+        assert np.array_equal(ok.cpu().numpy().astype(bool), d["ok_cuda"][lo:hi].astype(bool))
+        assert np.array_equal(P.cpu().numpy().view(np.uint64), d["P"][lo:hi])
+        assert np.array_equal(chk.cpu().numpy().view(np.uint64), d["check"][lo:hi])
+    pipe.close()
+
+
+def test_pipeline_inner_product_mode(bp, golden):
+    """range_mode 0 (cuda_inner_product_verify semantics) with the reference's P given."""
+    import torch
+    n = 64
+    d = golden(f"proofs_n{n}")
+    arrays = _batch_from_golden(bp, d, None)
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    pipe = bp.VerifyPipeline(8, n, T(d["G"]), T(d["H"]), T(d["h"]), range_mode=False)
+    batch = bp.RangeProofBatch.from_numpy(n, arrays, dev)
+    ok = torch.zeros(batch.count, dtype=torch.uint8, device=dev)
+    chk = torch.zeros(batch.count, 16, dtype=torch.int64, device=dev)
+    pipe.push(batch, ok, None, chk, P_in=T(d["P"]))
+    pipe.flush()
+    torch.cuda.synchronize()
+    assert np.array_equal(ok.cpu().numpy().astype(bool), d["ok_cuda"].astype(bool))
+    assert np.array_equal(chk.cpu().numpy().view(np.uint64), d["check"])
+    pipe.close()
