@@ -179,7 +179,8 @@ __device__ __forceinline__ void fold_task(const BatchView& bv, const VerifyWs& w
     else if (grp == 1) { pt = &Hs[j + np]; s = ws.uinv[p * Lr + r]; }
     else if (grp == 2) { pt = &Gs[j + np]; s = ws.u[p * Lr + r]; }
     else { pt = &Hs[j];      s = ws.u[p * Lr + r]; }
-    ge t = scalarmult<true>(s, *pt, qslot, dtab);
+    ge P = *pt;   // through registers (an aggregate copy from a flat pointer goes via scratch)
+    ge t = scalarmult<true>(s, P, qslot, dtab);
     ws.fold[p * (2 * n) + k] = ge_norm_host(t);
 }
 
@@ -237,14 +238,19 @@ __device__ __forceinline__ void final_terms_task(const SlotDev& sd, size_t i, ge
     const int n = bv.n;
     const ge* pt = (bv.L_len > 0) ? (isH ? &ws.Hc[p * (n / 2)] : &ws.Gc[p * (n / 2)]) : (isH ? &H[0] : &G[0]);
     fe s = ws.sc[p * 4 + (isH ? 2 : 1)];
-    ge t = scalarmult<true>(s, *pt, qslot, dtab);
+    ge P = *pt;
+    ge t = scalarmult<true>(s, P, qslot, dtab);
     ws.fin[p * 2 + (isH ? 1 : 0)] = ge_norm_host(t);
 }
 
-__device__ __forceinline__ int find_region(const RegionList& rl, size_t i) {
-    int k = 0;
-    while (k + 1 < rl.count && i >= rl.reg[k + 1].begin) k++;
-    return k;
+// Region lookup with constant indices only (a run-time index into the by-value kernel
+// argument would copy the whole list to scratch).
+__device__ __forceinline__ Region find_region(const RegionList& rl, size_t i) {
+    Region g = rl.reg[0];
+#pragma unroll
+    for (int k = 1; k < MAX_REGIONS; k++)
+        if (k < rl.count && i >= rl.reg[k].begin) g = rl.reg[k];
+    return g;
 }
 
 // One pipeline tick's scalar multiplications: every region is one in-flight batch at its
@@ -256,7 +262,7 @@ __global__ __launch_bounds__(TPB) void k_terms(RegionList rl, const SlotDev* __r
     __shared__ geq qs[TPB];
     size_t i = gid();
     if (i >= rl.total) return;
-    const Region& rg = rl.reg[find_region(rl, i)];
+    const Region rg = find_region(rl, i);
     size_t l = i - rg.begin;
     if (l >= rg.items) return;
     const SlotDev& sd = slots[rg.slot];
@@ -321,7 +327,7 @@ __device__ __forceinline__ void final_task(const SlotDev& sd, size_t p) {
 __global__ __launch_bounds__(TPB) void k_combine(RegionList rl, const SlotDev* __restrict__ slots) {
     size_t i = gid();
     if (i >= rl.total) return;
-    const Region& rg = rl.reg[find_region(rl, i)];
+    const Region rg = find_region(rl, i);
     size_t l = i - rg.begin;
     if (l >= rg.items) return;
     const SlotDev& sd = slots[rg.slot];

@@ -124,18 +124,63 @@ BP_DEV ge ge_add_qp(const ge& p, const geq* q) {
 // select is per lane, the operation order is ge25519_add's in both cases.
 template <bool QLDS>
 BP_DEV ge ge_add_sel(const ge& p, const geq* q, bool use_q) {
+    // q's operands are loaded unconditionally and selected as values: a select between a
+    // loaded and a computed value is otherwise folded into a load through a select of
+    // pointers, which forces `p` into private memory (scratch).
     fe ymx = fe_sub(p.Y, p.X);
-    fe A = fe_mul(ymx, use_q ? qget<QLDS>(&q->YmX) : ymx);
+    fe qa = qget<QLDS>(&q->YmX);
+    fe A = fe_mul(ymx, use_q ? qa : ymx);
     fe ypx = fe_add(p.Y, p.X);
-    fe B = fe_mul(ypx, use_q ? qget<QLDS>(&q->YpX) : ypx);
-    fe C = fe_mul(fe_mul(p.T, use_q ? qget<QLDS>(&q->T) : p.T), k_const());
-    fe D = fe_mul(p.Z, use_q ? qget<QLDS>(&q->Z) : p.Z);
+    fe qb = qget<QLDS>(&q->YpX);
+    fe B = fe_mul(ypx, use_q ? qb : ypx);
+    fe qt = qget<QLDS>(&q->T);
+    fe C = fe_mul(fe_mul(p.T, use_q ? qt : p.T), k_const());
+    fe qz = qget<QLDS>(&q->Z);
+    fe D = fe_mul(p.Z, use_q ? qz : p.Z);
     D = fe_add(D, D);
     fe E = fe_sub(B, A);
     fe F = fe_sub(D, C);
     fe G = fe_add(D, C);
     fe H = fe_add(B, A);
     return ge{fe_mul(E, F), fe_mul(G, H), fe_mul(F, G), fe_mul(E, H)};
+}
+
+// MSB-first bit stream over a 256-bit scalar, kept as a shift register of limbs so that no
+// array is ever indexed by a run-time value (that would place the scalar in scratch).
+struct BitStream {
+    uint64_t cur, n1, n2, n3;   // cur's MSB is the next bit
+    int left;                   // bits left in cur
+};
+
+// Position the stream at bit i (0..255) of s.
+BP_DEV BitStream bs_init(const fe& s, int i) {
+    BitStream b{s.v[3], s.v[2], s.v[1], s.v[0], 0};
+    int L = i >> 6;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        bool sh = k < 3 - L;
+        b.cur = sh ? b.n1 : b.cur;
+        b.n1 = sh ? b.n2 : b.n1;
+        b.n2 = sh ? b.n3 : b.n2;
+        b.n3 = sh ? 0 : b.n3;
+    }
+    int bi = i & 63;
+    b.cur <<= (63 - bi);
+    b.left = bi + 1;
+    return b;
+}
+
+BP_DEV uint32_t bs_next(BitStream& b) {
+    uint32_t bit = (uint32_t)(b.cur >> 63);
+    b.cur <<= 1;
+    if (--b.left == 0) {
+        b.cur = b.n1;
+        b.n1 = b.n2;
+        b.n2 = b.n3;
+        b.n3 = 0;
+        b.left = 64;
+    }
+    return bit;
 }
 
 // ge25519_scalarmult (curve25519_ops.cu:397-415 == device .cuh:272-290) for a scalar
@@ -153,9 +198,11 @@ BP_DEV ge sm_uniform(const fe& s_in, const geq* q, const ge* __restrict__ dtab) 
     }
     int lz = fe_clz256(s);
     ge r = ld_ge(&dtab[lz]);
+    if (lz == 256) return r;
+    BitStream bs = bs_init(s, 255 - lz);
     for (int i = 255 - lz; i >= 0; i--) {
         r = ge_dbl(r);
-        if (fe_bit(s, i)) r = ge_add_qp<QLDS>(r, q);
+        if (bs_next(bs)) r = ge_add_qp<QLDS>(r, q);
     }
     return r;
 }
@@ -166,17 +213,18 @@ template <bool QLDS>
 BP_DEV ge sm_lane(const fe& s, const geq* q, const ge* __restrict__ dtab) {
     int lz = fe_clz256(s);
     ge r = ld_ge(&dtab[lz]);
-    int i = 255 - lz;          // next bit to consume
+    int i = 255 - lz;          // index of the pending bit
+    BitStream bs = bs_init(s, i < 0 ? 0 : i);
+    uint32_t bit = i >= 0 ? bs_next(bs) : 0;
     bool add_phase = false;    // false: next op doubles; true: next op adds P
     while (i >= 0) {
         r = ge_add_sel<QLDS>(r, q, add_phase);
-        if (add_phase) {
-            add_phase = false;
-            i--;
-        } else if (fe_bit(s, i)) {
+        if (!add_phase && bit) {
             add_phase = true;
         } else {
+            add_phase = false;
             i--;
+            bit = bs_next(bs);
         }
     }
     return r;
@@ -189,7 +237,14 @@ BP_DEV ge scalarmult(const fe& s, const ge& P, geq* slot, const ge* __restrict__
     geq qreg;
     const geq* q;
     if (QLDS) {
-        *slot = ge_prep(P);
+        fe ymx = fe_sub(P.Y, P.X), ypx = fe_add(P.Y, P.X);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {   // limb stores: an aggregate copy would stage through scratch
+            slot->YmX.v[k] = ymx.v[k];
+            slot->YpX.v[k] = ypx.v[k];
+            slot->Z.v[k] = P.Z.v[k];
+            slot->T.v[k] = P.T.v[k];
+        }
         q = slot;
     } else {
         qreg = ge_prep(P);

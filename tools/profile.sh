@@ -1,0 +1,17 @@
+#!/usr/bin/env bash
+# Profile the batched verify with rocprofv3 on the GPU box (run from the repo root via gpurun).
+#   tools/profile.sh <tag>    -> gpurun_out/prof_<tag>/{trace,pmc_fetch,pmc_write,pmc_valu}/...
+# Kernel trace + stats in one run; PMC counters in their own runs (FETCH_SIZE and WRITE_SIZE
+# do not fit one TCC pass on gfx950: MI355X_MICROARCH.md, rocprofv3 PMC slots).
+set -euo pipefail
+TAG=${1:-r01}
+OUT=gpurun_out/prof_$TAG
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+BENCH="python3 bench.py --steps 6 --warmup 2 --no-cpu --msm-log2 18"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- $BENCH > "$OUT/bench_trace.json" 2> "$OUT/trace.err"
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o run -- $BENCH > "$OUT/bench_fetch.json" 2> "$OUT/fetch.err"
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run -- $BENCH > "$OUT/bench_write.json" 2> "$OUT/write.err"
+timeout -k 10 400 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_LDS --kernel-trace --output-format csv -d "$OUT/pmc_valu" -o run -- $BENCH > "$OUT/bench_valu.json" 2> "$OUT/valu.err"
+timeout -k 10 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$OUT/pmc_cyc" -o run -- $BENCH > "$OUT/bench_cyc.json" 2> "$OUT/cyc.err"
+ls -R "$OUT" | head -40
