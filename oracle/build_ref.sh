@@ -47,3 +47,15 @@ g++ $F -Dmain=ref_test_main -c "$REF/complete_bulletproof_test.cu" -o complete_b
 g++ -O2 -w -fPIC -I"$REF" -D__device__= -c "$HERE/ref/ref_harness.cc" -o ref_harness.o
 g++ -shared -Wl,-Bsymbolic -o "$OUT/libbpref.so" *.o -lcrypto
 echo "built $OUT/libbpref.so"
+
+# Drop-in demonstration: the reference's own test driver and host code,
+# unchanged, linked against OUR libcudabulletproof_hip.so instead of the CUDA objects.
+LIB="$(cd "$HERE/.." && pwd)/cudabulletproof_amd"
+if [ -f "$LIB/libcudabulletproof_hip.so" ]; then
+    g++ $F -c "$REF/complete_bulletproof_test.cu" -o test_main.o
+    gcc -O2 -fPIC -c "$HERE/ref/det_rand.c" -o det_rand.o
+    g++ -o "$OUT/complete_bulletproof_test_hip" curve25519_ops.o bulletproof_vectors.o bulletproof_challenge.o \
+        bulletproof_range_proof.o test_main.o det_rand.o -L"$LIB" -lcudabulletproof_hip \
+        -Wl,-rpath,'$ORIGIN/../../cudabulletproof_amd' -lcrypto
+    echo "built $OUT/complete_bulletproof_test_hip"
+fi

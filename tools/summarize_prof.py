@@ -1,0 +1,107 @@
+"""Summarize a tools/profile.sh run (gpurun_out/prof_<tag>/) into profiles/.
+
+  python tools/summarize_prof.py <tag>
+    -> profiles/rocprof_<tag>_summary.md   kernel stats + PMC-derived numbers
+    -> profiles/pmc_traffic.json           per-launch HBM bytes of the steady-state kernels
+                                           (read by bench.py for roofline.traffic)
+
+HBM bytes follow MI355X_MICROARCH.md (HBM / rocprofv3): FETCH_SIZE and WRITE_SIZE come from
+separate --pmc passes, are in KB, and FETCH_SIZE is doubled on gfx950 (it tallies 128-B
+requests at 64 B).  Steady-state k_terms launches are the ones with the largest grid
+(the pipeline-fill and drain ticks carry fewer regions).
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def short(name):
+    return name.split("(")[0].replace("bp::", "")
+
+
+def load_counters(d):
+    path = os.path.join(d, "run_counter_collection.csv")
+    rows = list(csv.DictReader(open(path)))
+    per = collections.defaultdict(dict)   # dispatch -> {counter: value, kernel, grid}
+    for r in rows:
+        k = int(r["Dispatch_Id"])
+        per[k]["kernel"] = short(r["Kernel_Name"])
+        per[k]["grid"] = int(r["Grid_Size"])
+        per[k]["vgpr"] = int(r["VGPR_Count"])
+        per[k]["dur_ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        per[k][r["Counter_Name"]] = per[k].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    return per
+
+
+def steady(per, kernel):
+    ds = [v for v in per.values() if v["kernel"] == kernel]
+    if not ds:
+        return []
+    g = max(v["grid"] for v in ds)
+    return [v for v in ds if v["grid"] == g]
+
+
+def mean(xs):
+    return sum(xs) / len(xs) if xs else float("nan")
+
+
+def main():
+    tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    base = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    out_md = os.path.join(ROOT, "profiles", f"rocprof_{tag}_summary.md")
+    stats = list(csv.DictReader(open(os.path.join(base, "trace", "run_kernel_stats.csv"))))
+    lines = [f"# rocprofv3 summary — {tag}", "",
+             "Command: `tools/profile.sh " + tag + "` on one MI355X "
+             "(bench.py --steps 6 --warmup 2 --no-cpu --msm-log2 18 under rocprofv3).", "",
+             "## Kernel trace (`rocprofv3 --kernel-trace --stats`)", "",
+             "| kernel | calls | avg ms | min ms | max ms | % time |", "|---|---|---|---|---|---|"]
+    for r in stats:
+        lines.append(f"| {short(r['Name'])} | {r['Calls']} | {float(r['AverageNs'])/1e6:.3f} | "
+                     f"{float(r['MinNs'])/1e6:.3f} | {float(r['MaxNs'])/1e6:.3f} | {float(r['Percentage']):.1f} |")
+    fetch = load_counters(os.path.join(base, "pmc_fetch"))
+    write = load_counters(os.path.join(base, "pmc_write"))
+    valu = load_counters(os.path.join(base, "pmc_valu"))
+    cyc = load_counters(os.path.join(base, "pmc_cyc"))
+    lines += ["", "## PMC counters, steady-state launches (largest grid), per launch", "",
+              "| kernel | launches | grid | VGPR | FETCH_SIZE KB (raw) | WRITE_SIZE KB | HBM bytes (2xFETCH+WRITE) "
+              "| SQ_WAVES | VALU instr/wave | SALU instr/wave | LDS instr/wave | eff. clock GHz | VALU cyc/instr/SIMD |",
+              "|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
+    traffic = {}
+    for kern in ("k_terms", "k_msm_points", "k_combine", "k_tree", "k_prep_range", "k_prep_ipa"):
+        f, w, v, c = steady(fetch, kern), steady(write, kern), steady(valu, kern), steady(cyc, kern)
+        if not f:
+            continue
+        fk = mean([x.get("FETCH_SIZE", 0) for x in f])
+        wk = mean([x.get("WRITE_SIZE", 0) for x in w])
+        hbm = (2 * fk + wk) * 1024
+        waves = mean([x.get("SQ_WAVES", 0) for x in v])
+        vi = mean([x.get("SQ_INSTS_VALU", 0) for x in v])
+        si = mean([x.get("SQ_INSTS_SALU", 0) for x in v])
+        li = mean([x.get("SQ_INSTS_LDS", 0) for x in v])
+        grbm = mean([x.get("GRBM_GUI_ACTIVE", 0) for x in c])
+        dur = mean([x["dur_ns"] for x in c])
+        clock = grbm / 8 / dur if dur else float("nan")        # GRBM_GUI_ACTIVE summed over 8 XCDs
+        cyc_per_instr = (grbm / 8) / (vi / 1024) if vi else float("nan")   # 1024 SIMDs
+        traffic[kern] = {"bytes_per_launch": hbm, "fetch_kb": fk, "write_kb": wk, "launches": len(f),
+                         "valu_instr_per_wave": vi / waves if waves else None, "eff_clock_ghz": clock}
+        lines.append(f"| {kern} | {len(f)} | {f[0]['grid']} | {f[0]['vgpr']} | {fk:.0f} | {wk:.0f} | {hbm:.3e} | "
+                     f"{waves:.0f} | {vi / waves:.0f} | {si / waves:.0f} | {li / waves:.0f} | {clock:.2f} | "
+                     f"{cyc_per_instr:.2f} |")
+    lines += ["", "Notes:",
+              "- `VALU cyc/instr/SIMD` = kernel cycles (GRBM_GUI_ACTIVE/8) / (SQ_INSTS_VALU / 1024 SIMDs): the "
+              "issue interval per SIMD; ~4.3 is the measured VOP3 issue floor on gfx950 at 8 waves/SIMD "
+              "(tools/ubench_int.hip), so values near it mean the kernel is VALU-issue bound.",
+              "- HBM bytes apply the gfx950 FETCH_SIZE x2 correction; the loads here are 16-B-per-lane "
+              "(dwordx4) gathers of 128-B points, partly served by L2/MALL, so treat absolute bytes as approximate."]
+    os.makedirs(os.path.dirname(out_md), exist_ok=True)
+    open(out_md, "w").write("\n".join(lines) + "\n")
+    json.dump({"tag": tag, **traffic}, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()
