@@ -235,11 +235,15 @@ bp::BatchView view_of(const hipbp_proof_batch* b) {
     return v;
 }
 
-// The verify pipeline: a ring of D = L_len + 1 batch slots.  Every tick launches ONE
-// k_terms over all in-flight batches (stage 0 of the newest, fold round r of the batch
-// pushed r ticks earlier, the final terms of the oldest), then the newest batch's MSM
-// tree, then ONE k_combine (fold combinations + final assembly).  Within a batch the
-// reference's order is kept exactly; across batches nothing depends on anything.
+// The verify pipeline: a ring of D = log2(n) + 2 batch slots.  Every tick launches ONE
+// k_terms over all in-flight batches (the newest batch's challenges/scalars, stage 0 of the
+// one before, fold round r of the batch pushed r+1 ticks earlier, the final terms of the
+// oldest), then ONE k_combine (the stage-0 batch's MSM trees, fold combinations, final
+// assembly).  Within a batch the reference's order is kept exactly; across batches nothing
+// depends on anything.  Stages of a batch with L fold rounds:
+//   0: RK_PREP            1: RK_STAGE0 | RK_TREE, RK_COMBINE r=0
+//   r+1 (1<=r<L): RK_ROUND r | RK_COMBINE r         L+1: RK_FINAL_TERMS | RK_FINAL
+// (L = 0: stage 1 also carries RK_FINAL_TERMS and RK_FINAL moves to stage 2, after the tree.)
 struct Pipeline {
     Engine* e = nullptr;
     hipStream_t s = nullptr;
@@ -263,7 +267,7 @@ struct Pipeline {
     hipError_t init(Engine* eng, hipStream_t st, size_t mb, int nn, bool range) {
         e = eng; s = st; maxB = mb; n = nn; range_mode = range;
         Lr = log2i((size_t)n);
-        D = Lr + 1;
+        D = (Lr > 0 ? Lr : 1) + 2;
         slots.resize(D);
         hipError_t r;
         if ((r = hipMalloc(&slots_dev, D * sizeof(bp::SlotDev))) != hipSuccess) return r;
@@ -323,51 +327,54 @@ struct Pipeline {
             BP_RET_ON(hipEventRecord(nw.copied, s));
             if (!range_mode)
                 BP_RET_ON(hipMemcpyAsync(nw.dev.ws.Pin, P_in, b->count * sizeof(ge25519), hipMemcpyDeviceToDevice, s));
-            if (tm) tm->mark(bp::KT_PREP, false, s);
-            bp::launch_prep(nw.dev.bv, nw.dev.ws, e->two_i, range_mode, s);
-            if (tm) tm->mark(bp::KT_PREP, true, s);
             nw.active = true;
             nw.stage = 0;
             nw.B = b->count;
         }
         bp::RegionList tr{}, cr{};
-        auto add = [](bp::RegionList& rl, int kind, int slot, int r, unsigned long long items) {
+        bool overflow = false;
+        auto add = [&overflow](bp::RegionList& rl, int kind, int slot, int r, unsigned long long items, unsigned align) {
             if (!items) return;
+            if (rl.count == bp::MAX_REGIONS) { overflow = true; return; }
             bp::Region& g = rl.reg[rl.count++];
             g.kind = kind; g.slot = slot; g.r = r; g.begin = rl.total; g.items = items;
-            rl.total += (items + 63) & ~63ull;   // regions start on wave boundaries
+            rl.total += (items + align - 1) & ~(unsigned long long)(align - 1);   // wave / block aligned
         };
-        for (int k = 0; k < D; k++) {
-            int idx = (head - k + D) % D;   // newest first
-            Slot& sl = slots[idx];
-            if (!sl.active) continue;
-            const bp::BatchView& bv = sl.dev.bv;
-            unsigned long long B = bv.B;
-            int L = bv.L_len, st = sl.stage;
-            if (st == 0) {
-                unsigned long long it = (range_mode ? B * 2 * n : 0) + (L > 0 ? B * 2 * n : 0) + B * 2;
-                add(tr, bp::RK_STAGE0, idx, 0, it);
+        for (int pass = 0; pass < 2; pass++) {   // pass 0: the (block-aligned) tree region first
+            for (int k = 0; k < D; k++) {
+                int idx = (head - k + D) % D;   // newest first
+                Slot& sl = slots[idx];
+                if (!sl.active) continue;
+                unsigned long long B = sl.dev.bv.B;
+                int L = sl.dev.bv.L_len, st = sl.stage;
+                if (pass == 0) {
+                    if (st == 1 && range_mode) add(cr, bp::RK_TREE, idx, 0, B * 2 * n, 256);
+                    continue;
+                }
+                int fin_terms = L > 0 ? L + 1 : 1, fin = L > 0 ? L + 1 : 2;
+                if (st == 0) add(tr, bp::RK_PREP, idx, 0, range_mode ? 2 * B : B, 64);
+                if (st == 1) {
+                    unsigned long long it = (range_mode ? B * 2 * n : 0) + (L > 0 ? B * 2 * n : 0) + B * 2;
+                    add(tr, bp::RK_STAGE0, idx, 0, it, 64);
+                }
+                if (st >= 2 && st <= L) add(tr, bp::RK_ROUND, idx, st - 1, B * 4 * (n >> st), 64);
+                if (st == fin_terms) add(tr, bp::RK_FINAL_TERMS, idx, 0, B * 2, 64);
+                if (st >= 1 && st <= L) add(cr, bp::RK_COMBINE, idx, st - 1, B * 2 * (n >> st), 64);
+                if (st == fin) add(cr, bp::RK_FINAL, idx, 0, B, 64);
             }
-            if (st >= 1 && st <= L - 1) add(tr, bp::RK_ROUND, idx, st, B * 4 * (n >> (st + 1)));
-            if (st == L) add(tr, bp::RK_FINAL_TERMS, idx, 0, B * 2);
-            if (st <= L - 1) add(cr, bp::RK_COMBINE, idx, st, B * 2 * (n >> (st + 1)));
-            if (st == L) add(cr, bp::RK_FINAL, idx, 0, B);
         }
+        if (overflow) { g_err = "pipeline region list overflow (internal)"; return HIPBP_ERR_ARG; }
         if (tm) tm->mark(bp::KT_TERMS, false, s);
-        bp::launch_terms(tr, slots_dev, G, H, h, e->dtab, s);
+        bp::launch_terms(tr, slots_dev, G, H, h, e->dtab, e->two_i, s);
         if (tm) tm->mark(bp::KT_TERMS, true, s);
-        if (has && range_mode) {
-            if (tm) tm->mark(bp::KT_TREE, false, s);
-            bp::launch_tree(nw.dev.ws.msm_part, nw.dev.ws.msm_pts, (int)(2 * nw.B), (size_t)n, s);
-            if (tm) tm->mark(bp::KT_TREE, true, s);
-        }
         if (tm) tm->mark(bp::KT_COMBINE, false, s);
         bp::launch_combine(cr, slots_dev, s);
         if (tm) tm->mark(bp::KT_COMBINE, true, s);
         BP_RET_ON(hipGetLastError());
         for (auto& sl : slots) {
             if (!sl.active) continue;
-            if (sl.stage == sl.dev.bv.L_len) sl.active = false;
+            int L = sl.dev.bv.L_len;
+            if (sl.stage == (L > 0 ? L + 1 : 2)) sl.active = false;
             else sl.stage++;
         }
         head = (head + 1) % D;

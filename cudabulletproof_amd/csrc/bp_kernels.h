@@ -57,7 +57,11 @@ struct SlotDev {
 };
 
 // A tick's work list: region k covers items [begin_k, begin_{k+1}) of one slot at one stage.
-enum RegionKind { RK_STAGE0 = 0, RK_ROUND = 1, RK_FINAL_TERMS = 2, RK_COMBINE = 3, RK_FINAL = 4 };
+// k_terms regions: RK_PREP (challenges/scalars, one lane per proof and kind), RK_STAGE0,
+// RK_ROUND, RK_FINAL_TERMS.  k_combine regions: RK_TREE (block-level MSM tree; always first,
+// 256-aligned), RK_COMBINE, RK_FINAL.
+enum RegionKind { RK_STAGE0 = 0, RK_ROUND = 1, RK_FINAL_TERMS = 2, RK_COMBINE = 3, RK_FINAL = 4, RK_PREP = 5,
+                  RK_TREE = 6 };
 struct Region {
     int kind;
     int slot;
@@ -78,9 +82,8 @@ struct RegionList {
 enum KernelKind { KT_PREP = 0, KT_TERMS, KT_TREE, KT_COMBINE, KT_COUNT };
 
 void launch_init_tables(ge* dtab, fe* two_i, int nmax, hipStream_t s);
-void launch_prep(const BatchView& bv, const VerifyWs& ws, const fe* two_i, bool range_mode, hipStream_t s);
 void launch_terms(const RegionList& rl, const SlotDev* slots, const ge* G, const ge* H, const ge* h,
-                  const ge* dtab, hipStream_t s);
+                  const ge* dtab, const fe* two_i, hipStream_t s);
 void launch_combine(const RegionList& rl, const SlotDev* slots, hipStream_t s);
 
 // Generic canonical-tree MSM: out[seg] for S segments of m points each.

@@ -97,9 +97,8 @@ __device__ __forceinline__ fe challenge_digest(sha256_ctx& c) {
 
 // cuda_range_proof_verify (crv:93-106) + calculate_inner_product_point scalars
 // (bulletproof_range_proof.cu:679-718): one lane per proof.
-__global__ __launch_bounds__(TPB) void k_prep_range(BatchView bv, VerifyWs ws, const fe* __restrict__ two_i) {
-    size_t p = gid();
-    if (p >= (size_t)bv.B) return;
+__device__ __forceinline__ void prep_range_task(const BatchView& bv, const VerifyWs& ws, const fe* __restrict__ two_i,
+                                             size_t p) {
     const int n = bv.n;
     sha256_ctx c;
     // y = H("BulletproofYChal" || V.X V.Y A.X A.Y S.X S.Y || "y_ch")   (challenge.cu:24-44)
@@ -130,9 +129,7 @@ __global__ __launch_bounds__(TPB) void k_prep_range(BatchView bv, VerifyWs ws, c
 }
 
 // cuda_inner_product_verify (crv:146-218): <a,b> check and the per-round challenges.
-__global__ __launch_bounds__(TPB) void k_prep_ipa(BatchView bv, VerifyWs ws) {
-    size_t p = gid();
-    if (p >= (size_t)bv.B) return;
+__device__ __forceinline__ void prep_ipa_task(const BatchView& bv, const VerifyWs& ws, size_t p) {
     const int abl = bv.ab_len, Lr = bv.L_len;
     fe acc = fe_set(0);
     for (int i = 0; i < abl; i++) acc = fe_add(acc, fe_mul(bv.a[p * abl + i], bv.b[p * abl + i]));   // vectors.cu:101
@@ -258,7 +255,8 @@ __device__ __forceinline__ Region find_region(const RegionList& rl, size_t i) {
 // worth of independent work however deep the batch-level dependency chain is.
 __global__ __launch_bounds__(TPB) void k_terms(RegionList rl, const SlotDev* __restrict__ slots,
                                                const ge* __restrict__ G, const ge* __restrict__ H,
-                                               const ge* __restrict__ h, const ge* __restrict__ dtab) {
+                                               const ge* __restrict__ h, const ge* __restrict__ dtab,
+                                               const fe* __restrict__ two_i) {
     __shared__ geq qs[TPB];
     size_t i = gid();
     if (i >= rl.total) return;
@@ -266,7 +264,12 @@ __global__ __launch_bounds__(TPB) void k_terms(RegionList rl, const SlotDev* __r
     size_t l = i - rg.begin;
     if (l >= rg.items) return;
     const SlotDev& sd = slots[rg.slot];
-    if (rg.kind == RK_STAGE0) {
+    if (rg.kind == RK_PREP) {
+        // lanes [0,B): range-proof challenges and MSM scalars (range mode only), then [.., +B): IPA
+        const size_t B = sd.bv.B;
+        if (sd.range_mode && l < B) prep_range_task(sd.bv, sd.ws, two_i, l);
+        else prep_ipa_task(sd.bv, sd.ws, sd.range_mode ? l - B : l);
+    } else if (rg.kind == RK_STAGE0) {
         stage0_task(sd, l, &qs[threadIdx.x], G, H, h, dtab);
     } else if (rg.kind == RK_ROUND) {
         const int np = sd.bv.n >> (rg.r + 1);
@@ -324,13 +327,28 @@ __device__ __forceinline__ void final_task(const SlotDev& sd, size_t p) {
 
 // One pipeline tick's point combinations: fold round r  G'_j = N(term(u^-1 G_j) + term(u G_{j+n'})),
 // H'_j = N(term(u H_j) + term(u^-1 H_{j+n'}))  (crv:230, :240), or the final assembly.
+// The RK_TREE region (if any) comes first and spans whole blocks: each block folds TPB/n
+// segments of the batch's 2B MSMs with the canonical tree of k_tree, barriers block-uniform.
 __global__ __launch_bounds__(TPB) void k_combine(RegionList rl, const SlotDev* __restrict__ slots) {
     size_t i = gid();
     if (i >= rl.total) return;
     const Region rg = find_region(rl, i);
     size_t l = i - rg.begin;
-    if (l >= rg.items) return;
     const SlotDev& sd = slots[rg.slot];
+    if (rg.kind == RK_TREE) {
+        __shared__ ge sh[TPB];
+        const int n = sd.bv.n, tid = threadIdx.x, idx = tid & (n - 1);
+        const bool live = l < rg.items;
+        if (live) sh[tid] = sd.ws.msm_pts[l];
+        __syncthreads();
+        for (int st = 1; st < n; st <<= 1) {
+            if (live && (idx % (2 * st)) == 0) sh[tid] = ge_norm_dev(ge_add(sh[tid], sh[tid + st]));
+            __syncthreads();
+        }
+        if (live && idx == 0) sd.ws.msm_part[l / n] = sh[tid];
+        return;
+    }
+    if (l >= rg.items) return;
     if (rg.kind == RK_COMBINE) {
         const int n = sd.bv.n, np = n >> (rg.r + 1);
         size_t p = l / (2 * np);
@@ -347,14 +365,9 @@ __global__ __launch_bounds__(TPB) void k_combine(RegionList rl, const SlotDev* _
 
 static inline unsigned nblk(size_t items) { return (unsigned)((items + TPB - 1) / TPB); }
 
-void launch_prep(const BatchView& bv, const VerifyWs& ws, const fe* two_i, bool range_mode, hipStream_t s) {
-    if (range_mode) k_prep_range<<<nblk(bv.B), TPB, 0, s>>>(bv, ws, two_i);
-    k_prep_ipa<<<nblk(bv.B), TPB, 0, s>>>(bv, ws);
-}
-
 void launch_terms(const RegionList& rl, const SlotDev* slots, const ge* G, const ge* H, const ge* h,
-                  const ge* dtab, hipStream_t s) {
-    if (rl.total) k_terms<<<nblk(rl.total), TPB, 0, s>>>(rl, slots, G, H, h, dtab);
+                  const ge* dtab, const fe* two_i, hipStream_t s) {
+    if (rl.total) k_terms<<<nblk(rl.total), TPB, 0, s>>>(rl, slots, G, H, h, dtab, two_i);
 }
 
 void launch_combine(const RegionList& rl, const SlotDev* slots, hipStream_t s) {
