@@ -43,7 +43,7 @@ void launch_init_tables(ge* dtab, fe* two_i, int nmax, hipStream_t s) {
 // ------------------------------------------------------------------ MSM
 // pts[seg*m + i] = Ndev(scalarmult(rawbytes(scal[seg*m+i]), P[i])) — point_scalar_mul_kernel
 // (cuda_bulletproof_kernels.cu:26-42); the scalar bytes are the raw limbs (device tobytes).
-__global__ __launch_bounds__(TPB) void k_msm_points(ge* pts, const fe* __restrict__ scal,
+__global__ __launch_bounds__(TPB, 3) void k_msm_points(ge* pts, const fe* __restrict__ scal,
                                                     const ge* __restrict__ P, size_t total, size_t m,
                                                     const ge* __restrict__ dtab) {
     __shared__ geq qs[TPB];
@@ -253,7 +253,7 @@ __device__ __forceinline__ Region find_region(const RegionList& rl, size_t i) {
 // One pipeline tick's scalar multiplications: every region is one in-flight batch at its
 // own stage (stage 0 / fold round r / final terms), so a launch carries a whole batch's
 // worth of independent work however deep the batch-level dependency chain is.
-__global__ __launch_bounds__(TPB) void k_terms(RegionList rl, const SlotDev* __restrict__ slots,
+__global__ __launch_bounds__(TPB, 3) void k_terms(RegionList rl, const SlotDev* __restrict__ slots,
                                                const ge* __restrict__ G, const ge* __restrict__ H,
                                                const ge* __restrict__ h, const ge* __restrict__ dtab,
                                                const fe* __restrict__ two_i) {

@@ -23,7 +23,7 @@ struct fe {
     uint64_t v[4];
 };
 
-#define BP_DEV __device__ __forceinline__
+#define BP_DEV __host__ __device__ __forceinline__
 
 constexpr uint64_t P0 = 0xFFFFFFFFFFFFFFEDull;   // curve25519_ops.cu:7-8
 constexpr uint64_t P3 = 0x7FFFFFFFFFFFFFFFull;
@@ -54,75 +54,119 @@ BP_DEV fe fe_lossy_sub_p(const fe& t) {
     return d;
 }
 
-BP_DEV fe fe_cond_sub_p(const fe& t, bool c) {
-    fe d = fe_lossy_sub_p(t);
-    fe r;
-#pragma unroll
-    for (int i = 0; i < 4; i++) r.v[i] = c ? d.v[i] : t.v[i];
-    return r;
+// m ? lossy_sub_p(t) : t, folded into the additions: with br1 = t0 < p0,
+// br2 = !br1 & t1 != 2^64-1, br3 = !br2 & t2 != 2^64-1 (the closed form above),
+//   out = t + m*(19, !br1, !br2, 2^63 + !br3)   (mod 2^64 per limb, no carries between limbs).
+BP_DEV fe fe_cond_sub_p(const fe& t, bool m) {
+    bool br1 = t.v[0] < P0;
+    bool br2 = !br1 & (t.v[1] != M64);
+    bool br3 = !br2 & (t.v[2] != M64);
+    fe o;
+    o.v[0] = t.v[0] + (m ? 19ull : 0ull);
+    o.v[1] = t.v[1] + (uint64_t)(m & !br1);
+    o.v[2] = t.v[2] + (uint64_t)(m & !br2);
+    o.v[3] = t.v[3] + (m ? (0x8000000000000000ull + (uint64_t)!br3) : 0ull);
+    return o;
+}
+
+// The fix-up shared by add and the product fold: (carry || t >= p) ? lossy_sub_p(t) : t,
+// with the compare masks of t >= p (curve25519_ops.cu:54-59) and of the borrow chain shared.
+BP_DEV fe fe_fix(const fe& t, bool carry) {
+    bool lt0 = t.v[0] < P0;              // br1
+    bool f1 = t.v[1] == M64, f2 = t.v[2] == M64;
+    bool top = (int64_t)t.v[3] < 0;
+    bool e3 = t.v[3] == P3;
+    bool m = carry | top | (e3 & f2 & f1 & !lt0);
+    bool br2 = !lt0 & !f1;
+    bool br3 = !br2 & !f2;
+    fe o;
+    o.v[0] = t.v[0] + (m ? 19ull : 0ull);
+    o.v[1] = t.v[1] + (uint64_t)(m & !lt0);
+    o.v[2] = t.v[2] + (uint64_t)(m & !br2);
+    o.v[3] = t.v[3] + (m ? (0x8000000000000000ull + (uint64_t)!br3) : 0ull);
+    return o;
+}
+
+// lo64(19 x) as two shift-adds (x + 16x, then + 2x).
+BP_DEV uint64_t mul19(uint64_t x) {
+#ifdef __HIP_DEVICE_COMPILE__
+    uint64_t y, z;
+    asm("v_lshl_add_u64 %0, %1, 4, %1" : "=v"(y) : "v"(x));
+    asm("v_lshl_add_u64 %0, %1, 1, %2" : "=v"(z) : "v"(x), "v"(y));
+    return z;
+#else
+    return x * 19ull;
+#endif
 }
 
 // host fe25519_tobytes (curve25519_ops.cu:220-251) minus the byte store: canonicalising limbs.
 BP_DEV fe fe_canon(const fe& t) { return fe_cond_sub_p(t, fe_ge_p(t)); }
 
-// fe25519_add (curve25519_ops.cu:41-68): exact 257-bit sum, then one lossy "- p".
+BP_DEV uint32_t lo32(uint64_t x) { return (uint32_t)x; }
+BP_DEV uint32_t hi32(uint64_t x) { return (uint32_t)(x >> 32); }
+BP_DEV uint64_t cat64(uint32_t lo, uint32_t hi) { return (uint64_t)lo | ((uint64_t)hi << 32); }
+
+// fe25519_add (curve25519_ops.cu:41-68): exact 257-bit sum (one 32-bit carry chain), then
+// one lossy "- p" when the sum carried out or is >= p.
 BP_DEV fe fe_add(const fe& f, const fe& g) {
     fe h;
-    uint64_t c = 0;
+    unsigned c = 0;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-        uint64_t s = f.v[i] + g.v[i];
-        uint64_t c1 = s < f.v[i];
-        uint64_t s2 = s + c;
-        uint64_t c2 = s2 < s;
-        h.v[i] = s2;
-        c = c1 | c2;
+        uint32_t l = __builtin_addc(lo32(f.v[i]), lo32(g.v[i]), c, &c);
+        uint32_t u = __builtin_addc(hi32(f.v[i]), hi32(g.v[i]), c, &c);
+        h.v[i] = cat64(l, u);
     }
-    return fe_cond_sub_p(h, (c != 0) | fe_ge_p(h));
+    return fe_fix(h, c != 0);
 }
 
-// fe25519_sub (curve25519_ops.cu:71-90): borrow = f_i < lo64(g_i + borrow) (lossy),
-// then, on a final borrow, temp_i += lo64(p_i + carry); carry = temp_i < p_i.
+// fe25519_sub (curve25519_ops.cu:71-90): t_i = f_i - g_i - br;  br = f_i < lo64(g_i + br).
+// The lossy borrow equals the true borrow except when g_i = 2^64-1 and br = 1 (g_i + br wraps
+// to 0 and the borrow is dropped).  Then, on a final borrow, the literal "+ p" pass:
+//   a0 = t0 + p0, cy = a0 < p0 (= t0 >= 19);  a_i = t_i + lo64(p_i + cy), cy = a_i < p_i
+// i.e. a_i = cy ? t_i : t_i - 1 and cy = a_i != 2^64-1 for i = 1, 2;  a3 = t3 + p3 + cy.
 BP_DEV fe fe_sub(const fe& f, const fe& g) {
     fe t;
-    uint64_t br = 0;
+    unsigned br = 0;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-        uint64_t gb = g.v[i] + br;
-        t.v[i] = f.v[i] - g.v[i] - br;
-        br = f.v[i] < gb;
+        unsigned b1, b2;
+        uint32_t l = __builtin_subc(lo32(f.v[i]), lo32(g.v[i]), br, &b1);
+        uint32_t u = __builtin_subc(hi32(f.v[i]), hi32(g.v[i]), b1, &b2);
+        t.v[i] = cat64(l, u);
+        br = b2 & !((g.v[i] == M64) & (br != 0));
     }
-    // "+ p" pass, literal form (p1 = p2 = 2^64-1: carry = temp != 2^64-1 there)
-    fe a;
-    a.v[0] = t.v[0] + P0;
-    uint64_t cy = a.v[0] < P0;
-    a.v[1] = t.v[1] + (M64 + cy);
-    cy = a.v[1] < M64;
-    a.v[2] = t.v[2] + (M64 + cy);
-    cy = a.v[2] < M64;
-    a.v[3] = t.v[3] + (P3 + cy);
-    fe r;
-#pragma unroll
-    for (int i = 0; i < 4; i++) r.v[i] = br ? a.v[i] : t.v[i];
-    return r;
+    const bool m = br != 0;
+    fe o;
+    o.v[0] = t.v[0] - (m ? 19ull : 0ull);
+    bool cy0 = t.v[0] >= 19;
+    o.v[1] = t.v[1] - (uint64_t)(m & !cy0);
+    bool cy1 = o.v[1] != M64;
+    o.v[2] = t.v[2] - (uint64_t)(m & !cy1);
+    bool cy2 = o.v[2] != M64;
+    o.v[3] = t.v[3] + (m ? (cy2 ? 0x8000000000000000ull : P3) : 0ull);
+    return o;
 }
 
 // Fold of the exact 512-bit product (curve25519_ops.cu:114-145):
 //   c = lo64(t4*19); t0 += c; cy = t0 < c;
 //   c = lo64(t_{i+4}*19 + cy); t_i += c; cy = t_i < c   (i = 1..3)
 //   if (cy || t >= p) lossy "- p"
+// Computed as one carry chain t_i + x_i + cy (x_i = lo64(19 t_{i+4})): the same sum; the
+// carry differs only when x_i = 2^64-1 and cy = 1 (c wraps to 0, the reference carries 0).
 BP_DEV fe fe_fold512(const uint64_t t[8]) {
     fe h;
-    uint64_t c = t[4] * 19ull;
-    h.v[0] = t[0] + c;
-    uint64_t cy = h.v[0] < c;
+    unsigned cy = 0;
 #pragma unroll
-    for (int i = 1; i < 4; i++) {
-        c = t[i + 4] * 19ull + cy;
-        h.v[i] = t[i] + c;
-        cy = h.v[i] < c;
+    for (int i = 0; i < 4; i++) {
+        uint64_t x = mul19(t[i + 4]);
+        unsigned k, c;
+        uint32_t l = __builtin_addc(lo32(t[i]), lo32(x), cy, &k);
+        uint32_t u = __builtin_addc(hi32(t[i]), hi32(x), k, &c);
+        h.v[i] = cat64(l, u);
+        cy = c & !((x == M64) & (cy != 0));
     }
-    return fe_cond_sub_p(h, (cy != 0) | fe_ge_p(h));
+    return fe_fix(h, cy != 0);
 }
 
 // Exact 256x256 -> 512-bit product, product scanning over 32-bit words with a
@@ -138,7 +182,7 @@ BP_DEV void mul512(uint64_t t[8], const fe& f, const fe& g) {
         b[2 * i] = (uint32_t)g.v[i];
         b[2 * i + 1] = (uint32_t)(g.v[i] >> 32);
     }
-#if BP_MUL_ASM
+#if BP_MUL_ASM && defined(__HIP_DEVICE_COMPILE__)   // host pass: the C form (host-side checks)
     mul512_asm(w, a, b);
 #else
     uint64_t acc = 0;

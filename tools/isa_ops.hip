@@ -1,0 +1,19 @@
+// isa_ops.hip — instruction-count probes (tools/isa_count.py): one field / point operation
+// per kernel, compiled for gfx950, so the VALU cost of each building block can be tracked.
+#include "../cudabulletproof_amd/csrc/ge25519_dev.h"
+using namespace bp;
+extern "C" __global__ void p_fe_add(fe* o, const fe* a, const fe* b) { o[threadIdx.x] = fe_add(a[threadIdx.x], b[threadIdx.x]); }
+extern "C" __global__ void p_fe_sub(fe* o, const fe* a, const fe* b) { o[threadIdx.x] = fe_sub(a[threadIdx.x], b[threadIdx.x]); }
+extern "C" __global__ void p_fe_mul(fe* o, const fe* a, const fe* b) { o[threadIdx.x] = fe_mul(a[threadIdx.x], b[threadIdx.x]); }
+extern "C" __global__ void p_fe_fold(fe* o, const uint64_t* t) {
+    uint64_t x[8];
+    for (int i = 0; i < 8; i++) x[i] = t[threadIdx.x * 8 + i];
+    o[threadIdx.x] = fe_fold512(x);
+}
+extern "C" __global__ void p_ge_dbl(ge* o, const ge* p) { o[threadIdx.x] = ge_dbl(p[threadIdx.x]); }
+extern "C" __global__ void p_ge_add_q(ge* o, const ge* p, const geq* q) { o[threadIdx.x] = ge_add_q(p[threadIdx.x], q[threadIdx.x]); }
+extern "C" __global__ void p_ge_add_sel(ge* o, const ge* p, const geq* q, const int* u) {
+    __shared__ geq qs[256];
+    qs[threadIdx.x] = q[threadIdx.x];
+    o[threadIdx.x] = ge_add_sel<true>(p[threadIdx.x], &qs[threadIdx.x], u[threadIdx.x] != 0);
+}
