@@ -62,6 +62,31 @@ def main():
     for r in stats:
         lines.append(f"| {short(r['Name'])} | {r['Calls']} | {float(r['AverageNs'])/1e6:.3f} | "
                      f"{float(r['MinNs'])/1e6:.3f} | {float(r['MaxNs'])/1e6:.3f} | {float(r['Percentage']):.1f} |")
+    # steady-state launches from the same kernel trace (largest grid = full pipeline ticks), next to
+    # the HIP-event average bench.py measured on the verify stream in the same run
+    trace = list(csv.DictReader(open(os.path.join(base, "trace", "run_kernel_trace.csv"))))
+    try:
+        bt = json.loads(open(os.path.join(base, "bench_trace.json")).read().strip().splitlines()[-1])
+        ev_kern, ev_ms = bt["roofline"]["kernel"], bt["roofline"]["avg_launch_ms"]
+    except (OSError, ValueError, KeyError, IndexError):
+        ev_kern, ev_ms = None, None
+    lines += ["", "## Steady-state launches (largest grid) from the kernel trace", "",
+              "| kernel | launches | grid | avg ms (rocprofv3) | avg ms (bench.py HIP events, same run) |",
+              "|---|---|---|---|---|"]
+    for kern in ("k_terms", "k_msm_points", "k_combine", "k_tree"):
+        ds = [r for r in trace if short(r["Kernel_Name"]) == kern]
+        if not ds:
+            continue
+        g = max(int(r["Grid_Size_X"]) for r in ds)
+        ss = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in ds if int(r["Grid_Size_X"]) == g]
+        ev = f"{ev_ms:.3f}" if kern == ev_kern and ev_ms else "—"
+        lines.append(f"| {kern} | {len(ss)} | {g} | {mean(ss) / 1e6:.3f} | {ev} |")
+    os.makedirs(os.path.join(ROOT, "profiles", f"raw_{tag}"), exist_ok=True)
+    for src, dst in (("trace/run_kernel_stats.csv", "kernel_stats.csv"), ("bench_trace.json", "bench_trace.json")):
+        try:
+            open(os.path.join(ROOT, "profiles", f"raw_{tag}", dst), "w").write(open(os.path.join(base, src)).read())
+        except OSError:
+            pass
     fetch = load_counters(os.path.join(base, "pmc_fetch"))
     write = load_counters(os.path.join(base, "pmc_write"))
     valu = load_counters(os.path.join(base, "pmc_valu"))
