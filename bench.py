@@ -13,7 +13,9 @@ Extra fields on the JSON line:
   roofline     the dominant kernel's algorithmic bytes / HIP-event launch time vs HBM peak
                (the path is VALU-integer bound; see DESIGN.md), PMC traffic when profiled;
   cpu_baseline the CPU restatement (oracle/, test infrastructure) on a bounded sample, 1 thread;
-  msm          2^20-point canonical-tree MSM points/s (BASELINE configs[2], per-point semantics).
+  msm          2^20-point canonical-tree MSM points/s (BASELINE configs[2], per-point semantics);
+               at N > 1 one MSM sharded over all ranks (cudabulletproof_amd/shard.py), strong scaling;
+  ipa          4096-element inner-product-argument verifies/s (BASELINE configs[3]), rank 0.
 """
 import argparse
 import json
@@ -42,6 +44,10 @@ def parse():
                          "oneshot: each step verifies one batch start to finish")
     ap.add_argument("--streams", type=int, default=2, help="oneshot mode: HIP streams batches rotate over")
     ap.add_argument("--msm-log2", type=int, default=20)
+    ap.add_argument("--ipa-n", type=int, default=4096, help="configs[3]: inner-product-argument size")
+    ap.add_argument("--ipa-batch", type=int, default=64, help="IPA proofs per pipeline tick")
+    ap.add_argument("--ipa-steps", type=int, default=4)
+    ap.add_argument("--no-ipa", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-msm", action="store_true")
@@ -109,6 +115,75 @@ def pmc_traffic(kernel):
         return d.get(kernel, {}).get("bytes_per_launch")
     except (OSError, ValueError):
         return None
+
+
+def msm_leg(args, dev, world, rank, T):
+    """2^k-point canonical-tree MSM; each rank holds its shard (shard.msm_shard_bounds) and the
+    roots meet in one all_gather + tree (bit-exact with one GPU).  Timed between barriers,
+    max over ranks."""
+    import torch
+    import torch.distributed as dist
+    from cudabulletproof_amd import shard, synth
+    nm = 1 << args.msm_log2
+    sc, pts = synth.msm_inputs(nm)
+    lo, hi = shard.msm_shard_bounds(nm, world, rank)
+    scd, ptd = T(sc[lo:hi]), T(pts[lo:hi])
+    del sc, pts
+    shard.sharded_msm(scd, ptd, nm)
+    torch.cuda.synchronize(dev)
+    reps = 3
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    for _ in range(reps):
+        res = shard.sharded_msm(scd, ptd, nm)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    mdt = (time.perf_counter() - t1) / reps
+    if world > 1:
+        t = torch.tensor([mdt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        mdt = float(t.item())
+    return {"metric": "MSM points/sec", "value": nm / mdt, "unit": "points/s", "points": nm,
+            "ms_per_msm": mdt * 1e3, "n_gpus": world, "scaling": "strong" if world > 1 else None,
+            "semantics": "canonical-tree per-point double-and-add (SURVEY A9); shards + all_gather + tree at N>1",
+            "result_digest": hex(int(res[0].item()) & 0xFFFFFFFF)}
+
+
+def ipa_leg(args, dev):
+    """configs[3]: cuda_inner_product_verify semantics at n = 4096 (P given), batches of
+    synthetic IPA proofs streamed through the pipeline in inner-product mode."""
+    import torch
+    import cudabulletproof_amd as bp
+    from cudabulletproof_amd import synth
+    n, B = args.ipa_n, args.ipa_batch
+    G, H, _, h = synth.generators(n, dev)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)
+    Gd, Hd, Qd = T(G), T(H), T(h)
+    nb = 2
+    batches = [bp.RangeProofBatch.from_numpy(n, synth.proofs(B, n, seed=90 + i), dev) for i in range(nb)]
+    Ps = [T(synth.proofs(B, 1, seed=70 + i)["V"]) for i in range(nb)]
+    oks = [torch.zeros(B, dtype=torch.uint8, device=dev) for _ in range(nb)]
+    stream = torch.cuda.Stream(dev)
+    pipe = bp.VerifyPipeline(B, n, Gd, Hd, Qd, range_mode=False, stream=stream)
+    for k in range(pipe.depth - 1):   # fill: every timed tick then completes one batch
+        pipe.push(batches[k % nb], oks[k % nb], P_in=Ps[k % nb])
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.ipa_steps):
+        pipe.push(batches[k % nb], oks[k % nb], P_in=Ps[k % nb])
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    pipe.flush()
+    torch.cuda.synchronize(dev)
+    pipe.close()
+    sm = 4 * (n - 1) + 3   # fold rounds + a0*G', b0*H', c*Q (crv:160-296)
+    return {"metric": f"{n}-element inner-product-argument verifies/sec", "value": B * args.ipa_steps / dt,
+            "unit": "verifies/s", "batch": B, "n": n, "ms_per_tick": dt / args.ipa_steps * 1e3,
+            "scalar_mults_per_verify": sm, "scalar_mults_per_s": B * args.ipa_steps * sm / dt,
+            "semantics": "cuda_inner_product_verify (crv:130), P given", "pipeline_depth": pipe.depth}
 
 
 def main():
@@ -210,21 +285,12 @@ def main():
     }
 
     msm = None
-    if not args.no_msm and rank == 0:
-        nm = 1 << args.msm_log2
-        sc, pts = synth.msm_inputs(nm)
-        scd, ptd = T(sc), T(pts)
-        res = torch.zeros(16, dtype=torch.int64, device=dev)
-        bp.msm(res, scd, ptd, stream=stream)
-        torch.cuda.synchronize(dev)
-        reps = 3
-        t1 = time.perf_counter()
-        for _ in range(reps):
-            bp.msm(res, scd, ptd, stream=stream)
-        torch.cuda.synchronize(dev)
-        mdt = (time.perf_counter() - t1) / reps
-        msm = {"metric": "MSM points/sec", "value": nm / mdt, "unit": "points/s", "points": nm,
-               "ms_per_msm": mdt * 1e3, "semantics": "canonical-tree per-point double-and-add (SURVEY A9)"}
+    if not args.no_msm:   # configs[2]; at N > 1 one MSM sharded over all ranks (strong scaling)
+        msm = msm_leg(args, dev, world, rank, T)
+
+    ipa = None
+    if not args.no_ipa and rank == 0:   # configs[3]: single-GPU
+        ipa = ipa_leg(args, dev)
 
     cpu = None
     if not args.no_cpu and rank == 0 and world == 1:
@@ -242,7 +308,7 @@ def main():
                        "parallelism": f"independent proof shards x{world}", "mode": args.mode,
                        "pipeline_depth": pipe.depth if pipe else None,
                        "proof_bytes": proof_bytes(n, 1), "passes_in_warmup_batch": passes_warm},
-            "roofline": roofline, "cpu_baseline": cpu, "msm": msm,
+            "roofline": roofline, "cpu_baseline": cpu, "msm": msm, "ipa": ipa,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

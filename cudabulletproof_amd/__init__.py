@@ -87,7 +87,7 @@ EXPORTS = [
     "cuda_batch_field_invert", "cuda_soa_field_add", "cuda_range_proof_verify", "cuda_inner_product_verify",
     "cuda_benchmark_multi_scalar_mul", "cuda_benchmark_inner_product", "cuda_benchmark_field_operations",
     "cuda_benchmark_range_proof", "hipbp_last_error", "hipbp_device_count", "hipbp_batch_range_proof_verify",
-    "hipbp_batch_inner_product_verify", "hipbp_msm", "hipbp_field_op", "hipbp_sync", "hipbp_timing_enable",
+    "hipbp_batch_inner_product_verify", "hipbp_msm", "hipbp_point_tree", "hipbp_field_op", "hipbp_sync", "hipbp_timing_enable",
     "hipbp_timing_collect", "hipbp_kernel_count", "hipbp_kernel_name", "hipbp_pipeline_create",
     "hipbp_pipeline_push", "hipbp_pipeline_flush", "hipbp_pipeline_depth", "hipbp_pipeline_destroy",
 ]
@@ -110,7 +110,7 @@ def lib():
         L.hipbp_last_error.restype = ctypes.c_char_p
         for f in ("cuda_range_proof_verify", "cuda_inner_product_verify"):
             getattr(L, f).restype = ctypes.c_bool
-        for f in ("hipbp_batch_range_proof_verify", "hipbp_batch_inner_product_verify", "hipbp_msm",
+        for f in ("hipbp_batch_range_proof_verify", "hipbp_batch_inner_product_verify", "hipbp_msm", "hipbp_point_tree",
                   "hipbp_field_op", "hipbp_sync", "hipbp_device_count"):
             getattr(L, f).restype = ctypes.c_int
         _lib = L
@@ -328,6 +328,12 @@ def msm(result, scalars, points, stream=None):
     """Canonical-tree MSM on CUDA tensors: result (16,), scalars (n,4), points (n,16)."""
     _chk(lib().hipbp_msm(_c(result.data_ptr()), _c(scalars.data_ptr()), _c(points.data_ptr()),
                          _sz(points.shape[0]), _stream_ptr(stream)))
+
+
+def point_tree(result, points, stream=None):
+    """Canonical tree over device points (the MSM's reduction half): result (16,), points (n,16)."""
+    _chk(lib().hipbp_point_tree(_c(result.data_ptr()), _c(points.data_ptr()), _sz(points.shape[0]),
+                                _stream_ptr(stream)))
 
 
 def field_op(op, r, a, b=None, stream=None):

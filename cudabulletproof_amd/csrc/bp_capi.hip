@@ -199,9 +199,13 @@ Engine& engine_or_exit() {
     return *e;
 }
 
-inline hipStream_t pick(void* s, Engine& e) { return s ? (hipStream_t)s : e.stream; }
+// Part-2 entry points run on the caller's stream; NULL is the default (null) stream, as for a
+// kernel launch — the stream torch reports as 0 — so work stays ordered with the caller's.
+inline hipStream_t pick(void* s, Engine&) { return (hipStream_t)s; }
 
 bool is_pow2(size_t n) { return n && !(n & (n - 1)); }
+
+constexpr size_t MAX_N = size_t(1) << 16;   // generators per proof (range bits / IPA length)
 
 int log2i(size_t n) {
     int k = 0;
@@ -212,7 +216,7 @@ int log2i(size_t n) {
 int check_batch(const hipbp_proof_batch* b, bool range_mode) {
     if (!b) { g_err = "null batch"; return HIPBP_ERR_ARG; }
     if (b->count == 0) return HIPBP_OK;
-    if (!is_pow2(b->n) || b->n > 256) { g_err = "n must be a power of two <= 256"; return HIPBP_ERR_ARG; }
+    if (!is_pow2(b->n) || b->n > MAX_N) { g_err = "n must be a power of two <= 65536"; return HIPBP_ERR_ARG; }
     if (b->ab_len < 1) { g_err = "ab_len must be >= 1"; return HIPBP_ERR_ARG; }
     if ((int)b->L_len > log2i(b->n)) { g_err = "L_len > log2(n)"; return HIPBP_ERR_ARG; }
     if (b->count > (size_t)1 << 24) { g_err = "batch too large"; return HIPBP_ERR_ARG; }
@@ -394,6 +398,7 @@ int run_verify(Engine& e, const hipbp_proof_batch* batch, const ge25519* P_in, c
                const ge25519* h, uint8_t* ok, ge25519* P_out, ge25519* chk_out, bool range_mode, hipStream_t s) {
     int rc = check_batch(batch, range_mode);
     if (rc != HIPBP_OK || batch->count == 0) return rc;
+    if (range_mode) BP_RET_ON(e.ensure_two((int)batch->n));
     auto key = std::make_tuple(s, (int)batch->n, range_mode);
     Pipeline*& pl = e.pipes[key];
     if (!pl) {
@@ -491,7 +496,14 @@ void* hipbp_pipeline_create(size_t max_batch, size_t n, int range_mode, const ge
     hipError_t err;
     Engine* e = engine_or_null(&err);
     if (!e) { g_err = std::string("engine: ") + hipGetErrorString(err); return nullptr; }
-    if (!is_pow2(n) || n > 256 || !G || !H || !h) { g_err = "pipeline: bad n or null generator"; return nullptr; }
+    if (!is_pow2(n) || n > MAX_N || !G || !H || !h) { g_err = "pipeline: bad n or null generator"; return nullptr; }
+    if (range_mode) {
+        std::lock_guard<std::mutex> lk(e->mu);
+        if ((err = e->ensure_two((int)n)) != hipSuccess) {
+            g_err = std::string("pipeline tables: ") + hipGetErrorString(err);
+            return nullptr;
+        }
+    }
     Pipeline* pl = new Pipeline();
     err = pl->init(e, pick(stream, *e), max_batch, (int)n, range_mode != 0);
     if (err != hipSuccess) {
@@ -544,6 +556,22 @@ int hipbp_msm(ge25519* result, const fe25519* scalars, const ge25519* points, si
     BP_RET_ON(e->scratch[2].need(nb * sizeof(bp::ge)));
     bp::launch_msm_full((bp::ge*)result, (const bp::fe*)scalars, (const bp::ge*)points, n, e->scratch[0].as<bp::ge>(),
                         e->scratch[1].as<bp::ge>(), e->scratch[2].as<bp::ge>(), e->dtab, pick(stream, *e));
+    BP_RET_ON(hipGetLastError());
+    return HIPBP_OK;
+}
+
+int hipbp_point_tree(ge25519* result, const ge25519* points, size_t n, void* stream) {
+    hipError_t err;
+    Engine* e = engine_or_null(&err);
+    BP_RET_ON(err);
+    if (n == 0) return HIPBP_OK;
+    if (!result || !points) { g_err = "null argument"; return HIPBP_ERR_ARG; }
+    std::lock_guard<std::mutex> lk(e->mu);
+    size_t nb = (n + 255) / 256;
+    BP_RET_ON(e->scratch[4].need(nb * sizeof(bp::ge)));
+    BP_RET_ON(e->scratch[5].need(nb * sizeof(bp::ge)));
+    bp::launch_tree_full((bp::ge*)result, (const bp::ge*)points, n, e->scratch[4].as<bp::ge>(),
+                         e->scratch[5].as<bp::ge>(), pick(stream, *e));
     BP_RET_ON(hipGetLastError());
     return HIPBP_OK;
 }

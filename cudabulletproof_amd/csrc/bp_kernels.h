@@ -70,7 +70,7 @@ struct Region {
     unsigned long long begin;
     unsigned long long items;   // lanes [begin+items, next begin) are wave-alignment padding
 };
-constexpr int MAX_REGIONS = 12;
+constexpr int MAX_REGIONS = 20;   // >= 2 + log2(MAX_N) stages in flight
 struct RegionList {
     int count;
     int pad;
@@ -98,6 +98,7 @@ void launch_ip_shared(fe* out, const fe* a, const fe* b, size_t n, hipStream_t s
 void launch_ip_grid(fe* out, fe* part, const fe* a, const fe* b, size_t n, hipStream_t s);
 void launch_ip_batch(fe* out, const fe* a, const fe* b, size_t n, size_t nvec, hipStream_t s);
 void launch_invert(fe* r, const fe* a, size_t count, hipStream_t s);
+void launch_tree_full(ge* result, const ge* in, size_t n, ge* part0, ge* part1, hipStream_t s);
 void launch_msm_full(ge* result, const fe* scal, const ge* P, size_t n, ge* ptsbuf, ge* part0, ge* part1,
                      const ge* dtab, hipStream_t s);
 }  // namespace bp

@@ -281,15 +281,33 @@ __global__ __launch_bounds__(TPB, 3) void k_terms(RegionList rl, const SlotDev* 
 
 __device__ __forceinline__ int absdiff(int a, int b) { return a > b ? a - b : b - a; }
 
+// Levels TPB, 2 TPB, ... of the canonical MSM tree over cnt chunk roots stored
+// `stride` apart (in place; the slot's own workspace).  Used when n > TPB.
+__device__ __forceinline__ ge tree_upper(ge* T, int cnt, int stride) {
+    for (int st = 1; st < cnt; st <<= 1)
+        for (int i = 0; i + st < cnt; i += 2 * st)
+            T[(size_t)i * stride] = ge_norm_dev(ge_add(T[(size_t)i * stride], T[(size_t)(i + st) * stride]));
+    return T[0];
+}
+
 // P assembly (rp.cu:785-801), check point (crv:257-278) and the tolerant accept rule
 // (crv:297-357).  One lane per proof.
 __device__ __forceinline__ void final_task(const SlotDev& sd, size_t p) {
     const VerifyWs& ws = sd.ws;
     ge P;
     if (sd.range_mode) {
+        ge m0, m1;
+        if (sd.bv.n > TPB) {   // upper tree levels over the per-block chunk roots (k_combine RK_TREE)
+            const int n = sd.bv.n;
+            m0 = tree_upper(ws.msm_pts + (p * 2 + 0) * n, n / TPB, TPB);
+            m1 = tree_upper(ws.msm_pts + (p * 2 + 1) * n, n / TPB, TPB);
+        } else {
+            m0 = ws.msm_part[p * 2 + 0];
+            m1 = ws.msm_part[p * 2 + 1];
+        }
         P = ge_zero();
-        P = ge_norm_host(ge_add(P, ws.msm_part[p * 2 + 0]));
-        P = ge_norm_host(ge_add(P, ws.msm_part[p * 2 + 1]));
+        P = ge_norm_host(ge_add(P, m0));
+        P = ge_norm_host(ge_add(P, m1));
         P = ge_norm_host(ge_add(P, ws.terms[p * 4 + 2]));
         P = ge_norm_host(P);
         P = ge_norm_host(P);
@@ -336,16 +354,22 @@ __global__ __launch_bounds__(TPB) void k_combine(RegionList rl, const SlotDev* _
     size_t l = i - rg.begin;
     const SlotDev& sd = slots[rg.slot];
     if (rg.kind == RK_TREE) {
+        // chunks of min(n, TPB) points: n <= TPB -> one MSM per chunk, root to msm_part;
+        // n > TPB -> the chunk root is written back in place at the chunk's first point and
+        // final_task runs the remaining levels (tree_upper).
         __shared__ ge sh[TPB];
-        const int n = sd.bv.n, tid = threadIdx.x, idx = tid & (n - 1);
+        const int n = sd.bv.n, ch = n < TPB ? n : TPB, tid = threadIdx.x, idx = tid & (ch - 1);
         const bool live = l < rg.items;
         if (live) sh[tid] = sd.ws.msm_pts[l];
         __syncthreads();
-        for (int st = 1; st < n; st <<= 1) {
+        for (int st = 1; st < ch; st <<= 1) {
             if (live && (idx % (2 * st)) == 0) sh[tid] = ge_norm_dev(ge_add(sh[tid], sh[tid + st]));
             __syncthreads();
         }
-        if (live && idx == 0) sd.ws.msm_part[l / n] = sh[tid];
+        if (live && idx == 0) {
+            if (n <= TPB) sd.ws.msm_part[l / n] = sh[tid];
+            else sd.ws.msm_pts[l] = sh[tid];
+        }
         return;
     }
     if (l >= rg.items) return;
@@ -493,10 +517,8 @@ void launch_invert(fe* r, const fe* a, size_t count, hipStream_t s) {
 }
 
 // Generic canonical-tree MSM on device: ptsbuf holds n points, part0/part1 ping-pong.
-void launch_msm_full(ge* result, const fe* scal, const ge* P, size_t n, ge* ptsbuf, ge* part0, ge* part1,
-                     const ge* dtab, hipStream_t s) {
-    launch_msm_points(ptsbuf, scal, P, n, dtab, s);
-    const ge* in = ptsbuf;
+// Canonical tree over n points (levels 1, 2, 4, ...: one k_tree launch per 256x reduction).
+void launch_tree_full(ge* result, const ge* in, size_t n, ge* part0, ge* part1, hipStream_t s) {
     size_t m = n;
     ge* bufs[2] = {part0, part1};
     int w = 0;
@@ -509,6 +531,12 @@ void launch_msm_full(ge* result, const fe* scal, const ge* P, size_t n, ge* ptsb
         m = nb;
         w ^= 1;
     }
+}
+
+void launch_msm_full(ge* result, const fe* scal, const ge* P, size_t n, ge* ptsbuf, ge* part0, ge* part1,
+                     const ge* dtab, hipStream_t s) {
+    launch_msm_points(ptsbuf, scal, P, n, dtab, s);
+    launch_tree_full(result, ptsbuf, n, part0, part1, s);
 }
 
 }  // namespace bp

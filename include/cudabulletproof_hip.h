@@ -10,7 +10,8 @@
  * (INTEGRATION.md).
  *
  * Part 2 is additive: batched, device-resident entry points (flat wire format,
- * explicit stream, error codes) used by the Python package and bench.py.
+ * explicit stream, error codes) used by the Python package and bench.py.  Every
+ * `void* stream` is a hipStream_t; NULL means the default (null) stream.
  *
  * The types are layout-identical to the reference's (curve25519_ops.h:15-25,
  * bulletproof_vectors.h:8-17, :65-74, bulletproof_range_proof.h:7-18); when the
@@ -152,6 +153,11 @@ void hipbp_pipeline_destroy(void* pipeline);
 
 /* Canonical-tree MSM on device buffers. */
 int hipbp_msm(ge25519* result, const fe25519* scalars, const ge25519* points, size_t n, void* stream);
+/* Canonical tree over n device points: for stride 1, 2, 4, ...: T[i] = Ndev(T[i] + T[i+stride])
+ * for i % (2 stride) == 0 and i + stride < n; result = T[0] (the reduction half of
+ * cuda_bulletproof_kernels.cu:45-115).  hipbp_msm = this tree over the per-point
+ * terms; a multi-GPU MSM combines per-rank shard roots with it. */
+int hipbp_point_tree(ge25519* result, const ge25519* points, size_t n, void* stream);
 /* Elementwise device field ops: op 0 add, 1 sub, 2 mul, 3 square (reference kernel quirk),
  * 4 SoA add (limbwise, no carry), 5 invert (host chain). */
 int hipbp_field_op(int op, fe25519* r, const fe25519* a, const fe25519* b, size_t count, void* stream);

@@ -296,6 +296,15 @@ void orc_msm_canon(orc_ge* r, const orc_fe* s, const orc_ge* P, size_t n) {
         orc_ge_scalarmult(&T[i], sb, &P[i]);
         orc_ge_normalize_dev(&T[i]);
     }
+    orc_point_tree(r, T, n);
+    free(T);
+}
+/* the reduction half of the GPU MSM: canonical pairwise tree, device normalize at each node
+ * (cuda_bulletproof_kernels.cu:45-58 / :162-168).  P is not modified. */
+void orc_point_tree(orc_ge* r, const orc_ge* P, size_t n) {
+    if (n == 0) return;
+    orc_ge* T = (orc_ge*)malloc(n * sizeof(orc_ge));
+    memcpy(T, P, n * sizeof(orc_ge));
     for (size_t st = 1; st < n; st *= 2)
         for (size_t i = 0; i + st < n; i += 2 * st) {
             orc_ge_add(&T[i], &T[i], &T[i + st]);

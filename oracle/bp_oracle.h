@@ -41,6 +41,7 @@ void orc_ge_normalize_dev(orc_ge* p);
 
 /* MSM */
 void orc_msm_canon(orc_ge* r, const orc_fe* s, const orc_ge* P, size_t n);   /* GPU MSM semantics (A9) */
+void orc_point_tree(orc_ge* r, const orc_ge* P, size_t n);                   /* the A9 tree alone */
 void orc_msm_cpu(orc_ge* r, const orc_fe* s, const orc_ge* P, size_t n);     /* vectors.cu:189 (A11) */
 void orc_inner_product(orc_fe* r, const orc_fe* a, const orc_fe* b, size_t n); /* vectors.cu:101 */
 void orc_ip_gpu(orc_fe* r, const orc_fe* a, const orc_fe* b, size_t n);        /* cuda_inner_product.cu:97 */

@@ -124,6 +124,12 @@ class Oracle(_Lib):
         self.f("msm_canon")(_p(r), _p(s), _p(P), _sz(len(P)))
         return r
 
+    def point_tree(self, P):
+        r = ge()
+        P = np.ascontiguousarray(P, np.uint64).reshape(-1, 16)
+        self.f("point_tree")(_p(r), _p(P), _sz(len(P)))
+        return r
+
     def msm_cpu(self, s, P):
         r = ge()
         s = np.ascontiguousarray(s, np.uint64)
@@ -190,6 +196,21 @@ class Oracle(_Lib):
         return bool(ok), P, chk, Gt, Ht
 
 
+    def cuda_inner_product_verify(self, n, a, b, c, L, R, x, P, G, H, Q, trace=False):
+        """orc_cuda_inner_product_verify -> (ok, check_point, Gtrace, Htrace)."""
+        a, b = np.ascontiguousarray(a, np.uint64).reshape(-1, 4), np.ascontiguousarray(b, np.uint64).reshape(-1, 4)
+        L, R = np.ascontiguousarray(L, np.uint64).reshape(-1, 16), np.ascontiguousarray(R, np.uint64).reshape(-1, 16)
+        chk = ge()
+        Gt = ge(max(n - 1, 1)) if trace else None
+        Ht = ge(max(n - 1, 1)) if trace else None
+        ok = self.f("cuda_inner_product_verify")(
+            _sz(n), _p(a), _p(b), _sz(len(a)), _p(np.ascontiguousarray(c, np.uint64)), _p(L), _p(R), _sz(len(L)),
+            _p(np.ascontiguousarray(x, np.uint64)), _p(np.ascontiguousarray(P, np.uint64)),
+            _p(np.ascontiguousarray(G, np.uint64)), _p(np.ascontiguousarray(H, np.uint64)),
+            _p(np.ascontiguousarray(Q, np.uint64)), _p(chk), _p(Gt) if trace else None, _p(Ht) if trace else None)
+        return bool(ok), chk, Gt, Ht
+
+
 class Reference(_Lib):
     """The reference's own host code (oracle/_ref/libbpref.so)."""
 
@@ -197,7 +218,7 @@ class Reference(_Lib):
 
     def __init__(self, path=REF_SO):
         super().__init__(path)
-        for n in ("prove", "cuda_range_proof_verify", "range_proof_verify"):
+        for n in ("prove", "cuda_range_proof_verify", "range_proof_verify", "ipa_prove", "cuda_inner_product_verify"):
             self.f(n).restype = ctypes.c_int
 
     def fe_op(self, name, *args):
@@ -272,6 +293,32 @@ class Reference(_Lib):
                            _p(np.ascontiguousarray(a0, np.uint64)), _p(np.ascontiguousarray(b0, np.uint64)),
                            _p(np.ascontiguousarray(c, np.uint64)), _p(Q), _p(Gt), _p(Ht), _p(chk))
         return Gt, Ht, chk
+
+
+    def ipa_prove(self, a, b, G, H, Q, c, transcript=None):
+        """inner_product_prove (bulletproof_vectors.cu:277) -> dict(a, b, L, R, x) or None."""
+        n = len(a)
+        a, b = np.ascontiguousarray(a, np.uint64), np.ascontiguousarray(b, np.uint64)
+        tr = np.zeros(32, np.uint8) if transcript is None else np.ascontiguousarray(transcript, np.uint8)
+        ao, bo, L, R, x = fe(n), fe(n), ge(max(n, 1)), ge(max(n, 1)), fe()
+        abl, ll = _sz(), _sz()
+        r = self.f("ipa_prove")(_p(a), _p(b), _sz(n), _p(np.ascontiguousarray(G, np.uint64)),
+                                _p(np.ascontiguousarray(H, np.uint64)), _p(np.ascontiguousarray(Q, np.uint64)),
+                                _p(np.ascontiguousarray(c, np.uint64)), _p(tr), _p(ao), _p(bo), ctypes.byref(abl),
+                                _p(L), _p(R), ctypes.byref(ll), _p(x))
+        if r != 0:
+            return None
+        return dict(a=ao[:abl.value].copy(), b=bo[:abl.value].copy(), L=L[:ll.value].copy(), R=R[:ll.value].copy(),
+                    x=x)
+
+    def cuda_inner_product_verify(self, n, a, b, c, L, R, x, P, G, H, Q):
+        a, b = np.ascontiguousarray(a, np.uint64).reshape(-1, 4), np.ascontiguousarray(b, np.uint64).reshape(-1, 4)
+        L, R = np.ascontiguousarray(L, np.uint64).reshape(-1, 16), np.ascontiguousarray(R, np.uint64).reshape(-1, 16)
+        return bool(self.f("cuda_inner_product_verify")(
+            _sz(n), _p(a), _p(b), _sz(len(a)), _p(np.ascontiguousarray(c, np.uint64)), _p(L), _p(R), _sz(len(L)),
+            _p(np.ascontiguousarray(x, np.uint64)), _p(np.ascontiguousarray(P, np.uint64)),
+            _p(np.ascontiguousarray(G, np.uint64)), _p(np.ascontiguousarray(H, np.uint64)),
+            _p(np.ascontiguousarray(Q, np.uint64))))
 
 
 def have_reference():

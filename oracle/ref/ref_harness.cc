@@ -334,3 +334,50 @@ extern "C" void ref_ipa_fold(const ge25519* G, const ge25519* H, size_t n, const
     free(Gc);
     free(Hc);
 }
+
+// inner_product_prove (bulletproof_vectors.cu:277) on caller vectors; the reference allocates the
+// proof's vectors itself (inner_product_proof_init) — copied out here and freed.
+// a_out/b_out hold the final (length-1) vectors, L/R hold log2(n) points each.
+extern "C" int ref_ipa_prove(const fe25519* a, const fe25519* b, size_t n, const ge25519* G, const ge25519* H,
+                             const ge25519* Q, const fe25519* c_in, const uint8_t* transcript32, fe25519* a_out,
+                             fe25519* b_out, size_t* ab_len, ge25519* L, ge25519* R, size_t* L_len, fe25519* x_out) {
+    FieldVector av = {(fe25519*)a, n}, bv = {(fe25519*)b, n};
+    PointVector Gv = {(ge25519*)G, n}, Hv = {(ge25519*)H, n};
+    InnerProductProof proof;
+    memset(&proof, 0, sizeof(proof));
+    quiet_begin();
+    inner_product_prove(&proof, &av, &bv, &Gv, &Hv, Q, c_in, transcript32);
+    quiet_end();
+    if (proof.a.elements == NULL) return -1;
+    *ab_len = proof.a.length;
+    *L_len = proof.L_len;
+    memcpy(a_out, proof.a.elements, proof.a.length * sizeof(fe25519));
+    memcpy(b_out, proof.b.elements, proof.b.length * sizeof(fe25519));
+    memcpy(L, proof.L.elements, proof.L_len * sizeof(ge25519));
+    memcpy(R, proof.R.elements, proof.L_len * sizeof(ge25519));
+    *x_out = proof.x;
+    inner_product_proof_free(&proof);
+    return 0;
+}
+
+// The notebook's cuda_inner_product_verify (crv:130) on a flat proof.
+extern "C" int ref_cuda_inner_product_verify(size_t n, const fe25519* a, const fe25519* b, size_t ab_len,
+                                             const fe25519* c, const ge25519* L, const ge25519* R, size_t L_len,
+                                             const fe25519* x, const ge25519* P, const ge25519* G, const ge25519* H,
+                                             const ge25519* Q) {
+    InnerProductProof p;
+    memset(&p, 0, sizeof(p));
+    p.n = n;
+    p.a.elements = (fe25519*)a; p.a.length = ab_len;
+    p.b.elements = (fe25519*)b; p.b.length = ab_len;
+    p.c = *c;
+    p.L.elements = (ge25519*)L; p.L.length = L_len;
+    p.R.elements = (ge25519*)R; p.R.length = L_len;
+    p.L_len = L_len;
+    p.x = *x;
+    PointVector Gv = {(ge25519*)G, n}, Hv = {(ge25519*)H, n};
+    quiet_begin();
+    bool ok = cuda_inner_product_verify(&p, P, &Gv, &Hv, Q);
+    quiet_end();
+    return ok ? 1 : 0;
+}

@@ -11,6 +11,14 @@ oracle/build_ref.sh) and records inputs + reference outputs as .npz (no pickles)
               reference proofs (generate_range_proof, deterministic RAND), the verdicts of
               cuda_range_proof_verify and range_proof_verify, P (calculate_inner_product_point),
               the IPA fold trace and the check point (crv:160-279 composed from reference primitives)
+  ipa4096.npz BASELINE configs[3]: inner_product_prove (bulletproof_vectors.cu:277)
+              at n = 4096 on SHA-derived a, b (ipa_vectors below), G/H = base points {1}/{2}, Q = h,
+              transcript 0^32; P = canonical-tree GPU-MSM semantics over (a||b, G||H).  The prover keeps
+              c = c_in, and with this arithmetic <a',b'> != c_in, so cuda_inner_product_verify would reject
+              at crv:146-158 before folding (recorded as ok_raw); the fold case sets c = <a',b'> (c_fix).
+              Recorded: the verdicts, the check point and the last 15 folded G'/H' (rounds 9-11).
+
+  python tests/golden/make_golden.py [ipa4096]   (argument: regenerate only that fixture)
 
 The survey's golden digests are reproduced by tests/test_oracle_golden.py.
 """
@@ -128,5 +136,41 @@ def main():
     print("fixtures written to", HERE)
 
 
+def ipa_vectors(n):
+    """a_i = SHA256("ipa-a" || i_le32), b_i = SHA256("ipa-b" || i_le32), byte 31 &= 0x7F, LE limbs."""
+    def vec(tag):
+        v = np.stack([np.frombuffer(hashlib.sha256(tag + i.to_bytes(4, "little")).digest(), "<u8")
+                      for i in range(n)]).astype(np.uint64)
+        v[:, 3] &= np.uint64(0x7FFFFFFFFFFFFFFF)
+        return v
+    return vec(b"ipa-a"), vec(b"ipa-b")
+
+
+def make_ipa4096():
+    po.build()
+    R = po.Reference()
+    n = 4096
+    a, b = ipa_vectors(n)
+    G, H = R.base_points(n, 1), R.base_points(n, 2)
+    _, Q = R.gh()
+    c_in = po.fe()
+    R.f("inner_product")(po._p(c_in), po._p(a), po._p(b), po._sz(n))
+    pr = R.ipa_prove(a, b, G, H, Q, c_in)
+    c_fix = po.fe()
+    R.f("inner_product")(po._p(c_fix), po._p(pr["a"]), po._p(pr["b"]), po._sz(len(pr["a"])))
+    P = R.msm("msm_canon", np.concatenate([a, b]), np.concatenate([G, H]))
+    ok_raw = R.cuda_inner_product_verify(n, pr["a"], pr["b"], c_in, pr["L"], pr["R"], pr["x"], P, G, H, Q)
+    ok = R.cuda_inner_product_verify(n, pr["a"], pr["b"], c_fix, pr["L"], pr["R"], pr["x"], P, G, H, Q)
+    Gt, Ht, chk = R.ipa_fold(G, H, n, pr["x"], pr["L"], pr["R"], pr["a"][0], pr["b"][0], c_fix, Q)
+    np.savez_compressed(os.path.join(HERE, "ipa4096.npz"), n=np.array(n), c_in=c_in, c_fix=c_fix, a=pr["a"],
+                        b=pr["b"], L=pr["L"], R=pr["R"], x=pr["x"], P=P, ok=np.array(ok), ok_raw=np.array(ok_raw),
+                        check=chk, Gtail=Gt[-15:], Htail=Ht[-15:])
+    print("ipa4096: ok", ok, "ok_raw", ok_raw)
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["ipa4096"]:
+        make_ipa4096()
+    else:
+        main()
+        make_ipa4096()

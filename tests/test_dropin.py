@@ -25,7 +25,8 @@ def test_reference_driver_runs_on_our_library():
     env = dict(os.environ, BP_RAND_SEED="1")
     # line-buffered stdout: the driver ends in undefined behaviour of its own
     # (complete_bulletproof_test.cu:305 frees the never-initialised ip_proof of the rejected
-    # out-of-range proof), which can crash it after everything below is printed.
+    # out-of-range proof), which can crash it after everything below is printed:
+    # SIGSEGV, or SIGABRT from glibc's "free(): invalid pointer", depending on stack contents.
     p = subprocess.run(["stdbuf", "-oL", BIN], capture_output=True, text=True, timeout=300, env=env)
     out = p.stdout
     # complete_bulletproof_test.cu:179-191 / :247-255
@@ -34,4 +35,4 @@ def test_reference_driver_runs_on_our_library():
     assert "FAILED (CORRECT)" in out, out[-3000:]
     assert "CUDA FIELD OPERATIONS BENCHMARK" in out
     assert "CUDA field squaring:" in out           # the last GPU call the driver makes
-    assert p.returncode in (0, -11, 139), p.returncode
+    assert p.returncode in (0, -6, -11, 134, 139), p.returncode

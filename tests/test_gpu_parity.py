@@ -155,7 +155,8 @@ def test_batch_verify_matches_reference(bp, golden, n):
     assert np.array_equal(chk, d["check"])
 
 
-@pytest.mark.parametrize("n,B,ab_len", [(64, 48, 1), (16, 40, 3), (4, 17, 2), (1, 9, 1), (256, 4, 1)])
+@pytest.mark.parametrize("n,B,ab_len", [(64, 48, 1), (16, 40, 3), (4, 17, 2), (1, 9, 1), (256, 4, 1), (512, 3, 1),
+                                        (1024, 2, 2)])
 def test_batch_verify_synthetic_vs_oracle(bp, oracle, n, B, ab_len):
     from cudabulletproof_amd import synth
     arrays = synth.proofs(B, n, seed=1000 + n)
@@ -166,8 +167,8 @@ def test_batch_verify_synthetic_vs_oracle(bp, oracle, n, B, ab_len):
         for p in range(B):   # make <a,b> = c for most proofs, leave a few failing
             if p % 5:
                 arrays["c"][p] = oracle.inner_product(arrays["a"][p], arrays["b"][p])
-    arrays["c"][2] = rand_fe(rng, 1)[0]          # a <a,b> != c proof (crv:153 early reject)
-    arrays["t"][3] = 0                          # t = 0: 256 doublings of the identity
+    arrays["c"][B - 1] = rand_fe(rng, 1)[0]      # a <a,b> != c proof (crv:153 early reject)
+    arrays["t"][B // 2] = 0                     # t = 0: 256 doublings of the identity
     G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
     g, h = oracle.gh()
     ok, P, chk = _run_batch(bp, n, arrays, G, H, g, h)
@@ -245,3 +246,55 @@ def test_pipeline_inner_product_mode(bp, golden):
     assert np.array_equal(ok.cpu().numpy().astype(bool), d["ok_cuda"].astype(bool))
     assert np.array_equal(chk.cpu().numpy().view(np.uint64), d["check"])
     pipe.close()
+
+
+# ----------------------------------------------------------------------------- IPA n = 4096 (configs[3])
+def _ipa4096(golden, oracle):
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_golden import ipa_vectors  # noqa: F401  (vectors only matter for P, which is recorded)
+    d = golden("ipa4096")
+    n = int(d["n"])
+    G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+    _, Q = oracle.gh()
+    return d, n, G, H, Q
+
+
+def test_ipa4096_single_call_matches_reference(bp, golden, oracle):
+    """cuda_inner_product_verify (C ABI, host buffers) at n = 4096."""
+    d, n, G, H, Q = _ipa4096(golden, oracle)
+    z = np.zeros(100, np.uint64)
+    for c, want in ((d["c_fix"], d["ok"]), (d["c_in"], d["ok_raw"])):
+        head = z.copy()
+        head[92:96] = c
+        head[96:100] = d["x"]
+        proof = dict(head=head, a=d["a"], b=d["b"], L=d["L"], R=d["R"])
+        assert bp.cuda_inner_product_verify(proof, d["P"], G, H, Q) == bool(want)
+
+
+def test_ipa4096_batch_matches_reference(bp, golden, oracle):
+    """hipbp_batch_inner_product_verify over a batch of 4096-element IPAs: verdicts and the
+    check point equal the reference's; rejected-at-<a,b> proofs leave no check point."""
+    import torch
+    d, n, G, H, Q = _ipa4096(golden, oracle)
+    B = 6
+    dev = torch.device("cuda:0")
+    zero_pt = np.zeros((B, 16), np.uint64)
+    c = np.stack([d["c_fix"] if p % 3 else d["c_in"] for p in range(B)])
+    arrays = dict(V=zero_pt, A=zero_pt, S=zero_pt, T1=zero_pt, T2=zero_pt, t=np.zeros((B, 4), np.uint64),
+                  a=np.repeat(d["a"][None], B, 0), b=np.repeat(d["b"][None], B, 0), c=c,
+                  x=np.repeat(d["x"][None], B, 0), L=np.repeat(d["L"][None], B, 0), R=np.repeat(d["R"][None], B, 0))
+    batch = bp.RangeProofBatch.from_numpy(n, arrays, dev)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    ok = torch.zeros(B, dtype=torch.uint8, device=dev)
+    chk = torch.zeros(B, 16, dtype=torch.int64, device=dev)
+    bp.batch_inner_product_verify(batch, T(np.repeat(d["P"][None], B, 0)), T(G), T(H), T(Q), ok, chk)
+    torch.cuda.synchronize()
+    ok = ok.cpu().numpy().astype(bool)
+    chk = chk.cpu().numpy().view(np.uint64)
+    for p in range(B):
+        if p % 3:
+            assert ok[p] == bool(d["ok"]) and np.array_equal(chk[p], d["check"]), p
+        else:
+            assert ok[p] == bool(d["ok_raw"]), p

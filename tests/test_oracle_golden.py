@@ -82,3 +82,25 @@ def test_survey_proof_digests(golden):
         assert d8(head[88:92]) == t
         assert d8(d["P"][0]) == P
         assert d8(d["L"][0]) == L
+
+
+def test_ipa4096_against_reference(oracle, golden):
+    """BASELINE configs[3]: the 4096-element inner-product argument (reference prover + verifier)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_golden import ipa_vectors
+    d = golden("ipa4096")
+    n = int(d["n"])
+    G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+    _, Q = oracle.gh()
+    a, b = ipa_vectors(n)
+    assert np.array_equal(oracle.inner_product(a, b), d["c_in"])
+    ok, chk, Gt, Ht = oracle.cuda_inner_product_verify(n, d["a"], d["b"], d["c_fix"], d["L"], d["R"], d["x"], d["P"],
+                                                       G, H, Q, trace=True)
+    assert ok == bool(d["ok"])
+    assert np.array_equal(chk, d["check"])
+    assert np.array_equal(Gt[-15:], d["Gtail"]) and np.array_equal(Ht[-15:], d["Htail"])
+    ok_raw, _, _, _ = oracle.cuda_inner_product_verify(n, d["a"], d["b"], d["c_in"], d["L"], d["R"], d["x"], d["P"],
+                                                       G, H, Q)
+    assert ok_raw == bool(d["ok_raw"])
