@@ -4,7 +4,7 @@
 // functions are __host__ __device__; the host pass takes the C product, the device pass the
 // gfx950 asm columns) as HOST code and compares it with the oracle (oracle/bp_oracle.c) on
 // edge-heavy seeded inputs: fe_add, fe_sub, fe_mul (product + fold), fe_canon (tobytes),
-// fe_invert.  Prints "<op> <mismatches>" per op; exit status 1 on any mismatch.
+// fe_sq (dedicated squaring vs mul(f, f)), fe_invert.  Prints "<op> <mismatches>" per op; exit status 1 on any mismatch.
 #include <cstdio>
 #include <cstring>
 
@@ -54,7 +54,7 @@ int main(int argc, char** argv) {
     if ((uint64_t)(0x79435E50D79435E5ull * 19ull) != ~0ull) {
         printf("bad edge constant %llx\n", (unsigned long long)(0x79435E50D79435E5ull * 19ull));
     }
-    long bad_add = 0, bad_sub = 0, bad_mul = 0, bad_canon = 0, bad_inv = 0, bad_fold = 0;
+    long bad_sq = 0, bad_add = 0, bad_sub = 0, bad_mul = 0, bad_canon = 0, bad_inv = 0, bad_fold = 0;
     for (long it = 0; it < n; it++) {
         int mode = (int)(it % 3);
         fe f = gen(mode), g = gen((mode + 1) % 3);
@@ -67,6 +67,8 @@ int main(int argc, char** argv) {
         bad_sub += !same(bp::fe_sub(f, g), r);
         orc_fe_mul(&r, &of, &og);
         bad_mul += !same(bp::fe_mul(f, g), r);
+        orc_fe_mul(&r, &of, &of);
+        bad_sq += !same(bp::fe_sq(f), r);   // dedicated squaring == mul(f, f)
         uint8_t bytes[32];
         orc_fe_tobytes(bytes, &of);
         fe c = bp::fe_canon(f);
@@ -102,7 +104,7 @@ int main(int argc, char** argv) {
             bad_inv += !same(bp::fe_invert(f), r);
         }
     }
-    printf("add %ld\nsub %ld\nmul %ld\ncanon %ld\nfold %ld\ninvert %ld\n", bad_add, bad_sub, bad_mul, bad_canon,
-           bad_fold, bad_inv);
-    return (bad_add | bad_sub | bad_mul | bad_canon | bad_fold | bad_inv) ? 1 : 0;
+    printf("add %ld\nsub %ld\nmul %ld\nsq %ld\ncanon %ld\nfold %ld\ninvert %ld\n", bad_add, bad_sub, bad_mul,
+           bad_sq, bad_canon, bad_fold, bad_inv);
+    return (bad_add | bad_sub | bad_mul | bad_sq | bad_canon | bad_fold | bad_inv) ? 1 : 0;
 }

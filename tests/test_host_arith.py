@@ -21,6 +21,6 @@ def test_field_ops_host_pass_match_oracle(oracle, tmp_path):
                     "-Wl,-rpath," + os.path.join(ROOT, "oracle")], check=True, capture_output=True)
     r = subprocess.run([str(exe), "200000", "7"], capture_output=True, text=True, timeout=300)
     counts = dict(line.split() for line in r.stdout.split("\n") if line.strip())
-    assert set(counts) == {"add", "sub", "mul", "canon", "fold", "invert"}, r.stdout
+    assert set(counts) == {"add", "sub", "mul", "sq", "canon", "fold", "invert"}, r.stdout
     assert all(v == "0" for v in counts.values()), r.stdout
     assert r.returncode == 0
