@@ -106,12 +106,14 @@ BP_DEV fe qget(const fe* p) {
 }
 
 // ge25519_add(p, q) with q's prepared operands (same operation order as ge_add_q).
+// zone (wave-uniform): every lane's q.Z is exactly 1 (generators, host-normalized points), so
+// Z1*Z2 = fold(Z1 || 0) = the conditional lossy "- p" of Z1 (fe_mul_one) — same bits, no product.
 template <bool QLDS>
-BP_DEV ge ge_add_qp(const ge& p, const geq* q) {
+BP_DEV ge ge_add_qp(const ge& p, const geq* q, bool zone = false) {
     fe A = fe_mul(fe_sub(p.Y, p.X), qget<QLDS>(&q->YmX));
     fe B = fe_mul(fe_add(p.Y, p.X), qget<QLDS>(&q->YpX));
     fe C = fe_mul(fe_mul(p.T, qget<QLDS>(&q->T)), k_const());
-    fe D = fe_mul(p.Z, qget<QLDS>(&q->Z));
+    fe D = zone ? fe_mul_one(p.Z) : fe_mul(p.Z, qget<QLDS>(&q->Z));
     D = fe_add(D, D);
     fe E = fe_sub(B, A);
     fe F = fe_sub(D, C);
@@ -199,10 +201,11 @@ BP_DEV ge sm_uniform(const fe& s_in, const geq* q, const ge* __restrict__ dtab) 
     int lz = fe_clz256(s);
     ge r = ld_ge(&dtab[lz]);
     if (lz == 256) return r;
+    const bool zone = __all(fe_is_one(qget<QLDS>(&q->Z)));
     BitStream bs = bs_init(s, 255 - lz);
     for (int i = 255 - lz; i >= 0; i--) {
         r = ge_dbl(r);
-        if (bs_next(bs)) r = ge_add_qp<QLDS>(r, q);
+        if (bs_next(bs)) r = ge_add_qp<QLDS>(r, q, zone);
     }
     return r;
 }

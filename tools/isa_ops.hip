@@ -18,3 +18,8 @@ extern "C" __global__ void p_ge_add_sel(ge* o, const ge* p, const geq* q, const 
     o[threadIdx.x] = ge_add_sel<true>(p[threadIdx.x], &qs[threadIdx.x], u[threadIdx.x] != 0);
 }
 extern "C" __global__ void p_fe_sq(fe* o, const fe* a) { o[threadIdx.x] = fe_sq(a[threadIdx.x]); }
+extern "C" __global__ void p_ge_add_zone(ge* o, const ge* p, const geq* q) {
+    __shared__ geq qs[256];
+    qs[threadIdx.x] = q[threadIdx.x];
+    o[threadIdx.x] = ge_add_qp<true>(p[threadIdx.x], &qs[threadIdx.x], true);
+}
