@@ -107,14 +107,22 @@ def cpu_model():
     return "unknown"
 
 
-def pmc_traffic(kernel):
-    """Per-launch HBM bytes for `kernel` from the committed rocprofv3 PMC summary, if present."""
+def pmc(kernel, key):
+    """A per-launch PMC figure for `kernel` from the committed rocprofv3 summary, if present."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(path))
-        return d.get(kernel, {}).get("bytes_per_launch")
+        return d.get(kernel, {}).get(key)
     except (OSError, ValueError):
         return None
+
+
+# VALU issue peak (the binding resource of this path): 1024 SIMDs x 2.4 GHz / 4 cycles per
+# wave64 instruction.  A SIMD-32 issues a wave64 instruction in 2 passes; the integer
+# instructions the limb arithmetic is made of (v_mad_u64_u32, v_addc/v_add_co, v_cmp,
+# v_cndmask, v_lshl_add_u64, v_alignbit) take 4 cycles per wave-instruction (tools/ubench_enc.hip
+# measures 4.3-5.1 at the nominal clock); only plain 32-bit add/sub/logic/mov take 2.
+VALU_PEAK_WINSTR = 1024 * 2.4e9 / 4
 
 
 def msm_leg(args, dev, world, rank, T):
@@ -277,11 +285,19 @@ def main():
     achieved = (per_launch / (avg_ms * 1e-3)) / 1e9 if per_launch else None
     roofline = {
         "bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": pmc_traffic(dom),
+        "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": pmc(dom, "bytes_per_launch"),
         "avg_launch_ms": avg_ms, "launches": launches,
         "kernel_ms_share": {k: round(v / sum(kern_ms.values()), 4) for k, v in kern_ms.items()},
-        "binding": "VALU integer (not HBM, not MFMA): see DESIGN.md",
+        "binding": "VALU integer (not HBM, not MFMA): see DESIGN.md and valu_roofline",
         "scalar_mults_per_s": value * sm_per_verify(n),
+    }
+    vi = pmc(dom, "valu_instr_per_launch")
+    valu_roofline = {
+        "kernel": dom, "unit": "wave64 VALU instr/s", "peak": VALU_PEAK_WINSTR,
+        "instr_per_launch": vi, "achieved": vi / (avg_ms * 1e-3) if vi else None,
+        "frac": vi / (avg_ms * 1e-3) / VALU_PEAK_WINSTR if vi else None,
+        "valu_busy_pct": pmc(dom, "valu_busy_pct"),
+        "source": "SQ_INSTS_VALU per steady-state launch (profiles/pmc_traffic.json) / live HIP-event launch time",
     }
 
     msm = None
@@ -308,7 +324,7 @@ def main():
                        "parallelism": f"independent proof shards x{world}", "mode": args.mode,
                        "pipeline_depth": pipe.depth if pipe else None,
                        "proof_bytes": proof_bytes(n, 1), "passes_in_warmup_batch": passes_warm},
-            "roofline": roofline, "cpu_baseline": cpu, "msm": msm, "ipa": ipa,
+            "roofline": roofline, "valu_roofline": valu_roofline, "cpu_baseline": cpu, "msm": msm, "ipa": ipa,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -8,10 +8,12 @@ TAG=${1:-r01}
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-BENCH="python3 bench.py --steps 6 --warmup 2 --no-cpu --msm-log2 18"
+BENCH="python3 bench.py --steps 6 --warmup 2 --no-cpu --no-ipa --msm-log2 18"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- $BENCH > "$OUT/bench_trace.json" 2> "$OUT/trace.err"
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o run -- $BENCH > "$OUT/bench_fetch.json" 2> "$OUT/fetch.err"
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run -- $BENCH > "$OUT/bench_write.json" 2> "$OUT/write.err"
 timeout -k 10 400 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_LDS --kernel-trace --output-format csv -d "$OUT/pmc_valu" -o run -- $BENCH > "$OUT/bench_valu.json" 2> "$OUT/valu.err"
 timeout -k 10 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$OUT/pmc_cyc" -o run -- $BENCH > "$OUT/bench_cyc.json" 2> "$OUT/cyc.err"
-ls -R "$OUT" | head -40
+timeout -k 10 400 rocprofv3 --pmc VALUBusy VALUUtilization --kernel-trace --output-format csv -d "$OUT/pmc_busy" -o run -- $BENCH > "$OUT/bench_busy.json" 2> "$OUT/busy.err"
+timeout -k 10 400 rocprofv3 --pmc SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_ACTIVE_INST_VALU2 --kernel-trace --output-format csv -d "$OUT/pmc_mix" -o run -- $BENCH > "$OUT/bench_mix.json" 2> "$OUT/mix.err"
+ls -R "$OUT" > "$OUT/listing.txt"

@@ -56,7 +56,7 @@ def main():
     stats = list(csv.DictReader(open(os.path.join(base, "trace", "run_kernel_stats.csv"))))
     lines = [f"# rocprofv3 summary — {tag}", "",
              "Command: `tools/profile.sh " + tag + "` on one MI355X "
-             "(bench.py --steps 6 --warmup 2 --no-cpu --msm-log2 18 under rocprofv3).", "",
+             "(bench.py --steps 6 --warmup 2 --no-cpu --no-ipa --msm-log2 18 under rocprofv3).", "",
              "## Kernel trace (`rocprofv3 --kernel-trace --stats`)", "",
              "| kernel | calls | avg ms | min ms | max ms | % time |", "|---|---|---|---|---|---|"]
     for r in stats:
@@ -112,16 +112,37 @@ def main():
         clock = grbm / 8 / dur if dur else float("nan")        # GRBM_GUI_ACTIVE summed over 8 XCDs
         cyc_per_instr = (grbm / 8) / (vi / 1024) if vi else float("nan")   # 1024 SIMDs
         traffic[kern] = {"bytes_per_launch": hbm, "fetch_kb": fk, "write_kb": wk, "launches": len(f),
-                         "valu_instr_per_wave": vi / waves if waves else None, "eff_clock_ghz": clock}
+                         "valu_instr_per_wave": vi / waves if waves else None, "valu_instr_per_launch": vi,
+                         "eff_clock_ghz": clock}
         lines.append(f"| {kern} | {len(f)} | {f[0]['grid']} | {f[0]['vgpr']} | {fk:.0f} | {wk:.0f} | {hbm:.3e} | "
                      f"{waves:.0f} | {vi / waves:.0f} | {si / waves:.0f} | {li / waves:.0f} | {clock:.2f} | "
                      f"{cyc_per_instr:.2f} |")
+    busy = load_counters(os.path.join(base, "pmc_busy")) if os.path.isdir(os.path.join(base, "pmc_busy")) else {}
+    mix = load_counters(os.path.join(base, "pmc_mix")) if os.path.isdir(os.path.join(base, "pmc_mix")) else {}
+    if busy:
+        lines += ["", "## VALU roofline (the binding resource), steady-state launches", "",
+                  "| kernel | VALUBusy % | VALUUtilization % | INT32 VALU instr/wave | INT64 VALU instr/wave | "
+                  "dual-issue quad-cycles/wave |", "|---|---|---|---|---|---|"]
+        for kern in ("k_terms", "k_msm_points", "k_combine", "k_tree"):
+            b, x, v = steady(busy, kern), steady(mix, kern), steady(valu, kern)
+            if not b:
+                continue
+            vb = mean([d.get("VALUBusy", float("nan")) for d in b])
+            vu = mean([d.get("VALUUtilization", float("nan")) for d in b])
+            waves = mean([d.get("SQ_WAVES", 0) for d in v]) or float("nan")
+            i32 = mean([d.get("SQ_INSTS_VALU_INT32", float("nan")) for d in x]) / waves if x else float("nan")
+            i64 = mean([d.get("SQ_INSTS_VALU_INT64", float("nan")) for d in x]) / waves if x else float("nan")
+            v2 = mean([d.get("SQ_ACTIVE_INST_VALU2", float("nan")) for d in x]) / waves if x else float("nan")
+            traffic.setdefault(kern, {}).update({"valu_busy_pct": vb, "valu_utilization_pct": vu})
+            lines.append(f"| {kern} | {vb:.1f} | {vu:.1f} | {i32:.0f} | {i64:.0f} | {v2:.0f} |")
     lines += ["", "Notes:",
               "- `VALU cyc/instr/SIMD` = kernel cycles (GRBM_GUI_ACTIVE/8) / (SQ_INSTS_VALU / 1024 SIMDs): the "
               "issue interval per SIMD; ~4.3 is the measured VOP3 issue floor on gfx950 at 8 waves/SIMD "
               "(tools/ubench_int.hip), so values near it mean the kernel is VALU-issue bound.",
               "- HBM bytes apply the gfx950 FETCH_SIZE x2 correction; the loads here are 16-B-per-lane "
-              "(dwordx4) gathers of 128-B points, partly served by L2/MALL, so treat absolute bytes as approximate."]
+              "(dwordx4) gathers of 128-B points, partly served by L2/MALL, so treat absolute bytes as approximate.",
+              "- VALUBusy = 100 * SQ_ACTIVE_INST_VALU / CU_NUM / GRBM_GUI_ACTIVE (rocprofv3 derived metric): the share "
+              "of kernel time the CUs' vector ALUs are issuing; VALUUtilization = active lanes per VALU instruction."]
     os.makedirs(os.path.dirname(out_md), exist_ok=True)
     open(out_md, "w").write("\n".join(lines) + "\n")
     json.dump({"tag": tag, **traffic}, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
