@@ -74,6 +74,18 @@ int orc_cuda_inner_product_verify(size_t n, const orc_fe* a, const orc_fe* b, si
                                   const orc_fe* x, const orc_ge* P, const orc_ge* G, const orc_ge* H,
                                   const orc_ge* Q, orc_ge* check_out, orc_ge* Gtrace, orc_ge* Htrace);
 
+/* range_proof_verify (bulletproof_range_proof.cu:1717): the reference's CPU verify.
+ * head->V is the proof's V, V the caller's.  det (nullable) receives every intermediate. */
+typedef struct {
+    int vmatch, range_ok, poly_ok, poly_m1, poly_m2, poly_m3, poly_m4, ip_ok;
+    orc_fe delta;
+    orc_ge left, right, left_mult, right_mult, P, check;
+} orc_rpv_detail;
+
+int orc_range_proof_verify(const orc_head* head, const orc_ge* V, size_t n, const orc_fe* a, const orc_fe* b,
+                           size_t ab_len, const orc_ge* L, const orc_ge* R, size_t L_len, const orc_ge* G,
+                           const orc_ge* H, const orc_ge* g, const orc_ge* h, orc_rpv_detail* det);
+
 #ifdef __cplusplus
 }
 #endif

@@ -64,6 +64,7 @@ class Oracle(_Lib):
         super().__init__(path)
         self.lib.orc_cuda_range_proof_verify.restype = ctypes.c_int
         self.lib.orc_cuda_inner_product_verify.restype = ctypes.c_int
+        self.lib.orc_range_proof_verify.restype = ctypes.c_int
 
     # field ------------------------------------------------------------
     def _fe2(self, name, f, g):
@@ -211,6 +212,28 @@ class Oracle(_Lib):
         return bool(ok), chk, Gt, Ht
 
 
+    RPV_KEYS = ("vmatch", "range_ok", "poly_ok", "poly_m1", "poly_m2", "poly_m3", "poly_m4", "ip_ok")
+    RPV_PTS = ("left", "right", "left_mult", "right_mult", "P", "check")
+
+    def range_proof_verify(self, head, V, n, a, b, L, R, G, H, g, h):
+        """orc_range_proof_verify (rp.cu:1717 semantics) -> (ok, detail dict)."""
+        head = np.ascontiguousarray(head, np.uint64)
+        a, b = np.ascontiguousarray(a, np.uint64).reshape(-1, 4), np.ascontiguousarray(b, np.uint64).reshape(-1, 4)
+        L, R = np.ascontiguousarray(L, np.uint64).reshape(-1, 16), np.ascontiguousarray(R, np.uint64).reshape(-1, 16)
+        det = np.zeros(8 * 4 + 32 + 6 * 128, np.uint8)
+        ok = self.f("range_proof_verify")(
+            _p(head), _p(np.ascontiguousarray(V, np.uint64)), _sz(n), _p(a), _p(b), _sz(len(a)), _p(L), _p(R),
+            _sz(len(L)), _p(np.ascontiguousarray(G, np.uint64)), _p(np.ascontiguousarray(H, np.uint64)),
+            _p(np.ascontiguousarray(g, np.uint64)), _p(np.ascontiguousarray(h, np.uint64)), _p(det))
+        flags = det[:32].view(np.int32)
+        d = {k: bool(flags[i]) for i, k in enumerate(self.RPV_KEYS)}
+        d["delta"] = det[32:64].view(np.uint64).copy()
+        pts = det[64:].view(np.uint64).reshape(6, 16)
+        for i, k in enumerate(self.RPV_PTS):
+            d[k] = pts[i].copy()
+        return bool(ok), d
+
+
 class Reference(_Lib):
     """The reference's own host code (oracle/_ref/libbpref.so)."""
 
@@ -319,6 +342,14 @@ class Reference(_Lib):
             _p(np.ascontiguousarray(x, np.uint64)), _p(np.ascontiguousarray(P, np.uint64)),
             _p(np.ascontiguousarray(G, np.uint64)), _p(np.ascontiguousarray(H, np.uint64)),
             _p(np.ascontiguousarray(Q, np.uint64))))
+
+
+    def rpv_parts(self, pr, n, G, H, g, h):
+        """range_proof_verify's sub-checks, each the reference's own function -> (delta, flags):
+        flags bit0 enhanced_range_check, bit1 robust_polynomial_identity_check, bit2 inner_product_verify."""
+        delta, flags = fe(), ctypes.c_int()
+        self.f("rpv_parts")(*self._vargs(pr, n, G, H, g, h), _p(delta), ctypes.byref(flags))
+        return delta, flags.value
 
 
 def have_reference():

@@ -381,3 +381,38 @@ extern "C" int ref_cuda_inner_product_verify(size_t n, const fe25519* a, const f
     quiet_end();
     return ok ? 1 : 0;
 }
+
+// ---- range_proof_verify (bulletproof_range_proof.cu:1717) sub-checks, each the
+// reference's own function on a flat proof, for pinning the restatement step by step.
+bool enhanced_range_check(const fe25519* t, const fe25519* delta, const fe25519* z, const ge25519* V,
+                          const ge25519* g, const ge25519* h, size_t n);   // rp.cu:765 (not in the header)
+
+// out: delta (32 B fe), flags bit0 enhanced_range_check, bit1 robust_polynomial_identity_check,
+// bit2 inner_product_verify (with P from calculate_inner_product_point, Q = h).
+extern "C" void ref_rpv_parts(const struct FlatHead* head, const ge25519* V, size_t n, const fe25519* a,
+                              const fe25519* b, size_t ab_len, const ge25519* L, const ge25519* R, size_t L_len,
+                              const ge25519* G, const ge25519* H, const ge25519* g, const ge25519* h,
+                              fe25519* delta_out, int* flags) {
+    RangeProof p;
+    build_proof(&p, head, n, a, b, ab_len, L, R, L_len);
+    PointVector Gv = {(ge25519*)G, n}, Hv = {(ge25519*)H, n};
+    uint8_t yb[32], zb[32], xb[32];
+    fe25519 y, z, x, delta;
+    quiet_begin();
+    generate_challenge_y(yb, V, &p.A, &p.S);
+    fe25519_frombytes(&y, yb);
+    generate_challenge_z(zb, yb);
+    fe25519_frombytes(&z, zb);
+    generate_challenge_x(xb, &p.T1, &p.T2);
+    fe25519_frombytes(&x, xb);
+    compute_precise_delta(&delta, &z, &y, n);
+    int f = 0;
+    if (enhanced_range_check(&p.t, &delta, &z, V, g, h, n)) f |= 1;
+    if (robust_polynomial_identity_check(&p, V, &x, &y, &z, &delta, g, h)) f |= 2;
+    ge25519 P;
+    calculate_inner_product_point(&P, &p, &x, &y, &z, &p.t, &Gv, &Hv, g, h, n);
+    if (inner_product_verify(&p.ip_proof, &P, &Gv, &Hv, h)) f |= 4;
+    quiet_end();
+    *delta_out = delta;
+    *flags = f;
+}

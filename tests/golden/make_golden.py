@@ -18,7 +18,13 @@ oracle/build_ref.sh) and records inputs + reference outputs as .npz (no pickles)
               at crv:146-158 before folding (recorded as ok_raw); the fold case sets c = <a',b'> (c_fix).
               Recorded: the verdicts, the check point and the last 15 folded G'/H' (rounds 9-11).
 
-  python tests/golden/make_golden.py [ipa4096]   (argument: regenerate only that fixture)
+  rpverify.npz range_proof_verify (bulletproof_range_proof.cu:1717) on reference proofs,
+              tampered copies (V argument != proof V, t / taux / mu / c perturbed) and proof-shaped
+              random inputs, n in {16, 64}: the verdict and, from the reference's own functions,
+              compute_precise_delta's delta and the enhanced_range_check /
+              robust_polynomial_identity_check / inner_product_verify results.
+
+  python tests/golden/make_golden.py [ipa4096|rpverify]   (argument: regenerate only that fixture)
 
 The survey's golden digests are reproduced by tests/test_oracle_golden.py.
 """
@@ -168,9 +174,56 @@ def make_ipa4096():
     print("ipa4096: ok", ok, "ok_raw", ok_raw)
 
 
+def make_rpverify():
+    po.build()
+    R = po.Reference()
+    rng = np.random.default_rng(77)
+    out = {}
+    for n, nproofs in ((16, 4), (64, 2)):
+        G, H = R.base_points(n, 1), R.base_points(n, 2)
+        g, h = R.gh()
+        cases = []
+        for seed in range(101, 101 + nproofs):
+            val = np.zeros(32, np.uint8)
+            val[:n // 8] = rng.integers(0, 256, n // 8)
+            pr = R.prove(seed, val, n, G, H, g, h)
+            cases.append(("ref", pr))
+            for kind, word in (("t", 90), ("taux", 80), ("mu", 84), ("c", 92)):
+                q = {k: v.copy() for k, v in pr.items()}
+                q["head"][word] ^= np.uint64(1 << int(rng.integers(0, 60)))
+                cases.append((kind, q))
+            q = {k: v.copy() for k, v in pr.items()}
+            q["V"][0] ^= np.uint64(1)                 # V argument != proof.V (rp.cu:1735)
+            cases.append(("V", q))
+        for _ in range(4):                            # proof-shaped random inputs
+            hd = np.zeros(po.HEAD_WORDS, np.uint64)
+            hd[:] = rng.integers(0, 2**63, po.HEAD_WORDS, dtype=np.uint64)
+            pr = dict(head=hd, V=hd[0:16].copy(), a=hd[88:92][None].copy(), b=np.array([[1, 0, 0, 0]], np.uint64),
+                      L=rng.integers(0, 2**63, (n.bit_length() - 1, 16), dtype=np.uint64),
+                      R=rng.integers(0, 2**63, (n.bit_length() - 1, 16), dtype=np.uint64))
+            pr["head"][92:96] = pr["head"][88:92]     # c = t = <[t],[1]>
+            cases.append(("rand", pr))
+        recs = {k: [] for k in ("kind", "head", "V", "a", "b", "L", "R", "ok", "delta", "flags")}
+        for kind, pr in cases:
+            recs["kind"].append(kind)
+            for k in ("head", "V", "a", "b", "L", "R"):
+                recs[k].append(pr[k])
+            recs["ok"].append(R.range_proof_verify(pr, n, G, H, g, h))
+            d, f = R.rpv_parts(pr, n, G, H, g, h)
+            recs["delta"].append(d)
+            recs["flags"].append(f)
+        for k, v in recs.items():
+            out[f"n{n}_{k}"] = np.array(v) if k == "kind" else np.stack([np.asarray(x) for x in v])
+        print(f"rpverify n={n}: ok {sum(recs['ok'])}/{len(cases)}, flags {recs['flags']}")
+    np.savez_compressed(os.path.join(HERE, "rpverify.npz"), **out)
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["ipa4096"]:
         make_ipa4096()
+    elif sys.argv[1:] == ["rpverify"]:
+        make_rpverify()
     else:
         main()
         make_ipa4096()
+        make_rpverify()

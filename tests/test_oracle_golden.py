@@ -104,3 +104,28 @@ def test_ipa4096_against_reference(oracle, golden):
     ok_raw, _, _, _ = oracle.cuda_inner_product_verify(n, d["a"], d["b"], d["c_in"], d["L"], d["R"], d["x"], d["P"],
                                                        G, H, Q)
     assert ok_raw == bool(d["ok_raw"])
+
+
+@pytest.mark.parametrize("n", [16, 64])
+def test_range_proof_verify_against_reference(oracle, golden, n):
+    """range_proof_verify (rp.cu:1717) — verdicts, delta and each sub-check."""
+    d = golden("rpverify")
+    G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+    g, h = oracle.gh()
+    k = f"n{n}_"
+    for i in range(len(d[k + "ok"])):
+        ok, det = oracle.range_proof_verify(d[k + "head"][i], d[k + "V"][i], n, d[k + "a"][i], d[k + "b"][i],
+                                            d[k + "L"][i], d[k + "R"][i], G, H, g, h)
+        f = int(det["range_ok"]) | int(det["poly_ok"]) << 1 | int(det["ip_ok"]) << 2
+        assert ok == bool(d[k + "ok"][i]), (i, d[k + "kind"][i])
+        assert f == int(d[k + "flags"][i]), (i, d[k + "kind"][i])
+        assert np.array_equal(det["delta"], d[k + "delta"][i]), i
+
+
+def test_range_proof_verify_golden_proofs(oracle, golden):
+    for n in (16, 64):
+        d = golden(f"proofs_n{n}")
+        for i in range(len(d["head"])):
+            ok, _ = oracle.range_proof_verify(d["head"][i], d["V"][i], n, d["a"][i], d["b"][i], d["L"][i], d["R"][i],
+                                              d["G"], d["H"], d["g"], d["h"])
+            assert ok == bool(d["ok_cpu"][i]), (n, i)
