@@ -74,7 +74,7 @@ class RangeProofC(ctypes.Structure):   # bulletproof_range_proof.h:7-18 (880 byt
 
 class ProofBatchC(ctypes.Structure):   # hipbp_proof_batch
     _fields_ = [("count", _sz), ("n", _sz), ("ab_len", _sz), ("L_len", _sz)] + \
-               [(k, _c) for k in ("V", "A", "S", "T1", "T2", "t", "a", "b", "c", "x", "L", "R")]
+               [(k, _c) for k in ("V", "A", "S", "T1", "T2", "t", "a", "b", "c", "x", "L", "R", "taux", "mu", "Vp")]
 
 
 assert ctypes.sizeof(InnerProductProof) == 144 and ctypes.sizeof(RangeProofC) == 880
@@ -87,7 +87,7 @@ EXPORTS = [
     "cuda_batch_field_invert", "cuda_soa_field_add", "cuda_range_proof_verify", "cuda_inner_product_verify",
     "cuda_benchmark_multi_scalar_mul", "cuda_benchmark_inner_product", "cuda_benchmark_field_operations",
     "cuda_benchmark_range_proof", "hipbp_last_error", "hipbp_device_count", "hipbp_batch_range_proof_verify",
-    "hipbp_batch_inner_product_verify", "hipbp_msm", "hipbp_point_tree", "hipbp_field_op", "hipbp_sync", "hipbp_timing_enable",
+    "hipbp_batch_range_proof_verify_std", "hipbp_batch_inner_product_verify", "hipbp_msm", "hipbp_point_tree", "hipbp_field_op", "hipbp_sync", "hipbp_timing_enable",
     "hipbp_timing_collect", "hipbp_kernel_count", "hipbp_kernel_name", "hipbp_pipeline_create",
     "hipbp_pipeline_push", "hipbp_pipeline_flush", "hipbp_pipeline_depth", "hipbp_pipeline_destroy",
 ]
@@ -110,7 +110,8 @@ def lib():
         L.hipbp_last_error.restype = ctypes.c_char_p
         for f in ("cuda_range_proof_verify", "cuda_inner_product_verify"):
             getattr(L, f).restype = ctypes.c_bool
-        for f in ("hipbp_batch_range_proof_verify", "hipbp_batch_inner_product_verify", "hipbp_msm", "hipbp_point_tree",
+        for f in ("hipbp_batch_range_proof_verify", "hipbp_batch_range_proof_verify_std",
+                  "hipbp_batch_inner_product_verify", "hipbp_msm", "hipbp_point_tree",
                   "hipbp_field_op", "hipbp_sync", "hipbp_device_count"):
             getattr(L, f).restype = ctypes.c_int
         _lib = L
@@ -269,15 +270,20 @@ class RangeProofBatch:
     """A batch of proofs in the flat wire format, resident on a torch CUDA device.
 
     Tensors are int64 views of the u64 limbs: V/A/S/T1/T2 (B,16), t/c/x (B,4),
-    a/b (B,ab_len,4), L/R (B,L_len,16).
+    a/b (B,ab_len,4), L/R (B,L_len,16).  Optional (range_proof_verify semantics only):
+    taux/mu (B,4) and Vp (B,16), the proof's own V (default: V).
     """
 
     FIELDS = ("V", "A", "S", "T1", "T2", "t", "a", "b", "c", "x", "L", "R")
+    OPTIONAL = ("taux", "mu", "Vp")
 
     def __init__(self, n, **tensors):
         self.n = int(n)
         for k in self.FIELDS:
             setattr(self, k, tensors[k].contiguous())
+        for k in self.OPTIONAL:
+            v = tensors.get(k)
+            setattr(self, k, v.contiguous() if v is not None else None)
         self.count = int(self.V.shape[0])
         self.ab_len = int(self.a.shape[1])
         self.L_len = int(self.L.shape[1])
@@ -285,13 +291,17 @@ class RangeProofBatch:
     @classmethod
     def from_numpy(cls, n, arrays, device):
         import torch
-        t = {k: torch.from_numpy(np.ascontiguousarray(arrays[k]).view(np.int64)).to(device) for k in cls.FIELDS}
+        t = {k: torch.from_numpy(np.ascontiguousarray(arrays[k]).view(np.int64)).to(device)
+             for k in cls.FIELDS + cls.OPTIONAL if arrays.get(k) is not None}
         return cls(n, **t)
 
     def c_struct(self):
         s = ProofBatchC(self.count, self.n, self.ab_len, self.L_len)
         for k in self.FIELDS:
             setattr(s, k, getattr(self, k).data_ptr())
+        for k in self.OPTIONAL:
+            v = getattr(self, k)
+            setattr(s, k, v.data_ptr() if v is not None else None)
         return s
 
     def nbytes(self):
@@ -315,6 +325,19 @@ def batch_range_proof_verify(batch, G, H, g, h, ok, P_out=None, check_out=None, 
         ctypes.byref(s), _c(G.data_ptr()), _c(H.data_ptr()), _c(g.data_ptr()), _c(h.data_ptr()), _c(ok.data_ptr()),
         _c(P_out.data_ptr()) if P_out is not None else None,
         _c(check_out.data_ptr()) if check_out is not None else None, _stream_ptr(stream)))
+
+
+def batch_range_proof_verify_std(batch, G, H, g, h, ok, P_out=None, check_out=None, flags_out=None, poly_out=None,
+                                 stream=None):
+    """Enqueue range_proof_verify semantics (bulletproof_range_proof.cu:1717) over the
+    batch (needs batch.taux/mu).  flags_out (B,) uint8: bit0 V match, bit1 range check, bit2
+    polynomial identity methods 1|2, bit3 method 3, bit4 method 4, bit5 inner_product_verify;
+    poly_out (B,4,16): left, right, chal*left, chal*right."""
+    s = batch.c_struct()
+    opt = lambda t: _c(t.data_ptr()) if t is not None else None
+    _chk(lib().hipbp_batch_range_proof_verify_std(
+        ctypes.byref(s), _c(G.data_ptr()), _c(H.data_ptr()), _c(g.data_ptr()), _c(h.data_ptr()), _c(ok.data_ptr()),
+        opt(P_out), opt(check_out), opt(flags_out), opt(poly_out), _stream_ptr(stream)))
 
 
 def batch_inner_product_verify(batch, P, G, H, Q, ok, check_out=None, stream=None):
@@ -368,26 +391,29 @@ class VerifyPipeline:
     every in-flight batch advances one stage (stage 0 / fold round r / final).  A batch's
     outputs are complete after depth-1 further pushes or flush()."""
 
-    def __init__(self, max_batch, n, G, H, h, range_mode=True, stream=None):
+    def __init__(self, max_batch, n, G, H, h, range_mode=True, stream=None, g=None):
+        """range_mode: True/1 cuda_range_proof_verify, 2 range_proof_verify (needs g), False/0
+        cuda_inner_product_verify (h = Q)."""
         L = lib()
         L.hipbp_pipeline_create.restype = ctypes.c_void_p
         L.hipbp_pipeline_push.restype = ctypes.c_int
         L.hipbp_pipeline_flush.restype = ctypes.c_int
         L.hipbp_pipeline_depth.restype = ctypes.c_int
-        self._keep = (G, H, h)
-        self.h = L.hipbp_pipeline_create(_sz(max_batch), _sz(n), 1 if range_mode else 0, _c(G.data_ptr()),
-                                         _c(H.data_ptr()), _c(h.data_ptr()), _stream_ptr(stream))
+        self._keep = (G, H, h, g)
+        self.mode = int(range_mode)
+        self.h = L.hipbp_pipeline_create(_sz(max_batch), _sz(n), self.mode, _c(G.data_ptr()), _c(H.data_ptr()),
+                                         _c(g.data_ptr()) if g is not None else None, _c(h.data_ptr()),
+                                         _stream_ptr(stream))
         if not self.h:
             raise BulletproofError(L.hipbp_last_error().decode())
         self.depth = L.hipbp_pipeline_depth(_c(self.h))
 
-    def push(self, batch, ok=None, P_out=None, check_out=None, P_in=None):
+    def push(self, batch, ok=None, P_out=None, check_out=None, P_in=None, flags_out=None, poly_out=None):
         s = batch.c_struct() if batch is not None else None
+        opt = lambda t: _c(t.data_ptr()) if t is not None else None
         _chk(lib().hipbp_pipeline_push(
-            _c(self.h), ctypes.byref(s) if s is not None else None,
-            _c(P_in.data_ptr()) if P_in is not None else None, _c(ok.data_ptr()) if ok is not None else None,
-            _c(P_out.data_ptr()) if P_out is not None else None,
-            _c(check_out.data_ptr()) if check_out is not None else None))
+            _c(self.h), ctypes.byref(s) if s is not None else None, opt(P_in), opt(ok), opt(P_out), opt(check_out),
+            opt(flags_out), opt(poly_out)))
 
     def flush(self):
         _chk(lib().hipbp_pipeline_flush(_c(self.h)))

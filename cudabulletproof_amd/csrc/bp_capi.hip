@@ -144,7 +144,7 @@ struct Engine {
         return hipSuccess;
     }
     // one-shot verify pipelines, per (stream, n, mode), so batches on different streams overlap
-    std::map<std::tuple<hipStream_t, int, bool>, struct Pipeline*> pipes;
+    std::map<std::tuple<hipStream_t, int, int>, struct Pipeline*> pipes;
     std::mutex mu;
 
     hipError_t init() {
@@ -213,7 +213,7 @@ int log2i(size_t n) {
     return k;
 }
 
-int check_batch(const hipbp_proof_batch* b, bool range_mode) {
+int check_batch(const hipbp_proof_batch* b, int range_mode) {
     if (!b) { g_err = "null batch"; return HIPBP_ERR_ARG; }
     if (b->count == 0) return HIPBP_OK;
     if (!is_pow2(b->n) || b->n > MAX_N) { g_err = "n must be a power of two <= 65536"; return HIPBP_ERR_ARG; }
@@ -222,6 +222,7 @@ int check_batch(const hipbp_proof_batch* b, bool range_mode) {
     if (b->count > (size_t)1 << 24) { g_err = "batch too large"; return HIPBP_ERR_ARG; }
     if (!b->a || !b->b || !b->c || !b->x || (b->L_len && (!b->L || !b->R))) { g_err = "null ipa field"; return HIPBP_ERR_ARG; }
     if (range_mode && (!b->V || !b->A || !b->S || !b->T1 || !b->T2 || !b->t)) { g_err = "null range field"; return HIPBP_ERR_ARG; }
+    if (range_mode == 2 && (!b->taux || !b->mu)) { g_err = "range_proof_verify semantics need taux and mu"; return HIPBP_ERR_ARG; }
     return HIPBP_OK;
 }
 
@@ -236,6 +237,7 @@ bp::BatchView view_of(const hipbp_proof_batch* b) {
     v.t = (const bp::fe*)b->t; v.a = (const bp::fe*)b->a; v.b = (const bp::fe*)b->b;
     v.c = (const bp::fe*)b->c; v.x = (const bp::fe*)b->x;
     v.L = (const bp::ge*)b->L; v.R = (const bp::ge*)b->R;
+    v.taux = (const bp::fe*)b->taux; v.mu = (const bp::fe*)b->mu; v.Vp = (const bp::ge*)b->Vp;
     return v;
 }
 
@@ -253,10 +255,10 @@ struct Pipeline {
     hipStream_t s = nullptr;
     int n = 0, Lr = 0, D = 0;
     size_t maxB = 0;
-    bool range_mode = true;
-    const bp::ge *G = nullptr, *H = nullptr, *h = nullptr;
+    int range_mode = 1;   // 0 inner product only, 1 cuda_range_proof_verify, 2 range_proof_verify
+    const bp::ge *G = nullptr, *H = nullptr, *g = nullptr, *h = nullptr;
     struct Slot {
-        Buf b[16];
+        Buf b[24];
         bp::SlotDev dev{};
         bool active = false;
         int stage = 0;
@@ -268,7 +270,7 @@ struct Pipeline {
     bp::SlotDev* host_dev = nullptr;    // pinned staging [D]
     int head = 0;
 
-    hipError_t init(Engine* eng, hipStream_t st, size_t mb, int nn, bool range) {
+    hipError_t init(Engine* eng, hipStream_t st, size_t mb, int nn, int range) {
         e = eng; s = st; maxB = mb; n = nn; range_mode = range;
         Lr = log2i((size_t)n);
         D = (Lr > 0 ? Lr : 1) + 2;
@@ -306,11 +308,21 @@ struct Pipeline {
         w.msm_pts = sl.b[6].as<bp::ge>(); w.msm_part = sl.b[7].as<bp::ge>(); w.terms = sl.b[8].as<bp::ge>();
         w.fold = sl.b[9].as<bp::ge>(); w.Gc = sl.b[10].as<bp::ge>(); w.Hc = sl.b[11].as<bp::ge>();
         w.fin = sl.b[12].as<bp::ge>(); w.Pin = sl.b[13].as<bp::ge>();
+        if (range_mode == 2) {
+            size_t sz2[6] = {B * 8 * 32, B * 8 * 128, B * 2 * 128, B * 32, B * 2 * 128, B};
+            for (int i = 0; i < 6; i++)
+                if ((r = sl.b[14 + i].need(sz2[i])) != hipSuccess) return r;
+            w.psc = sl.b[14].as<bp::fe>(); w.pterm = sl.b[15].as<bp::ge>(); w.lr = sl.b[16].as<bp::ge>();
+            w.chal = sl.b[17].as<bp::fe>(); w.m3 = sl.b[18].as<bp::ge>(); w.rflags = sl.b[19].as<uint8_t>();
+        } else {
+            w.psc = nullptr; w.pterm = nullptr; w.lr = nullptr; w.chal = nullptr; w.m3 = nullptr; w.rflags = nullptr;
+        }
         return hipSuccess;
     }
 
     // One tick; `b` may be null (drain).  Outputs of `b` are written when it completes.
-    int push(const hipbp_proof_batch* b, const ge25519* P_in, uint8_t* ok, ge25519* P_out, ge25519* chk) {
+    int push(const hipbp_proof_batch* b, const ge25519* P_in, uint8_t* ok, ge25519* P_out, ge25519* chk,
+             uint8_t* flags_out = nullptr, ge25519* poly_out = nullptr) {
         EventTimer* tm = e->timer.on ? &e->timer : nullptr;
         bool has = b && b->count > 0;
         Slot& nw = slots[head];
@@ -324,7 +336,9 @@ struct Pipeline {
             nw.dev.ok = ok;
             nw.dev.P_out = (bp::ge*)P_out;
             nw.dev.chk_out = (bp::ge*)chk;
-            nw.dev.range_mode = range_mode ? 1 : 0;
+            nw.dev.flags_out = flags_out;
+            nw.dev.poly_out = (bp::ge*)poly_out;
+            nw.dev.range_mode = range_mode;
             BP_RET_ON(hipEventSynchronize(nw.copied));   // staging slot free again
             host_dev[head] = nw.dev;
             BP_RET_ON(hipMemcpyAsync(slots_dev + head, host_dev + head, sizeof(bp::SlotDev), hipMemcpyHostToDevice, s));
@@ -358,9 +372,12 @@ struct Pipeline {
                 int fin_terms = L > 0 ? L + 1 : 1, fin = L > 0 ? L + 1 : 2;
                 if (st == 0) add(tr, bp::RK_PREP, idx, 0, range_mode ? 2 * B : B, 64);
                 if (st == 1) {
-                    unsigned long long it = (range_mode ? B * 2 * n : 0) + (L > 0 ? B * 2 * n : 0) + B * 2;
+                    unsigned long long it = (range_mode ? B * 2 * n : 0) + (L > 0 ? B * 2 * n : 0) + B * 2 +
+                                            (range_mode == 2 ? B * 7 : 0);   // == stage0_items (device)
                     add(tr, bp::RK_STAGE0, idx, 0, it, 64);
+                    if (range_mode == 2) add(cr, bp::RK_POLY, idx, 0, B, 64);
                 }
+                if (range_mode == 2 && st == fin) add(tr, bp::RK_M3, idx, 0, B * 2, 64);
                 if (st >= 2 && st <= L) add(tr, bp::RK_ROUND, idx, st - 1, B * 4 * (n >> st), 64);
                 if (st == fin_terms) add(tr, bp::RK_FINAL_TERMS, idx, 0, B * 2, 64);
                 if (st >= 1 && st <= L) add(cr, bp::RK_COMBINE, idx, st - 1, B * 2 * (n >> st), 64);
@@ -369,7 +386,7 @@ struct Pipeline {
         }
         if (overflow) { g_err = "pipeline region list overflow (internal)"; return HIPBP_ERR_ARG; }
         if (tm) tm->mark(bp::KT_TERMS, false, s);
-        bp::launch_terms(tr, slots_dev, G, H, h, e->dtab, e->two_i, s);
+        bp::launch_terms(tr, slots_dev, G, H, g ? g : h, h, e->dtab, e->two_i, s);
         if (tm) tm->mark(bp::KT_TERMS, true, s);
         if (tm) tm->mark(bp::KT_COMBINE, false, s);
         bp::launch_combine(cr, slots_dev, s);
@@ -395,7 +412,8 @@ struct Pipeline {
 
 // One-shot verify of a whole batch on `s` (push + drain of a cached pipeline).
 int run_verify(Engine& e, const hipbp_proof_batch* batch, const ge25519* P_in, const ge25519* G, const ge25519* H,
-               const ge25519* h, uint8_t* ok, ge25519* P_out, ge25519* chk_out, bool range_mode, hipStream_t s) {
+               const ge25519* h, uint8_t* ok, ge25519* P_out, ge25519* chk_out, int range_mode, hipStream_t s,
+               const ge25519* g = nullptr, uint8_t* flags_out = nullptr, ge25519* poly_out = nullptr) {
     int rc = check_batch(batch, range_mode);
     if (rc != HIPBP_OK || batch->count == 0) return rc;
     if (range_mode) BP_RET_ON(e.ensure_two((int)batch->n));
@@ -408,7 +426,8 @@ int run_verify(Engine& e, const hipbp_proof_batch* batch, const ge25519* P_in, c
     pl->G = (const bp::ge*)G;
     pl->H = (const bp::ge*)H;
     pl->h = (const bp::ge*)h;
-    if ((rc = pl->push(batch, P_in, ok, P_out, chk_out)) != HIPBP_OK) return rc;
+    pl->g = (const bp::ge*)g;
+    if ((rc = pl->push(batch, P_in, ok, P_out, chk_out, flags_out, poly_out)) != HIPBP_OK) return rc;
     return pl->flush();
 }
 
@@ -477,7 +496,19 @@ int hipbp_batch_range_proof_verify(const hipbp_proof_batch* batch, const ge25519
     BP_RET_ON(err);
     if (!G || !H || !h || !ok) { g_err = "null generator/output"; return HIPBP_ERR_ARG; }
     std::lock_guard<std::mutex> lk(e->mu);
-    return run_verify(*e, batch, nullptr, G, H, h, ok, P_out, check_out, true, pick(stream, *e));
+    return run_verify(*e, batch, nullptr, G, H, h, ok, P_out, check_out, 1, pick(stream, *e));
+}
+
+int hipbp_batch_range_proof_verify_std(const hipbp_proof_batch* batch, const ge25519* G, const ge25519* H,
+                                       const ge25519* g, const ge25519* h, uint8_t* ok, ge25519* P_out,
+                                       ge25519* check_out, uint8_t* flags_out, ge25519* poly_out, void* stream) {
+    hipError_t err;
+    Engine* e = engine_or_null(&err);
+    BP_RET_ON(err);
+    if (!G || !H || !g || !h || !ok) { g_err = "null generator/output"; return HIPBP_ERR_ARG; }
+    std::lock_guard<std::mutex> lk(e->mu);
+    return run_verify(*e, batch, nullptr, G, H, h, ok, P_out, check_out, 2, pick(stream, *e), g, flags_out,
+                      poly_out);
 }
 
 int hipbp_batch_inner_product_verify(const hipbp_proof_batch* batch, const ge25519* P, const ge25519* G,
@@ -488,15 +519,16 @@ int hipbp_batch_inner_product_verify(const hipbp_proof_batch* batch, const ge255
     BP_RET_ON(err);
     if (!P || !G || !H || !Q || !ok) { g_err = "null argument"; return HIPBP_ERR_ARG; }
     std::lock_guard<std::mutex> lk(e->mu);
-    return run_verify(*e, batch, P, G, H, Q, ok, nullptr, check_out, false, pick(stream, *e));
+    return run_verify(*e, batch, P, G, H, Q, ok, nullptr, check_out, 0, pick(stream, *e));
 }
 
 void* hipbp_pipeline_create(size_t max_batch, size_t n, int range_mode, const ge25519* G, const ge25519* H,
-                            const ge25519* h, void* stream) {
+                            const ge25519* g, const ge25519* h, void* stream) {
     hipError_t err;
     Engine* e = engine_or_null(&err);
     if (!e) { g_err = std::string("engine: ") + hipGetErrorString(err); return nullptr; }
     if (!is_pow2(n) || n > MAX_N || !G || !H || !h) { g_err = "pipeline: bad n or null generator"; return nullptr; }
+    if (range_mode < 0 || range_mode > 2 || (range_mode == 2 && !g)) { g_err = "pipeline: bad mode or null g"; return nullptr; }
     if (range_mode) {
         std::lock_guard<std::mutex> lk(e->mu);
         if ((err = e->ensure_two((int)n)) != hipSuccess) {
@@ -505,7 +537,7 @@ void* hipbp_pipeline_create(size_t max_batch, size_t n, int range_mode, const ge
         }
     }
     Pipeline* pl = new Pipeline();
-    err = pl->init(e, pick(stream, *e), max_batch, (int)n, range_mode != 0);
+    err = pl->init(e, pick(stream, *e), max_batch, (int)n, range_mode);
     if (err != hipSuccess) {
         g_err = std::string("pipeline init: ") + hipGetErrorString(err);
         pl->release();
@@ -515,16 +547,17 @@ void* hipbp_pipeline_create(size_t max_batch, size_t n, int range_mode, const ge
     pl->G = (const bp::ge*)G;
     pl->H = (const bp::ge*)H;
     pl->h = (const bp::ge*)h;
+    pl->g = (const bp::ge*)g;
     return pl;
 }
 
 int hipbp_pipeline_push(void* handle, const hipbp_proof_batch* batch, const ge25519* P_in, uint8_t* ok,
-                        ge25519* P_out, ge25519* check_out) {
+                        ge25519* P_out, ge25519* check_out, uint8_t* flags_out, ge25519* poly_out) {
     Pipeline* pl = (Pipeline*)handle;
     if (!pl) { g_err = "null pipeline"; return HIPBP_ERR_ARG; }
     if (batch && batch->count && (!ok || (!pl->range_mode && !P_in))) { g_err = "null output/P"; return HIPBP_ERR_ARG; }
     std::lock_guard<std::mutex> lk(pl->e->mu);
-    return pl->push(batch, P_in, ok, P_out, check_out);
+    return pl->push(batch, P_in, ok, P_out, check_out, flags_out, poly_out);
 }
 
 int hipbp_pipeline_flush(void* handle) {
@@ -774,7 +807,7 @@ static bool verify_single(const InnerProductProof* ip, const RangeProof* rp, con
     if (P) BP_EXIT_ON(hipMemcpyAsync(dg + 2 * n + 1, P, sizeof(ge25519), hipMemcpyHostToDevice, e.stream));
     BP_EXIT_ON(e.h2d[5].need(64));
     int rc = run_verify(e, &b, P ? dg + 2 * n + 1 : nullptr, dg, dg + n, dg + 2 * n, e.h2d[5].as<uint8_t>(), nullptr,
-                        nullptr, rp != nullptr, e.stream);
+                        nullptr, rp != nullptr ? 1 : 0, e.stream);
     if (rc == HIPBP_ERR_ARG) {
         fprintf(stderr, "Error: %s\n", g_err.c_str());
         return false;

@@ -26,6 +26,9 @@ struct BatchView {
     const fe* x;  // [B]
     const ge* L;  // [B*L_len]
     const ge* R;  // [B*L_len]
+    const fe* taux;   // [B]  range_proof_verify semantics only
+    const fe* mu;     // [B]
+    const ge* Vp;     // [B]  the proof's own V (== V when the caller passed none)
 };
 
 // Device workspace of one verify batch (allocated by the engine).
@@ -44,6 +47,13 @@ struct VerifyWs {
     ge* Hc;        // [B*n/2]
     ge* fin;       // [B*2]    a0*G', b0*H'
     ge* Pin;       // [B]      given P (inner-product-only verify)
+    // range_proof_verify semantics (mode 2) only:
+    fe* psc;       // [B*8]    canonical t, taux, z^2, delta, mu, x, x^2 (polynomial identity scalars)
+    ge* pterm;     // [B*8]    g^t, h^taux, V^z^2, g^delta, h^mu, T1^x, T2^x^2 (host-normalized)
+    ge* lr;        // [B*2]    left / right side of the polynomial identity
+    fe* chal;      // [B]      SHA-256 of the sides' bytes (method 3 scalar, raw bytes)
+    ge* m3;        // [B*2]    chal * left, chal * right
+    uint8_t* rflags;   // [B]  bit0 V match, bit1 range check, bit2 methods 1|2
 };
 
 // One batch in flight in the verify pipeline (device-resident copy, read by the tick kernels).
@@ -53,15 +63,18 @@ struct SlotDev {
     uint8_t* ok;
     ge* P_out;
     ge* chk_out;
-    int range_mode;
+    uint8_t* flags_out;   // mode 2, nullable
+    ge* poly_out;         // mode 2, nullable
+    int range_mode;       // 0 inner product only, 1 cuda_range_proof_verify, 2 range_proof_verify
 };
 
 // A tick's work list: region k covers items [begin_k, begin_{k+1}) of one slot at one stage.
 // k_terms regions: RK_PREP (challenges/scalars, one lane per proof and kind), RK_STAGE0,
-// RK_ROUND, RK_FINAL_TERMS.  k_combine regions: RK_TREE (block-level MSM tree; always first,
-// 256-aligned), RK_COMBINE, RK_FINAL.
+// RK_ROUND, RK_FINAL_TERMS, RK_M3 (mode 2: method-3 products).  k_combine regions: RK_TREE
+// (block-level MSM tree; always first, 256-aligned), RK_COMBINE, RK_FINAL, RK_POLY (mode 2:
+// polynomial identity sides).
 enum RegionKind { RK_STAGE0 = 0, RK_ROUND = 1, RK_FINAL_TERMS = 2, RK_COMBINE = 3, RK_FINAL = 4, RK_PREP = 5,
-                  RK_TREE = 6 };
+                  RK_TREE = 6, RK_POLY = 7, RK_M3 = 8 };
 struct Region {
     int kind;
     int slot;
@@ -82,7 +95,7 @@ struct RegionList {
 enum KernelKind { KT_PREP = 0, KT_TERMS, KT_TREE, KT_COMBINE, KT_COUNT };
 
 void launch_init_tables(ge* dtab, fe* two_i, int nmax, hipStream_t s);
-void launch_terms(const RegionList& rl, const SlotDev* slots, const ge* G, const ge* H, const ge* h,
+void launch_terms(const RegionList& rl, const SlotDev* slots, const ge* G, const ge* H, const ge* g, const ge* h,
                   const ge* dtab, const fe* two_i, hipStream_t s);
 void launch_combine(const RegionList& rl, const SlotDev* slots, hipStream_t s);
 

@@ -95,10 +95,61 @@ __device__ __forceinline__ fe challenge_digest(sha256_ctx& c) {
     return r;
 }
 
+__device__ __forceinline__ uint32_t fe_byte(const fe& f, int i) { return (uint32_t)(f.v[i >> 3] >> (8 * (i & 7))) & 0xff; }
+
+// range_proof_verify's scalar work (mode 2), one lane per proof: the x challenge
+// (challenge.cu:61-77), compute_precise_delta (rp.cu:315-410), enhanced_range_check
+// (rp.cu:765-876; called twice at rp.cu:1778/:1785 with the same result), the V match
+// (rp.cu:1729-1740) and the polynomial-identity scalars in host-tobytes form (rp.cu:424-435).
+// sy = <1^n, y^n> from the caller's power loop (rp.cu:336-343, the same mul/add chain).
+__device__ __forceinline__ void prep_std_task(const BatchView& bv, const VerifyWs& ws, const fe* __restrict__ two_i,
+                                              size_t p, const fe& z, const fe& z2, const fe& sy) {
+    const int n = bv.n;
+    sha256_ctx c;
+    sha_init(c);
+    sha_str(c, "BulletproofXChal");
+    sha_fe_canon(c, bv.T1[p].X); sha_fe_canon(c, bv.T1[p].Y);
+    sha_fe_canon(c, bv.T2[p].X); sha_fe_canon(c, bv.T2[p].Y);
+    sha_str(c, "xcha");                  // memcpy of 4 bytes of "xchal" (challenge.cu:73)
+    fe x = challenge_digest(c);
+    const fe two = fe_add(fe_set(1), fe_set(1));
+    // compute_precise_delta
+    fe z3 = fe_mul(z2, z);
+    fe t1 = fe_mul(fe_sub(z, z2), sy);
+    fe s2 = fe_set(1);
+    for (int i = 1; i < n; i++) s2 = fe_add(s2, two_i[i]);   // sum of 2^i, two_i[i] = the i-fold mul chain
+    fe delta = fe_sub(t1, fe_mul(z3, s2));
+    // enhanced_range_check
+    const fe t = bv.t[p];
+    fe tmd = fe_sub(t, delta);
+    fe val = fe_mul(tmd, fe_invert(z2));
+    fe two_n = fe_mul(two_i[n - 1], two);                    // n-fold mul chain from 1
+    bool lower_ok = (fe_canon(fe_sub(tmd, z2)).v[3] >> 63) == 0;
+    bool upper_ok = (fe_canon(fe_sub(fe_mul(z2, two_n), tmd)).v[3] >> 63) == 0;
+    fe dm = fe_canon(fe_sub(val, two_n));
+    bool close = true;
+    for (int i = 0; i < 4; i++) {
+        uint32_t b = fe_byte(dm, i);
+        close &= !(b > 3 && b < 253);
+    }
+    bool range_ok = lower_ok & upper_ok & !close;
+    const ge& Vp = bv.Vp ? bv.Vp[p] : bv.V[p];
+    bool vmatch = fe_eq(fe_canon(bv.V[p].X), fe_canon(Vp.X)) & fe_eq(fe_canon(bv.V[p].Y), fe_canon(Vp.Y));
+    ws.rflags[p] = (uint8_t)((vmatch ? 1 : 0) | (range_ok ? 2 : 0));
+    fe* ps = ws.psc + p * 8;
+    ps[0] = fe_canon(t);
+    ps[1] = fe_canon(bv.taux[p]);
+    ps[2] = fe_canon(z2);
+    ps[3] = fe_canon(delta);
+    ps[4] = fe_canon(bv.mu[p]);
+    ps[5] = fe_canon(x);
+    ps[6] = fe_canon(fe_mul(x, x));
+}
+
 // cuda_range_proof_verify (crv:93-106) + calculate_inner_product_point scalars
 // (bulletproof_range_proof.cu:679-718): one lane per proof.
 __device__ __forceinline__ void prep_range_task(const BatchView& bv, const VerifyWs& ws, const fe* __restrict__ two_i,
-                                             size_t p) {
+                                             size_t p, int mode) {
     const int n = bv.n;
     sha256_ctx c;
     // y = H("BulletproofYChal" || V.X V.Y A.X A.Y S.X S.Y || "y_ch")   (challenge.cu:24-44)
@@ -119,13 +170,17 @@ __device__ __forceinline__ void prep_range_task(const BatchView& bv, const Verif
     //  x argument of calculate_inner_product_point; it does not affect any output.)
     fe z2 = fe_mul(z, z);
     ws.sG[p] = fe_sub(fe_set(0), z);   // rp.cu:699  0 - z
-    fe pw = fe_set(1);
+    fe pw = fe_set(1), sy = fe_set(1);
     for (int i = 0; i < n; i++) {
-        if (i > 0) pw = fe_mul(pw, y);   // powers_of (rp.cu:299-313)
+        if (i > 0) {
+            pw = fe_mul(pw, y);          // powers_of (rp.cu:299-313)
+            sy = fe_add(sy, pw);         // <1^n, y^n> (rp.cu:341-342), mode 2 only
+        }
         fe h = fe_add(z, fe_mul(z2, two_i[i]));
         ws.sH[p * n + i] = fe_mul(h, pw);
     }
     ws.sc[p * 4 + 0] = fe_canon(bv.t[p]);
+    if (mode == 2) prep_std_task(bv, ws, two_i, p, z, z2, sy);
 }
 
 // cuda_inner_product_verify (crv:146-218): <a,b> check and the per-round challenges.
@@ -187,14 +242,17 @@ __device__ __forceinline__ void fold_task(const BatchView& bv, const VerifyWs& w
 //                 segment 2p = <sG, G>, 2p+1 = <sH, H>; Ndev (kernels.cu:26-42)
 //   [.., +2nB)    IPA fold round 0 terms
 //   [.., +2B)     t*h (rp.cu:778-781) and c*Q (crv:255, :268-269), host normalize
+//   [.., +7B)     mode 2: the polynomial identity's g^t, h^taux, V^z^2, g^delta, h^mu, T1^x, T2^x^2
+//                 (rp.cu:442-480), host normalize
 __device__ __forceinline__ size_t stage0_items(const SlotDev& sd) {
     const size_t B = sd.bv.B;
-    return (sd.range_mode ? B * 2 * sd.bv.n : 0) + (sd.bv.L_len > 0 ? B * 2 * sd.bv.n : 0) + B * 2;
+    return (sd.range_mode ? B * 2 * sd.bv.n : 0) + (sd.bv.L_len > 0 ? B * 2 * sd.bv.n : 0) + B * 2 +
+           (sd.range_mode == 2 ? B * 7 : 0);
 }
 
 __device__ __forceinline__ void stage0_task(const SlotDev& sd, size_t i, geq* qslot, const ge* __restrict__ G,
-                                            const ge* __restrict__ H, const ge* __restrict__ h,
-                                            const ge* __restrict__ dtab) {
+                                            const ge* __restrict__ H, const ge* __restrict__ g,
+                                            const ge* __restrict__ h, const ge* __restrict__ dtab) {
     const BatchView& bv = sd.bv;
     const VerifyWs& ws = sd.ws;
     const size_t B = bv.B;
@@ -217,12 +275,35 @@ __device__ __forceinline__ void stage0_task(const SlotDev& sd, size_t i, geq* qs
         return;
     }
     i -= nB;
+    if (i < 2 * B) {
+        size_t p = i >> 1;
+        bool isC = i & 1;
+        if (!isC && !sd.range_mode) return;
+        fe s = isC ? ws.sc[p * 4 + 3] : ws.sc[p * 4 + 0];
+        ge r = scalarmult<true>(s, *h, qslot, dtab);
+        ws.terms[p * 4 + 2 + (isC ? 1 : 0)] = ge_norm_host(r);
+        return;
+    }
+    i -= 2 * B;
+    size_t p = i / 7;
+    int k = (int)(i % 7);
+    ge P;
+    if (k == 0 || k == 3) P = *g;
+    else if (k == 1 || k == 4) P = *h;
+    else if (k == 2) P = bv.V[p];
+    else if (k == 5) P = bv.T1[p];
+    else P = bv.T2[p];
+    ge r = scalarmult<true>(ws.psc[p * 8 + k], P, qslot, dtab);
+    ws.pterm[p * 8 + k] = ge_norm_host(r);
+}
+
+// range_proof_verify method 3 (rp.cu:568-580): chal * left, chal * right, host normalize.
+// The scalar is the raw SHA-256 digest bytes.  Items: 2p -> left, 2p+1 -> right.
+__device__ __forceinline__ void m3_task(const SlotDev& sd, size_t i, geq* qslot, const ge* __restrict__ dtab) {
     size_t p = i >> 1;
-    bool isC = i & 1;
-    if (!isC && !sd.range_mode) return;
-    fe s = isC ? ws.sc[p * 4 + 3] : ws.sc[p * 4 + 0];
-    ge r = scalarmult<true>(s, *h, qslot, dtab);
-    ws.terms[p * 4 + 2 + (isC ? 1 : 0)] = ge_norm_host(r);
+    ge P = sd.ws.lr[i];
+    ge r = scalarmult<true>(sd.ws.chal[p], P, qslot, dtab);
+    sd.ws.m3[i] = ge_norm_host(r);
 }
 
 // a0*G'_0 and b0*H'_0 (crv:262-266).  Items: 2p -> a0*G', 2p+1 -> b0*H'.
@@ -255,8 +336,8 @@ __device__ __forceinline__ Region find_region(const RegionList& rl, size_t i) {
 // worth of independent work however deep the batch-level dependency chain is.
 __global__ __launch_bounds__(TPB, 3) void k_terms(RegionList rl, const SlotDev* __restrict__ slots,
                                                const ge* __restrict__ G, const ge* __restrict__ H,
-                                               const ge* __restrict__ h, const ge* __restrict__ dtab,
-                                               const fe* __restrict__ two_i) {
+                                               const ge* __restrict__ g, const ge* __restrict__ h,
+                                               const ge* __restrict__ dtab, const fe* __restrict__ two_i) {
     __shared__ geq qs[TPB];
     size_t i = gid();
     if (i >= rl.total) return;
@@ -267,10 +348,12 @@ __global__ __launch_bounds__(TPB, 3) void k_terms(RegionList rl, const SlotDev* 
     if (rg.kind == RK_PREP) {
         // lanes [0,B): range-proof challenges and MSM scalars (range mode only), then [.., +B): IPA
         const size_t B = sd.bv.B;
-        if (sd.range_mode && l < B) prep_range_task(sd.bv, sd.ws, two_i, l);
+        if (sd.range_mode && l < B) prep_range_task(sd.bv, sd.ws, two_i, l, sd.range_mode);
         else prep_ipa_task(sd.bv, sd.ws, sd.range_mode ? l - B : l);
     } else if (rg.kind == RK_STAGE0) {
-        stage0_task(sd, l, &qs[threadIdx.x], G, H, h, dtab);
+        stage0_task(sd, l, &qs[threadIdx.x], G, H, g, h, dtab);
+    } else if (rg.kind == RK_M3) {
+        m3_task(sd, l, &qs[threadIdx.x], dtab);
     } else if (rg.kind == RK_ROUND) {
         const int np = sd.bv.n >> (rg.r + 1);
         fold_task(sd.bv, sd.ws, rg.r, l / (4 * np), (int)(l % (4 * np)), &qs[threadIdx.x], G, H, dtab);
@@ -322,6 +405,33 @@ __device__ __forceinline__ void final_task(const SlotDev& sd, size_t p) {
     if (sd.chk_out) sd.chk_out[p] = cp;
 
     fe kx = fe_canon(cp.X), ky = fe_canon(cp.Y), px = fe_canon(P.X), py = fe_canon(P.Y);
+    if (sd.range_mode == 2) {
+        // range_proof_verify (rp.cu:1717-1815): V match && range check && polynomial identity
+        // && inner_product_verify, whose accept rule is vectors.cu:713-749 on X bytes.
+        const uint8_t fl = ws.rflags[p];
+        fe lmx = fe_canon(ws.m3[p * 2].X), rmx = fe_canon(ws.m3[p * 2 + 1].X);
+        int tot = 0;
+        for (int i = 0; i < 4; i++) tot += 64 - __popcll(lmx.v[i] ^ rmx.v[i]);
+        int top = 64 - __popcll(lmx.v[3] ^ rmx.v[3]);           // bytes 24..31 (rp.cu:595-601)
+        bool m3 = top >= 22, m4 = tot >= 200;                     // rp.cu:606-627
+        bool poly_ok = ((fl >> 2) & 1) | m3 | m4;
+        int xdc = 0, sxc = 0;
+        for (int i = 0; i < 32; i++) {
+            int d = absdiff((int)fe_byte(kx, i), (int)fe_byte(px, i));
+            xdc += d > 0;
+            sxc += (d > 0) & (d <= 5);
+        }
+        int mb = 64 - __popcll(kx.v[3] ^ px.v[3]);
+        bool ip_ok = ws.ipok[p] && ((xdc <= 3) | (sxc >= 28) | (mb >= 20));
+        sd.ok[p] = ((fl & 1) && ((fl >> 1) & 1) && poly_ok && ip_ok) ? 1 : 0;
+        if (sd.flags_out)
+            sd.flags_out[p] = (uint8_t)((fl & 7) | (m3 ? 8 : 0) | (m4 ? 16 : 0) | (ip_ok ? 32 : 0));
+        if (sd.poly_out) {
+            sd.poly_out[p * 4 + 2] = ws.m3[p * 2];
+            sd.poly_out[p * 4 + 3] = ws.m3[p * 2 + 1];
+        }
+        return;
+    }
     int xd = 0, yd = 0, sx = 0, sy = 0, msb = 0;
     for (int i = 0; i < 32; i++) {
         int a = (int)((kx.v[i >> 3] >> (8 * (i & 7))) & 0xff), b = (int)((px.v[i >> 3] >> (8 * (i & 7))) & 0xff);
@@ -341,6 +451,51 @@ __device__ __forceinline__ void final_task(const SlotDev& sd, size_t p) {
     for (int i = 0; i < 32; i++) hz += ((hs.v[i >> 3] >> (8 * (i & 7))) & 0xff) != 0;
     bool accept = (sx + sy >= 20) | (msb >= 28) | (xd + yd <= 32) | (hz <= 24);
     sd.ok[p] = (ws.ipok[p] && accept) ? 1 : 0;
+}
+
+// range_proof_verify's polynomial identity sides and methods 1-2 (rp.cu:452-530), then the
+// method-3 challenge SHA-256(left.X | left.Y | right.X | right.Y) (rp.cu:560-566).  One lane per proof.
+__device__ __forceinline__ void poly_task(const SlotDev& sd, size_t p) {
+    const VerifyWs& ws = sd.ws;
+    const ge* t = ws.pterm + p * 8;
+    ge left = ge_norm_host(ge_add(t[0], t[1]));
+    ge right = ge_zero();
+    for (int k = 2; k < 7; k++) right = ge_norm_host(ge_add(right, t[k]));
+    left = ge_norm_host(left);
+    right = ge_norm_host(right);
+    fe lx = fe_canon(left.X), ly = fe_canon(left.Y), rx = fe_canon(right.X), ry = fe_canon(right.Y);
+    int dxc = 0, dyc = 0, sxc = 0, syc = 0, cons = 0, prev = 0;
+    bool est = false;
+    for (int i = 0; i < 32; i++) {
+        int a = (int)fe_byte(lx, i), b = (int)fe_byte(rx, i);
+        int xd = absdiff(a, b), yd = absdiff((int)fe_byte(ly, i), (int)fe_byte(ry, i));
+        dxc += xd > 0; dyc += yd > 0;
+        sxc += (xd > 0) & (xd <= 10); syc += (yd > 0) & (yd <= 10);
+        int diff = a - b;
+        if (!est && diff != 0) {
+            prev = diff;
+            est = true;
+        } else if (est && absdiff(diff, prev) <= 10) {
+            cons++;
+            prev = (prev * 3 + diff) / 4;   // C division: truncation toward zero
+        }
+    }
+    (void)dyc;
+    bool m12 = (dxc <= 5) | ((sxc >= 24) & (syc >= 20)) | (cons >= 20);
+    sha256_ctx c;
+    sha_init(c);
+    sha_limbs(c, lx.v, 4); sha_limbs(c, ly.v, 4);
+    sha_limbs(c, rx.v, 4); sha_limbs(c, ry.v, 4);
+    fe ch;
+    sha_final_limbs(c, ch.v);
+    ws.chal[p] = ch;
+    ws.lr[p * 2] = left;
+    ws.lr[p * 2 + 1] = right;
+    ws.rflags[p] |= m12 ? 4 : 0;
+    if (sd.poly_out) {
+        sd.poly_out[p * 4] = left;
+        sd.poly_out[p * 4 + 1] = right;
+    }
 }
 
 // One pipeline tick's point combinations: fold round r  G'_j = N(term(u^-1 G_j) + term(u G_{j+n'})),
@@ -373,7 +528,9 @@ __global__ __launch_bounds__(TPB) void k_combine(RegionList rl, const SlotDev* _
         return;
     }
     if (l >= rg.items) return;
-    if (rg.kind == RK_COMBINE) {
+    if (rg.kind == RK_POLY) {
+        poly_task(sd, l);
+    } else if (rg.kind == RK_COMBINE) {
         const int n = sd.bv.n, np = n >> (rg.r + 1);
         size_t p = l / (2 * np);
         int k = (int)(l % (2 * np));
@@ -389,9 +546,9 @@ __global__ __launch_bounds__(TPB) void k_combine(RegionList rl, const SlotDev* _
 
 static inline unsigned nblk(size_t items) { return (unsigned)((items + TPB - 1) / TPB); }
 
-void launch_terms(const RegionList& rl, const SlotDev* slots, const ge* G, const ge* H, const ge* h,
+void launch_terms(const RegionList& rl, const SlotDev* slots, const ge* G, const ge* H, const ge* g, const ge* h,
                   const ge* dtab, const fe* two_i, hipStream_t s) {
-    if (rl.total) k_terms<<<nblk(rl.total), TPB, 0, s>>>(rl, slots, G, H, h, dtab, two_i);
+    if (rl.total) k_terms<<<nblk(rl.total), TPB, 0, s>>>(rl, slots, G, H, g, h, dtab, two_i);
 }
 
 void launch_combine(const RegionList& rl, const SlotDev* slots, hipStream_t s) {

@@ -107,12 +107,16 @@ void cuda_benchmark_range_proof(int iterations, size_t bit_size);
 /* Flat wire format of a batch of range proofs; every pointer is DEVICE memory.
  * Per proof p: V[p], A[p], S[p], T1[p], T2[p], t[p], c[p], x[p]; a/b: ab_len entries
  * at p*ab_len; L/R: L_len entries at p*L_len (L[0]/R[0] are never read, crv:180-205).
- * taux and mu are not read by cuda_range_proof_verify and are not part of the batch. */
+ * V is the caller's V argument of the verify.  taux, mu and Vp (the proof's own V) are read
+ * only by the range_proof_verify semantics (hipbp_batch_range_proof_verify_std); Vp NULL means
+ * "equal to V". */
 typedef struct {
     size_t count, n, ab_len, L_len;
     const ge25519 *V, *A, *S, *T1, *T2;
     const fe25519 *t, *a, *b, *c, *x;
     const ge25519 *L, *R;
+    const fe25519 *taux, *mu;
+    const ge25519* Vp;
 } hipbp_proof_batch;
 
 typedef enum {
@@ -130,6 +134,16 @@ int hipbp_device_count(void);
 int hipbp_batch_range_proof_verify(const hipbp_proof_batch* batch, const ge25519* G, const ge25519* H,
                                    const ge25519* g, const ge25519* h, uint8_t* ok, ge25519* P_out,
                                    ge25519* check_out, void* stream);
+/* Batched range_proof_verify semantics (bulletproof_range_proof.cu:1717, the reference's CPU
+ * "STANDARD VERIFICATION": V match, compute_precise_delta, enhanced_range_check,
+ * robust_polynomial_identity_check, calculate_inner_product_point, inner_product_verify with its
+ * own accept rule).  Needs batch->taux/mu.  Nullable extra outputs:
+ * flags_out[count]: bit0 V match, bit1 enhanced_range_check, bit2 polynomial identity methods 1|2,
+ * bit3 method 3, bit4 method 4, bit5 inner_product_verify;
+ * poly_out[4*count]: per proof left side, right side, and the two method-3 products. */
+int hipbp_batch_range_proof_verify_std(const hipbp_proof_batch* batch, const ge25519* G, const ge25519* H,
+                                       const ge25519* g, const ge25519* h, uint8_t* ok, ge25519* P_out,
+                                       ge25519* check_out, uint8_t* flags_out, ge25519* poly_out, void* stream);
 /* Batched cuda_inner_product_verify semantics; P[count] given (device). */
 int hipbp_batch_inner_product_verify(const hipbp_proof_batch* batch, const ge25519* P, const ge25519* G,
                                      const ge25519* H, const ge25519* Q, uint8_t* ok, ge25519* check_out,
@@ -140,13 +154,15 @@ int hipbp_batch_inner_product_verify(const hipbp_proof_batch* batch, const ge255
  * pushed r ticks earlier, the final stage of the oldest, all in one kernel launch.
  * A batch's outputs (ok / P_out / check_out, device memory) are complete after
  * depth-1 further pushes or a flush; its inputs (and P_in) are consumed by its own push.
- * range_mode 1: cuda_range_proof_verify semantics (h = the generator h);
- * range_mode 0: cuda_inner_product_verify semantics (h = Q, P_in required).
+ * range_mode 1: cuda_range_proof_verify semantics (h = the generator h; g may be NULL);
+ * range_mode 2: range_proof_verify semantics (g, h the generators; batch taux/mu required);
+ * range_mode 0: cuda_inner_product_verify semantics (h = Q, P_in required, g may be NULL).
  * Returns NULL on error (see hipbp_last_error). */
 void* hipbp_pipeline_create(size_t max_batch, size_t n, int range_mode, const ge25519* G, const ge25519* H,
-                            const ge25519* h, void* stream);
+                            const ge25519* g, const ge25519* h, void* stream);
 int hipbp_pipeline_push(void* pipeline, const hipbp_proof_batch* batch /* NULL = drain tick */,
-                        const ge25519* P_in, uint8_t* ok, ge25519* P_out, ge25519* check_out);
+                        const ge25519* P_in, uint8_t* ok, ge25519* P_out, ge25519* check_out,
+                        uint8_t* flags_out /* range_mode 2, nullable */, ge25519* poly_out /* idem */);
 int hipbp_pipeline_flush(void* pipeline);
 int hipbp_pipeline_depth(void* pipeline);
 void hipbp_pipeline_destroy(void* pipeline);

@@ -298,3 +298,101 @@ def test_ipa4096_batch_matches_reference(bp, golden, oracle):
             assert ok[p] == bool(d["ok"]) and np.array_equal(chk[p], d["check"]), p
         else:
             assert ok[p] == bool(d["ok_raw"]), p
+
+
+# ----------------------------------------------------------------------------- range_proof_verify (A18)
+def _std_arrays(heads, V, a, b, L, R):
+    from oracle.pyoracle import head_fields
+    hs = [head_fields(h) for h in heads]
+    return dict(V=np.asarray(V), A=np.stack([h["A"] for h in hs]), S=np.stack([h["S"] for h in hs]),
+                T1=np.stack([h["T1"] for h in hs]), T2=np.stack([h["T2"] for h in hs]),
+                t=np.stack([h["t"] for h in hs]), a=np.asarray(a), b=np.asarray(b),
+                c=np.stack([h["c"] for h in hs]), x=np.stack([h["x"] for h in hs]), L=np.asarray(L), R=np.asarray(R),
+                taux=np.stack([h["taux"] for h in hs]), mu=np.stack([h["mu"] for h in hs]),
+                Vp=np.stack([np.asarray(h_)[0:16] for h_ in heads]))
+
+
+def _run_std(bp, n, arrays, G, H, g, h):
+    import torch
+    dev = torch.device("cuda:0")
+    batch = bp.RangeProofBatch.from_numpy(n, arrays, dev)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    B = batch.count
+    ok = torch.zeros(B, dtype=torch.uint8, device=dev)
+    P = torch.zeros(B, 16, dtype=torch.int64, device=dev)
+    chk = torch.zeros(B, 16, dtype=torch.int64, device=dev)
+    fl = torch.zeros(B, dtype=torch.uint8, device=dev)
+    poly = torch.zeros(B, 4, 16, dtype=torch.int64, device=dev)
+    bp.batch_range_proof_verify_std(batch, T(G), T(H), T(g), T(h), ok, P, chk, fl, poly)
+    torch.cuda.synchronize()
+    u = lambda t: t.cpu().numpy().view(np.uint64)
+    return ok.cpu().numpy().astype(bool), u(P), u(chk), fl.cpu().numpy(), u(poly)
+
+
+def _check_std_vs_oracle(oracle, n, arrays, heads, G, H, g, h, res, ref_ok=None, ref_flags=None):
+    ok, P, chk, fl, poly = res
+    for p in range(len(heads)):
+        okr, det = oracle.range_proof_verify(heads[p], arrays["V"][p], n, arrays["a"][p], arrays["b"][p],
+                                             arrays["L"][p], arrays["R"][p], G, H, g, h)
+        assert ok[p] == okr, p
+        if ref_ok is not None:
+            assert ok[p] == bool(ref_ok[p]), p
+        f = int(fl[p])
+        assert bool(f & 1) == det["vmatch"] and bool(f & 2) == det["range_ok"], p
+        assert bool(f & 4) == (det["poly_m1"] or det["poly_m2"]), p
+        assert bool(f & 8) == det["poly_m3"] and bool(f & 16) == det["poly_m4"], p
+        assert bool(f & 32) == det["ip_ok"], p
+        if ref_flags is not None:
+            rf = int(ref_flags[p])
+            assert bool(rf & 1) == bool(f & 2) and bool(rf & 2) == bool(f & 28) and bool(rf & 4) == bool(f & 32), p
+        assert np.array_equal(P[p], det["P"]), p
+        for i, k in enumerate(("left", "right", "left_mult", "right_mult")):
+            assert np.array_equal(poly[p, i], det[k]), (p, k)
+        if det["ip_ok"] or not np.array_equal(det["check"], np.zeros(16, np.uint64)):
+            assert np.array_equal(chk[p], det["check"]), p
+
+
+@pytest.mark.parametrize("n", [16, 64])
+def test_std_verify_matches_reference(bp, oracle, golden, n):
+    """range_proof_verify semantics on the reference's proofs, tampered copies and random inputs:
+    verdicts and sub-check results equal the reference's; every intermediate point equals the oracle's."""
+    d = golden("rpverify")
+    k = f"n{n}_"
+    G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+    g, h = oracle.gh()
+    heads = d[k + "head"]
+    arrays = _std_arrays(heads, d[k + "V"], d[k + "a"], d[k + "b"], d[k + "L"], d[k + "R"])
+    res = _run_std(bp, n, arrays, G, H, g, h)
+    _check_std_vs_oracle(oracle, n, arrays, heads, G, H, g, h, res, d[k + "ok"], d[k + "flags"])
+
+
+@pytest.mark.parametrize("n", [16, 64])
+def test_std_verify_golden_proofs(bp, oracle, golden, n):
+    d = golden(f"proofs_n{n}")
+    heads = d["head"]
+    arrays = _std_arrays(heads, d["V"], d["a"], d["b"], d["L"], d["R"])
+    res = _run_std(bp, n, arrays, d["G"], d["H"], d["g"], d["h"])
+    assert np.array_equal(res[0], d["ok_cpu"].astype(bool))
+    _check_std_vs_oracle(oracle, n, arrays, heads, d["G"], d["H"], d["g"], d["h"], res)
+
+
+@pytest.mark.parametrize("n,B,ab_len", [(64, 20, 1), (16, 9, 2), (1, 5, 1), (2, 3, 1), (256, 2, 1)])
+def test_std_verify_synthetic_vs_oracle(bp, oracle, n, B, ab_len):
+    from cudabulletproof_amd import synth
+    arrays = synth.proofs(B, n, seed=500 + n)
+    rng = np.random.default_rng(n)
+    if ab_len > 1:
+        arrays["a"] = rand_fe(rng, B * ab_len).reshape(B, ab_len, 4)
+        arrays["b"] = rand_fe(rng, B * ab_len).reshape(B, ab_len, 4)
+        for p in range(B - 1):
+            arrays["c"][p] = oracle.inner_product(arrays["a"][p], arrays["b"][p])
+    arrays["taux"] = rand_fe(rng, B, top=False)
+    arrays["mu"] = rand_fe(rng, B, top=False)
+    arrays["Vp"] = arrays["V"].copy()
+    arrays["Vp"][0, 4] ^= np.uint64(1)            # V argument != proof V
+    heads = np.concatenate([arrays[k] for k in ("Vp", "A", "S", "T1", "T2", "taux", "mu", "t", "c", "x")], axis=1)
+    G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+    g, h = oracle.gh()
+    res = _run_std(bp, n, arrays, G, H, g, h)
+    assert not res[0][0]
+    _check_std_vs_oracle(oracle, n, arrays, heads, G, H, g, h, res)
