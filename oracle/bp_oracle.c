@@ -778,3 +778,225 @@ int orc_range_proof_verify(const orc_head* head, const orc_ge* V, size_t n, cons
     if (det) *det = d;
     return d.vmatch && d.range_ok && d.poly_ok && d.ip_ok;
 }
+
+/* ------------------------------------------------------------------ prover */
+/* bulletproof_range_proof.cu:277-297 pedersen_commit */
+static void pedersen(orc_ge* r, const orc_fe* value, const orc_fe* blinding, const orc_ge* g, const orc_ge* h) {
+    orc_ge t1, t2;
+    scalarmult_host_norm(&t1, value, g);
+    scalarmult_host_norm(&t2, blinding, h);
+    orc_ge_add(r, &t1, &t2);
+    orc_ge_normalize_host(r);
+}
+
+/* bulletproof_range_proof.cu:238-264 validate_range_input (n < 256) */
+static int validate_range(const orc_fe* v, size_t n) {
+    uint8_t vb[32];
+    orc_fe_tobytes(vb, v);
+    size_t bi = n / 8, bit = n % 8;
+    if (vb[bi] & (1u << bit)) return 0;
+    for (size_t i = bi + (bit == 7 ? 1 : 0); i < 32; i++)
+        if (vb[i]) return 0;
+    return 1;
+}
+
+/* bulletproof_vectors.cu:189-224 point_vector_multi_scalar_mul == orc_msm_cpu */
+
+/* bulletproof_vectors.cu:277-523 inner_product_prove on a/b (length n, modified in place) */
+static void ipa_prove(orc_fe* a, orc_fe* b, size_t n, const orc_ge* G, const orc_ge* H, const orc_ge* Q,
+                      const uint8_t transcript0[32], orc_ge* L_out, orc_ge* R_out, size_t* L_len, orc_fe* x_out) {
+    uint8_t tr[32];
+    memcpy(tr, transcript0, 32);
+    size_t rounds = 0;
+    for (size_t i = n; i > 1; i >>= 1) rounds++;
+    *L_len = rounds;
+    size_t np = n;
+    orc_fe* tmp = (orc_fe*)malloc((n ? n : 1) * sizeof(orc_fe));
+    for (size_t r = 0; r < rounds; r++) {
+        np >>= 1;
+        orc_fe cL, cR;
+        orc_inner_product(&cL, a, b + np, np);              /* <a_L, b_R> */
+        orc_inner_product(&cR, a + np, b, np);              /* <a_R, b_L> */
+        orc_ge L, R, t1, t2, t3;
+        orc_msm_cpu(&t1, a, G + np, np);                     /* <a_L, G_R> */
+        orc_msm_cpu(&t2, b + np, H, np);                     /* <b_R, H_L> */
+        uint8_t cb[32];
+        orc_fe_tobytes(cb, &cL);
+        orc_ge_scalarmult(&t3, cb, Q);
+        orc_ge_zero(&L);
+        orc_ge_add(&L, &L, &t1); orc_ge_add(&L, &L, &t2); orc_ge_add(&L, &L, &t3);
+        orc_ge_normalize_host(&L);
+        L_out[r] = L;
+        orc_msm_cpu(&t1, a + np, G, np);                     /* <a_R, G_L> */
+        orc_msm_cpu(&t2, b, H + np, np);                     /* <b_L, H_R> */
+        orc_fe_tobytes(cb, &cR);
+        orc_ge_scalarmult(&t3, cb, Q);
+        orc_ge_zero(&R);
+        orc_ge_add(&R, &R, &t1); orc_ge_add(&R, &R, &t2); orc_ge_add(&R, &R, &t3);
+        orc_ge_normalize_host(&R);
+        R_out[r] = R;
+        uint8_t d[96], ch[32];
+        memcpy(d, tr, 32);
+        orc_fe_tobytes(d + 32, &L.X);
+        orc_fe_tobytes(d + 64, &R.X);
+        orc_challenge(ch, d, 96, "InnerProductChal");
+        memcpy(tr, ch, 32);
+        orc_fe u, ui;
+        fe_from_le(&u, ch);
+        if (r == 0) *x_out = u;
+        orc_fe_invert(&ui, &u);
+        for (size_t j = 0; j < np; j++) {                    /* a' = u^-1 a_L + u a_R, b' = u b_L + u^-1 b_R */
+            orc_fe p1, p2;
+            orc_fe_mul(&p1, &u, &a[j + np]);
+            orc_fe_mul(&p2, &ui, &a[j]);
+            orc_fe_add(&tmp[j], &p2, &p1);
+        }
+        for (size_t j = 0; j < np; j++) {
+            orc_fe p1, p2;
+            orc_fe_mul(&p1, &u, &b[j]);
+            orc_fe_mul(&p2, &ui, &b[j + np]);
+            orc_fe_add(&b[j], &p1, &p2);
+        }
+        memcpy(a, tmp, np * sizeof(orc_fe));
+    }
+    free(tmp);
+}
+
+int orc_generate_range_proof(const uint8_t value32[32], const uint8_t gamma32[32], const uint8_t* sLR,
+                             const uint8_t rnd4[4][32], size_t n, const orc_ge* G, const orc_ge* H, const orc_ge* g,
+                             const orc_ge* h, orc_head* hd, orc_fe* a_out, orc_fe* b_out, orc_ge* L_out,
+                             orc_ge* R_out, size_t* L_len) {
+    orc_fe v, gamma, one, zero, two;
+    fe_from_le(&v, value32);
+    fe_from_le(&gamma, gamma32);
+    if (!validate_range(&v, n)) return -1;                   /* rp.cu:1176-1188 */
+    memset(hd, 0, sizeof(*hd));
+    fe_set(&one, 1);
+    fe_set(&zero, 0);
+    orc_fe_add(&two, &one, &one);
+    pedersen(&hd->V, &v, &gamma, g, h);                      /* rp.cu:1194 */
+    uint8_t vb[32];
+    orc_fe_tobytes(vb, &v);
+    orc_fe* aL = (orc_fe*)calloc(n, sizeof(orc_fe));
+    orc_fe* aR = (orc_fe*)calloc(n, sizeof(orc_fe));
+    orc_fe* sL = (orc_fe*)calloc(n, sizeof(orc_fe));
+    orc_fe* sR = (orc_fe*)calloc(n, sizeof(orc_fe));
+    orc_fe* py = (orc_fe*)calloc(n, sizeof(orc_fe));
+    orc_fe* p2 = (orc_fe*)calloc(n, sizeof(orc_fe));
+    orc_fe* l = (orc_fe*)calloc(n, sizeof(orc_fe));
+    orc_fe* rr = (orc_fe*)calloc(n, sizeof(orc_fe));
+    orc_fe* u1 = (orc_fe*)calloc(n, sizeof(orc_fe));
+    orc_fe* u2 = (orc_fe*)calloc(n, sizeof(orc_fe));
+    for (size_t i = 0; i < n; i++) {                         /* rp.cu:1218-1238 */
+        fe_set(&aL[i], (vb[i / 8] >> (i % 8)) & 1);
+        orc_fe_sub(&aR[i], &aL[i], &one);
+    }
+    for (size_t i = 0; i < n; i++) {                         /* rp.cu:1246-1252 */
+        fe_from_le(&sL[i], sLR + 64 * i);
+        fe_from_le(&sR[i], sLR + 64 * i + 32);
+    }
+    orc_fe alpha, rho, tau1, tau2;
+    fe_from_le(&alpha, rnd4[0]);
+    fe_from_le(&rho, rnd4[1]);
+    orc_ge t1, t2, t3;                                       /* rp.cu:1266-1290 */
+    orc_ge_scalarmult(&t1, rnd4[0], h);
+    orc_msm_cpu(&t2, aL, G, n);
+    orc_msm_cpu(&t3, aR, H, n);
+    orc_ge_add(&hd->A, &t1, &t2);
+    orc_ge_add(&hd->A, &hd->A, &t3);
+    orc_ge_normalize_host(&hd->A);
+    orc_ge_scalarmult(&t1, rnd4[1], h);
+    orc_msm_cpu(&t2, sL, G, n);
+    orc_msm_cpu(&t3, sR, H, n);
+    orc_ge_add(&hd->S, &t1, &t2);
+    orc_ge_add(&hd->S, &hd->S, &t3);
+    orc_ge_normalize_host(&hd->S);
+    uint8_t yb[32], zb[32], xb[32];                          /* rp.cu:1302-1332 */
+    orc_fe y, z, z2, x, x2;
+    challenge_y(yb, &hd->V, &hd->A, &hd->S);
+    challenge_z(zb, yb);
+    fe_from_le(&y, yb);
+    fe_from_le(&z, zb);
+    orc_fe_mul(&z2, &z, &z);
+    fe_set(&py[0], 1);                                       /* powers_of (rp.cu:299) */
+    for (size_t i = 1; i < n; i++) orc_fe_mul(&py[i], &py[i - 1], &y);
+    orc_fe tp;
+    fe_set(&tp, 1);
+    for (size_t i = 0; i < n; i++) {                         /* rp.cu:1347-1350 */
+        p2[i] = tp;
+        orc_fe_mul(&tp, &tp, &two);
+    }
+    /* t0 = <aL - z, y^n o (aR + z)> + z^2 <1, 2^n>   (rp.cu:1370-1407) */
+    for (size_t i = 0; i < n; i++) {
+        orc_fe_sub(&l[i], &aL[i], &z);                       /* aL - z */
+        orc_fe_add(&rr[i], &aR[i], &z);                      /* aR + z */
+        orc_fe_mul(&u1[i], &py[i], &rr[i]);                  /* y^n o (aR + z) */
+        orc_fe_mul(&u2[i], &py[i], &sR[i]);                  /* y^n o sR */
+    }
+    orc_fe t0, s2n, zs2n, t1a, t1b, tt1, tt2;
+    orc_inner_product(&t0, l, u1, n);
+    fe_set(&s2n, 0);
+    for (size_t i = 0; i < n; i++) orc_fe_add(&s2n, &s2n, &p2[i]);
+    orc_fe_mul(&zs2n, &z2, &s2n);
+    orc_fe_add(&t0, &t0, &zs2n);
+    orc_inner_product(&t1a, sL, u1, n);                      /* rp.cu:1418-1426 */
+    orc_inner_product(&t1b, l, u2, n);
+    orc_fe_add(&tt1, &t1a, &t1b);
+    orc_inner_product(&tt2, sL, u2, n);                      /* rp.cu:1430 */
+    fe_from_le(&tau1, rnd4[2]);
+    fe_from_le(&tau2, rnd4[3]);
+    pedersen(&hd->T1, &tt1, &tau1, g, h);                    /* rp.cu:1442-1445 */
+    pedersen(&hd->T2, &tt2, &tau2, g, h);
+    orc_ge_normalize_host(&hd->T1);
+    orc_ge_normalize_host(&hd->T2);
+    challenge_x(xb, &hd->T1, &hd->T2);                       /* rp.cu:1452 */
+    fe_from_le(&x, xb);
+    orc_fe_mul(&x2, &x, &x);
+    orc_fe m1, m2, t;                                        /* rp.cu:1470-1495 */
+    orc_fe_mul(&m1, &tt1, &x);
+    orc_fe_mul(&m2, &tt2, &x2);
+    t = t0;
+    orc_fe_add(&t, &t, &m1);
+    orc_fe_add(&t, &t, &m2);
+    hd->t = t;
+    orc_fe_mul(&hd->taux, &tau1, &x);
+    orc_fe_mul(&m2, &tau2, &x2);
+    orc_fe_add(&hd->taux, &hd->taux, &m2);
+    orc_fe_mul(&m1, &rho, &x);
+    orc_fe_add(&hd->mu, &alpha, &m1);
+    for (size_t i = 0; i < n; i++) {                         /* l(x), r(x) (rp.cu:1515-1580) */
+        orc_fe e, sx;
+        orc_fe_sub(&e, &aL[i], &z);
+        orc_fe_mul(&sx, &sL[i], &x);
+        orc_fe_add(&l[i], &e, &sx);
+        orc_fe_add(&e, &aR[i], &z);
+        orc_fe_mul(&sx, &sR[i], &x);
+        orc_fe_add(&e, &e, &sx);
+        orc_fe_mul(&e, &e, &py[i]);
+        orc_fe_mul(&sx, &z2, &p2[i]);
+        orc_fe_add(&rr[i], &e, &sx);
+    }
+    orc_fe ip;
+    uint8_t ib[32], tb[32];
+    orc_inner_product(&ip, l, rr, n);                        /* rp.cu:1600-1622 */
+    orc_fe_tobytes(ib, &ip);
+    orc_fe_tobytes(tb, &t);
+    if (memcmp(ib, tb, 32) != 0) {
+        memset(l, 0, n * sizeof(orc_fe));
+        memset(rr, 0, n * sizeof(orc_fe));
+        l[0] = t;
+        fe_set(&rr[0], 1);
+    }
+    uint8_t fc[96], ipc[32];                                 /* rp.cu:1636-1650 */
+    orc_fe_tobytes(fc, &t);
+    orc_fe_tobytes(fc + 32, &hd->taux);
+    orc_fe_tobytes(fc + 64, &hd->mu);
+    orc_challenge(ipc, fc, 96, "BulletproofIP");
+    fe_set(&hd->x, 0);
+    ipa_prove(l, rr, n, G, H, h, ipc, L_out, R_out, L_len, &hd->x);   /* rp.cu:1656 */
+    a_out[0] = t;                                            /* fix_inner_product_proof (rp.cu:198-235) */
+    fe_set(&b_out[0], 1);
+    hd->c = t;
+    free(aL); free(aR); free(sL); free(sR); free(py); free(p2); free(l); free(rr); free(u1); free(u2);
+    return 0;
+}

@@ -86,6 +86,17 @@ int orc_range_proof_verify(const orc_head* head, const orc_ge* V, size_t n, cons
                            size_t ab_len, const orc_ge* L, const orc_ge* R, size_t L_len, const orc_ge* G,
                            const orc_ge* H, const orc_ge* g, const orc_ge* h, orc_rpv_detail* det);
 
+/* generate_range_proof (bulletproof_range_proof.cu:1159-1715) + inner_product_prove
+ * (bulletproof_vectors.cu:277-523) + fix_inner_product_proof (rp.cu:198), with the prover's random
+ * scalars given (each the 32 bytes generate_random_scalar, rp.cu:153, produced — masks applied):
+ * gamma (the V blinding), sLR[2i] = sL_i, sLR[2i+1] = sR_i (n pairs, generated interleaved),
+ * rnd4 = alpha, rho, tau1, tau2.  Returns -1 when validate_range_input (rp.cu:238) refuses the
+ * value (outputs untouched), else 0; a/b get the final length-1 vectors, L/R log2(n) points. */
+int orc_generate_range_proof(const uint8_t value32[32], const uint8_t gamma32[32], const uint8_t* sLR,
+                             const uint8_t rnd4[4][32], size_t n, const orc_ge* G, const orc_ge* H, const orc_ge* g,
+                             const orc_ge* h, orc_head* head_out, orc_fe* a_out, orc_fe* b_out, orc_ge* L_out,
+                             orc_ge* R_out, size_t* L_len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -65,6 +65,7 @@ class Oracle(_Lib):
         self.lib.orc_cuda_range_proof_verify.restype = ctypes.c_int
         self.lib.orc_cuda_inner_product_verify.restype = ctypes.c_int
         self.lib.orc_range_proof_verify.restype = ctypes.c_int
+        self.lib.orc_generate_range_proof.restype = ctypes.c_int
 
     # field ------------------------------------------------------------
     def _fe2(self, name, f, g):
@@ -234,6 +235,23 @@ class Oracle(_Lib):
         return bool(ok), d
 
 
+    def generate_range_proof(self, value32, gamma32, sLR, rnd4, n, G, H, g, h):
+        """orc_generate_range_proof -> dict(head, V, a, b, L, R) or None (value refused)."""
+        head = np.zeros(HEAD_WORDS, np.uint64)
+        a, b = fe(1), fe(1)
+        L, R = ge(max(n, 1)), ge(max(n, 1))
+        ll = _sz()
+        r = self.f("generate_range_proof")(
+            _p(np.ascontiguousarray(value32, np.uint8)), _p(np.ascontiguousarray(gamma32, np.uint8)),
+            _p(np.ascontiguousarray(sLR, np.uint8)), _p(np.ascontiguousarray(rnd4, np.uint8)), _sz(n),
+            _p(np.ascontiguousarray(G, np.uint64)), _p(np.ascontiguousarray(H, np.uint64)),
+            _p(np.ascontiguousarray(g, np.uint64)), _p(np.ascontiguousarray(h, np.uint64)), _p(head), _p(a), _p(b),
+            _p(L), _p(R), ctypes.byref(ll))
+        if r != 0:
+            return None
+        return dict(head=head, V=head[0:16].copy(), a=a, b=b, L=L[:ll.value].copy(), R=R[:ll.value].copy())
+
+
 class Reference(_Lib):
     """The reference's own host code (oracle/_ref/libbpref.so)."""
 
@@ -350,6 +368,26 @@ class Reference(_Lib):
         delta, flags = fe(), ctypes.c_int()
         self.f("rpv_parts")(*self._vargs(pr, n, G, H, g, h), _p(delta), ctypes.byref(flags))
         return delta, flags.value
+
+
+def prover_randomness(seed, n):
+    """The random scalars the reference prover draws under oracle/ref's deterministic RAND_bytes
+    (block k = SHA256(seed_le64 || k_le64)), each masked as generate_random_scalar does (rp.cu:153-159):
+    gamma (ref_prove's blinding), then sL_i, sR_i interleaved (rp.cu:1246-1252), alpha, rho, tau1, tau2.
+    Returns (gamma (32,), sLR (n, 64), rnd4 (4, 32)) as uint8."""
+    import hashlib
+
+    def block(k):
+        b = bytearray(hashlib.sha256(int(seed).to_bytes(8, "little") + int(k).to_bytes(8, "little")).digest())
+        b[31] &= 0x7F
+        b[0] &= 0xF8
+        b[31] |= 0x40
+        return np.frombuffer(bytes(b), np.uint8)
+    gamma = block(0)
+    sLR = np.stack([np.concatenate([block(1 + 2 * i), block(2 + 2 * i)]) for i in range(n)]) if n else \
+        np.zeros((0, 64), np.uint8)
+    rnd4 = np.stack([block(2 * n + 1 + k) for k in range(4)])
+    return gamma, sLR, rnd4
 
 
 def have_reference():

@@ -129,3 +129,33 @@ def test_range_proof_verify_golden_proofs(oracle, golden):
             ok, _ = oracle.range_proof_verify(d["head"][i], d["V"][i], n, d["a"][i], d["b"][i], d["L"][i], d["R"][i],
                                               d["G"], d["H"], d["g"], d["h"])
             assert ok == bool(d["ok_cpu"][i]), (n, i)
+
+
+@pytest.mark.parametrize("n", [16, 64])
+def test_prover_against_reference(oracle, golden, n):
+    """§8(f) rank 1: generate_range_proof + inner_product_prove + fix_inner_product_proof restated,
+    on the reference's own proofs (same values, same RAND_bytes stream): every proof byte equal."""
+    from oracle.pyoracle import prover_randomness
+    d = golden(f"proofs_n{n}")
+    for i in range(len(d["head"])):
+        gamma, sLR, rnd4 = prover_randomness(i + 1, n)   # make_golden.py: seed = i + 1
+        pr = oracle.generate_range_proof(d["value"][i], gamma, sLR, rnd4, n, d["G"], d["H"], d["g"], d["h"])
+        assert np.array_equal(pr["head"], d["head"][i]), i
+        for k in ("V", "a", "b", "L", "R"):
+            assert np.array_equal(pr[k], d[k][i]), (i, k)
+
+
+def test_prover_refuses_out_of_range(oracle):
+    """validate_range_input (rp.cu:238): bit n or any higher byte set -> no proof."""
+    from oracle.pyoracle import prover_randomness
+    n = 16
+    G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+    g, h = oracle.gh()
+    gamma, sLR, rnd4 = prover_randomness(3, n)
+    for bad in ((2, 0x01), (5, 0x80), (31, 0x01)):
+        v = np.zeros(32, np.uint8)
+        v[bad[0]] = bad[1]
+        assert oracle.generate_range_proof(v, gamma, sLR, rnd4, n, G, H, g, h) is None
+    v = np.zeros(32, np.uint8)
+    v[0], v[1] = 0xFF, 0xFF                                # 2^16 - 1: in range
+    assert oracle.generate_range_proof(v, gamma, sLR, rnd4, n, G, H, g, h) is not None
