@@ -23,7 +23,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB_PATH = os.path.join(HERE, "libcudabulletproof_hip.so")
 CSRC = os.path.join(HERE, "csrc")
-SOURCES = ["bp_kernels.hip", "bp_capi.hip"]
+SOURCES = ["bp_kernels.hip", "bp_prove.hip", "bp_capi.hip"]
 
 _lib = None
 
@@ -77,6 +77,14 @@ class ProofBatchC(ctypes.Structure):   # hipbp_proof_batch
                [(k, _c) for k in ("V", "A", "S", "T1", "T2", "t", "a", "b", "c", "x", "L", "R", "taux", "mu", "Vp")]
 
 
+class ProveInputC(ctypes.Structure):   # hipbp_prove_input
+    _fields_ = [("count", _sz), ("n", _sz)] + [(k, _c) for k in ("v", "gamma", "sL", "sR", "rnd")]
+
+
+class ProofOutC(ctypes.Structure):   # hipbp_proof_out
+    _fields_ = [(k, _c) for k in ("V", "A", "S", "T1", "T2", "taux", "mu", "t", "c", "x", "a", "b", "L", "R", "valid")]
+
+
 assert ctypes.sizeof(InnerProductProof) == 144 and ctypes.sizeof(RangeProofC) == 880
 
 EXPORTS = [
@@ -87,7 +95,8 @@ EXPORTS = [
     "cuda_batch_field_invert", "cuda_soa_field_add", "cuda_range_proof_verify", "cuda_inner_product_verify",
     "cuda_benchmark_multi_scalar_mul", "cuda_benchmark_inner_product", "cuda_benchmark_field_operations",
     "cuda_benchmark_range_proof", "hipbp_last_error", "hipbp_device_count", "hipbp_batch_range_proof_verify",
-    "hipbp_batch_range_proof_verify_std", "hipbp_batch_inner_product_verify", "hipbp_msm", "hipbp_point_tree", "hipbp_field_op", "hipbp_sync", "hipbp_timing_enable",
+    "hipbp_batch_range_proof_verify_std", "hipbp_batch_inner_product_verify", "hipbp_batch_generate_range_proof", "hipbp_msm",
+    "hipbp_point_tree", "hipbp_field_op", "hipbp_sync", "hipbp_timing_enable",
     "hipbp_timing_collect", "hipbp_kernel_count", "hipbp_kernel_name", "hipbp_pipeline_create",
     "hipbp_pipeline_push", "hipbp_pipeline_flush", "hipbp_pipeline_depth", "hipbp_pipeline_destroy",
 ]
@@ -111,7 +120,8 @@ def lib():
         for f in ("cuda_range_proof_verify", "cuda_inner_product_verify"):
             getattr(L, f).restype = ctypes.c_bool
         for f in ("hipbp_batch_range_proof_verify", "hipbp_batch_range_proof_verify_std",
-                  "hipbp_batch_inner_product_verify", "hipbp_msm", "hipbp_point_tree",
+                  "hipbp_batch_inner_product_verify", "hipbp_batch_generate_range_proof", "hipbp_msm",
+                  "hipbp_point_tree",
                   "hipbp_field_op", "hipbp_sync", "hipbp_device_count"):
             getattr(L, f).restype = ctypes.c_int
         _lib = L
@@ -345,6 +355,32 @@ def batch_inner_product_verify(batch, P, G, H, Q, ok, check_out=None, stream=Non
     _chk(lib().hipbp_batch_inner_product_verify(
         ctypes.byref(s), _c(P.data_ptr()), _c(G.data_ptr()), _c(H.data_ptr()), _c(Q.data_ptr()), _c(ok.data_ptr()),
         _c(check_out.data_ptr()) if check_out is not None else None, _stream_ptr(stream)))
+
+
+def batch_generate_range_proof(n, v, gamma, sL, sR, rnd, G, H, g, h, stream=None):
+    """generate_range_proof (bulletproof_range_proof.cu:1159) over a batch, on the GPU.
+
+    v, gamma (B,4); sL, sR (B,n,4); rnd (B,4,4) = alpha, rho, tau1, tau2: int64 CUDA tensors of the
+    u64 limbs (the random scalars exactly as generate_random_scalar produced them).  Returns a dict
+    of CUDA tensors in RangeProofBatch layout (V, A, S, T1, T2, t, a, b, c, x, L, R, taux, mu) plus
+    "valid" (B,) uint8; RangeProofBatch(n, **out) verifies it directly."""
+    import torch
+    B = int(v.shape[0])
+    Lr = int(n).bit_length() - 1
+    dev = v.device
+    z = lambda *shape: torch.zeros(*shape, dtype=torch.int64, device=dev)
+    out = dict(V=z(B, 16), A=z(B, 16), S=z(B, 16), T1=z(B, 16), T2=z(B, 16), taux=z(B, 4), mu=z(B, 4), t=z(B, 4),
+               c=z(B, 4), x=z(B, 4), a=z(B, 1, 4), b=z(B, 1, 4), L=z(B, max(Lr, 0), 16), R=z(B, max(Lr, 0), 16),
+               valid=torch.zeros(B, dtype=torch.uint8, device=dev))
+    ins = [t.contiguous() for t in (v, gamma, sL, sR, rnd)]
+    ic = ProveInputC(B, int(n), *[t.data_ptr() for t in ins])
+    oc = ProofOutC(*[out[k].data_ptr() if out[k].numel() else None for k in
+                     ("V", "A", "S", "T1", "T2", "taux", "mu", "t", "c", "x", "a", "b", "L", "R", "valid")])
+    _chk(lib().hipbp_batch_generate_range_proof(ctypes.byref(ic), _c(G.data_ptr()), _c(H.data_ptr()),
+                                                _c(g.data_ptr()), _c(h.data_ptr()), ctypes.byref(oc),
+                                                _stream_ptr(stream)))
+    out["_keep"] = ins
+    return out
 
 
 def msm(result, scalars, points, stream=None):

@@ -128,6 +128,7 @@ struct Engine {
     int two_cap = 0;
     // single-call staging
     Buf h2d[8], scratch[8];
+    Buf prv[14];   // prover workspace (hipbp_batch_generate_range_proof)
     // pinned host staging for the single-proof entry points (a pageable source of an
     // async copy must outlive the copy; this one does, and the stream is synced after use)
     uint8_t* pinned = nullptr;
@@ -589,6 +590,59 @@ int hipbp_msm(ge25519* result, const fe25519* scalars, const ge25519* points, si
     BP_RET_ON(e->scratch[2].need(nb * sizeof(bp::ge)));
     bp::launch_msm_full((bp::ge*)result, (const bp::fe*)scalars, (const bp::ge*)points, n, e->scratch[0].as<bp::ge>(),
                         e->scratch[1].as<bp::ge>(), e->scratch[2].as<bp::ge>(), e->dtab, pick(stream, *e));
+    BP_RET_ON(hipGetLastError());
+    return HIPBP_OK;
+}
+
+int hipbp_batch_generate_range_proof(const hipbp_prove_input* in, const ge25519* G, const ge25519* H,
+                                     const ge25519* g, const ge25519* h, hipbp_proof_out* out, void* stream) {
+    hipError_t err;
+    Engine* e = engine_or_null(&err);
+    BP_RET_ON(err);
+    if (!in || !out || !G || !H || !g || !h) { g_err = "null argument"; return HIPBP_ERR_ARG; }
+    if (in->count == 0) return HIPBP_OK;
+    if (!is_pow2(in->n) || in->n > 128) { g_err = "prover: n must be a power of two <= 128"; return HIPBP_ERR_ARG; }
+    if (in->count > ((size_t)1 << 22)) { g_err = "prover: batch too large"; return HIPBP_ERR_ARG; }
+    if (!in->v || !in->gamma || !in->sL || !in->sR || !in->rnd) { g_err = "prover: null input"; return HIPBP_ERR_ARG; }
+    if (!out->V || !out->A || !out->S || !out->T1 || !out->T2 || !out->taux || !out->mu || !out->t || !out->c ||
+        !out->x || !out->a || !out->b || !out->valid || (in->n > 1 && (!out->L || !out->R))) {
+        g_err = "prover: null output";
+        return HIPBP_ERR_ARG;
+    }
+    std::lock_guard<std::mutex> lk(e->mu);
+    BP_RET_ON(e->ensure_two((int)in->n));
+    const size_t B = in->count, n = in->n;
+    bp::ProveIn pin{(int)B, (int)n, log2i(n), (const bp::fe*)in->v, (const bp::fe*)in->gamma,
+                    (const bp::fe*)in->sL, (const bp::fe*)in->sR, (const bp::fe*)in->rnd};
+    bp::ProveOut po{(bp::ge*)out->V, (bp::ge*)out->A, (bp::ge*)out->S, (bp::ge*)out->T1, (bp::ge*)out->T2,
+                    (bp::fe*)out->taux, (bp::fe*)out->mu, (bp::fe*)out->t, (bp::fe*)out->c, (bp::fe*)out->x,
+                    (bp::fe*)out->a, (bp::fe*)out->b, (bp::ge*)out->L, (bp::ge*)out->R, out->valid};
+    // workspace: prover buffers are the engine's prv[] (reused across calls on the engine's lock)
+    const size_t FE = sizeof(bp::fe), GE = sizeof(bp::ge);
+    size_t sz[14] = {B * 4 * n * FE, B * (4 * n + 4) * GE, B * 4 * GE, B * 5 * GE, B * 8 * FE, B * 4 * FE, B * 4 * GE,
+                     B * n * FE, B * n * FE, B * 2 * n * FE, B * 2 * FE, B * (2 * n + 2) * GE, B * 4 * FE, B};
+    for (int i = 0; i < 14; i++) BP_RET_ON(e->prv[i].need(sz[i]));
+    bp::ProveWs w{e->prv[0].as<bp::fe>(), e->prv[1].as<bp::ge>(), e->prv[2].as<bp::ge>(), e->prv[3].as<bp::ge>(),
+                  e->prv[4].as<bp::fe>(), e->prv[5].as<bp::fe>(), e->prv[6].as<bp::ge>(), e->prv[7].as<bp::fe>(),
+                  e->prv[8].as<bp::fe>(), e->prv[9].as<bp::fe>(), e->prv[10].as<bp::fe>(), e->prv[11].as<bp::ge>(),
+                  e->prv[12].as<bp::fe>(), e->prv[13].as<uint8_t>()};
+    hipStream_t s = pick(stream, *e);
+    auto run = [&](int stage, int r) {
+        bp::launch_prove(stage, r, pin, w, po, (const bp::ge*)G, (const bp::ge*)H, (const bp::ge*)g,
+                         (const bp::ge*)h, e->dtab, e->two_i, s);
+    };
+    run(bp::PS_PREP, 0);
+    run(bp::PS_TERMS0, 0);
+    run(bp::PS_CHAIN0, 0);
+    run(bp::PS_COMMIT, 0);
+    run(bp::PS_TERMS1, 0);
+    run(bp::PS_TX, 0);
+    for (int r = 0; r < pin.L; r++) {
+        run(bp::PS_RTERMS, r);
+        run(bp::PS_RCHAIN, r);
+        run(bp::PS_ROUND, r);
+    }
+    run(bp::PS_FINAL, 0);
     BP_RET_ON(hipGetLastError());
     return HIPBP_OK;
 }

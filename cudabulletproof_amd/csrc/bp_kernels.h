@@ -105,6 +105,44 @@ void launch_tree(ge* out, const ge* in, int S, size_t m, hipStream_t s);
 
 
 
+// ------------------------------------------------------------------ prover (bp_prove.hip)
+// Inputs of a batch of generate_range_proof calls (include/cudabulletproof_hip.h hipbp_prove_input).
+struct ProveIn {
+    int B, n, L;
+    const fe* v;       // [B] value (fe25519_frombytes of the value bytes)
+    const fe* gamma;   // [B] V blinding (raw random scalar)
+    const fe* sL;      // [B*n]
+    const fe* sR;      // [B*n]
+    const fe* rnd;     // [B*4] alpha, rho, tau1, tau2 (raw random scalars)
+};
+struct ProveOut {
+    ge *V, *A, *S, *T1, *T2;
+    fe *taux, *mu, *t, *c, *x, *a, *b;
+    ge *L, *R;          // [B*L]
+    uint8_t* valid;     // [B]
+};
+// Prover workspace (per batch).
+struct ProveWs {
+    fe* ps;       // [B*4n]    MSM scalars aL | aR | sL | sR (host tobytes form)
+    ge* pterm;    // [B*(4n+4)] aL_i G_i | aR_i H_i | sL_i G_i | sR_i H_i | g^v | h^gamma | h^alpha | h^rho
+    ge* chain;    // [B*4]     sequential MSM accumulations (point_vector_multi_scalar_mul order)
+    ge* pts;      // [B*5]     V, A, S, T1, T2
+    fe* st;       // [B*8]     y, z, z^2, t0, t1, t2, t, transcript
+    fe* tsc;      // [B*4]     t1, tau1, t2, tau2 (tobytes form)
+    ge* tt;       // [B*4]     g^t1, h^tau1, g^t2, h^tau2
+    fe* acur;     // [B*n]     IPA a (folded in place)
+    fe* bcur;     // [B*n]     IPA b
+    fe* iscal;    // [B*2n]    round MSM scalars a_L | b_R | a_R | b_L
+    fe* csc;      // [B*2]     c_L, c_R (tobytes form)
+    ge* iterm;    // [B*(2n+2)] round terms + c_L Q, c_R Q
+    fe* misc;     // [B*4]     taux, mu, x
+    uint8_t* valid;   // [B]
+};
+enum ProveStage { PS_PREP = 0, PS_TERMS0, PS_CHAIN0, PS_COMMIT, PS_TERMS1, PS_TX, PS_RTERMS, PS_RCHAIN, PS_ROUND,
+                  PS_FINAL };
+void launch_prove(int stage, int r, const ProveIn& in, const ProveWs& ws, const ProveOut& out, const ge* G,
+                  const ge* H, const ge* g, const ge* h, const ge* dtab, const fe* two_i, hipStream_t s);
+
 // Elementwise field ops: op 0 add, 1 sub, 2 mul, 3 square-kernel quirk, 4 soa add (limbwise, no carry)
 void launch_field_op(int op, fe* r, const fe* a, const fe* b, size_t count, hipStream_t s);
 void launch_ip_shared(fe* out, const fe* a, const fe* b, size_t n, hipStream_t s);

@@ -83,19 +83,7 @@ void launch_tree(ge* out, const ge* in, int S, size_t m, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------ verify: challenges & scalars
-__device__ __forceinline__ void sha_fe_canon(sha256_ctx& c, const fe& f) {
-    fe t = fe_canon(f);
-    sha_limbs(c, t.v, 4);
-}
 
-__device__ __forceinline__ fe challenge_digest(sha256_ctx& c) {
-    fe r;
-    sha_final_limbs(c, r.v);
-    r.v[3] &= 0x7FFFFFFFFFFFFFFFull;   // output[31] &= 0x7F (bulletproof_challenge.cu:20)
-    return r;
-}
-
-__device__ __forceinline__ uint32_t fe_byte(const fe& f, int i) { return (uint32_t)(f.v[i >> 3] >> (8 * (i & 7))) & 0xff; }
 
 // range_proof_verify's scalar work (mode 2), one lane per proof: the x challenge
 // (challenge.cu:61-77), compute_precise_delta (rp.cu:315-410), enhanced_range_check

@@ -319,6 +319,8 @@ BP_DEV fe fe_square_kernel_quirk(const fe& f) {
     return fe_fold512(t);
 }
 
+BP_DEV uint32_t fe_byte(const fe& f, int i) { return (uint32_t)(f.v[i >> 3] >> (8 * (i & 7))) & 0xff; }
+
 BP_DEV uint32_t fe_bit(const fe& s, int i) { return (uint32_t)(s.v[i >> 6] >> (i & 63)) & 1u; }
 
 }  // namespace bp

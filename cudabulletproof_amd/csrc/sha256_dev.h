@@ -3,6 +3,7 @@
 // hash term of the tolerant accept rule (cuda_range_proof_verify.cu:330-344).
 // One lane hashes one message; messages on this path are < 256 bytes.
 #pragma once
+#include "fe25519_dev.h"
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -104,6 +105,20 @@ __device__ __forceinline__ void sha_final_limbs(sha256_ctx& c, uint64_t out[4]) 
         uint64_t lo = __builtin_bswap32(w0), hi = __builtin_bswap32(w1);
         out[i] = lo | (hi << 32);
     }
+}
+
+// host fe25519_tobytes (canonicalising) into the hash (challenge inputs, bulletproof_challenge.cu)
+__device__ __forceinline__ void sha_fe_canon(sha256_ctx& c, const fe& f) {
+    fe t = fe_canon(f);
+    sha_limbs(c, t.v, 4);
+}
+
+// generate_challenge's digest as a field element: output[31] &= 0x7F (bulletproof_challenge.cu:20)
+__device__ __forceinline__ fe challenge_digest(sha256_ctx& c) {
+    fe r;
+    sha_final_limbs(c, r.v);
+    r.v[3] &= 0x7FFFFFFFFFFFFFFFull;
+    return r;
 }
 
 }  // namespace bp

@@ -167,6 +167,32 @@ int hipbp_pipeline_flush(void* pipeline);
 int hipbp_pipeline_depth(void* pipeline);
 void hipbp_pipeline_destroy(void* pipeline);
 
+/* ---- prover: generate_range_proof (bulletproof_range_proof.cu:1159) + inner_product_prove
+ * (bulletproof_vectors.cu:277) + fix_inner_product_proof (rp.cu:198), batched, bit-exact.
+ * The prover's randomness is an input: each random scalar is the 32 bytes that
+ * generate_random_scalar (rp.cu:153) produces (RAND_bytes + its masks), as 4 LE limbs.
+ * All pointers DEVICE memory.  n: power of two, 1..128 (validate_range_input reads byte n/8). */
+typedef struct {
+    size_t count, n;
+    const fe25519* v;       /* [count] value (fe25519_frombytes of the value bytes) */
+    const fe25519* gamma;   /* [count] blinding of V = g^v h^gamma */
+    const fe25519* sL;      /* [count*n] */
+    const fe25519* sR;      /* [count*n] */
+    const fe25519* rnd;     /* [count*4] alpha, rho, tau1, tau2 */
+} hipbp_prove_input;
+/* Output in the flat wire format of hipbp_proof_batch (ab_len = 1, L_len = log2 n), so it can be
+ * verified as is.  valid[p] = 0: validate_range_input refused the value; the proof is then the
+ * reference's zeroed one (V, A, S, T1, T2 identity; taux, mu, t 0; the rest 0). */
+typedef struct {
+    ge25519 *V, *A, *S, *T1, *T2;          /* [count] */
+    fe25519 *taux, *mu, *t, *c, *x;        /* [count] */
+    fe25519 *a, *b;                        /* [count] */
+    ge25519 *L, *R;                        /* [count*L_len] */
+    uint8_t* valid;                        /* [count] */
+} hipbp_proof_out;
+int hipbp_batch_generate_range_proof(const hipbp_prove_input* in, const ge25519* G, const ge25519* H,
+                                     const ge25519* g, const ge25519* h, hipbp_proof_out* out, void* stream);
+
 /* Canonical-tree MSM on device buffers. */
 int hipbp_msm(ge25519* result, const fe25519* scalars, const ge25519* points, size_t n, void* stream);
 /* Canonical tree over n device points: for stride 1, 2, 4, ...: T[i] = Ndev(T[i] + T[i+stride])

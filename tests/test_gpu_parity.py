@@ -396,3 +396,109 @@ def test_std_verify_synthetic_vs_oracle(bp, oracle, n, B, ab_len):
     res = _run_std(bp, n, arrays, G, H, g, h)
     assert not res[0][0]
     _check_std_vs_oracle(oracle, n, arrays, heads, G, H, g, h, res)
+
+
+# ----------------------------------------------------------------------------- prover (§8(f) rank 1)
+def _prove_inputs(seeds, values, n):
+    from oracle.pyoracle import prover_randomness
+    B = len(seeds)
+    gam = np.zeros((B, 4), np.uint64)
+    sL = np.zeros((B, n, 4), np.uint64)
+    sR = np.zeros((B, n, 4), np.uint64)
+    rnd = np.zeros((B, 4, 4), np.uint64)
+    rb = []
+    for p, sd in enumerate(seeds):
+        gamma, sLR, rnd4 = prover_randomness(sd, n)
+        gam[p] = gamma.view("<u8")
+        sL[p] = sLR[:, :32].copy().view("<u8").reshape(n, 4)
+        sR[p] = sLR[:, 32:].copy().view("<u8").reshape(n, 4)
+        rnd[p] = rnd4.view("<u8").reshape(4, 4)
+        rb.append((gamma, sLR, rnd4))
+    v = np.stack([np.asarray(x, np.uint8).view("<u8") for x in values]).astype(np.uint64)
+    return v, gam, sL, sR, rnd, rb
+
+
+def _run_prover(bp, n, v, gam, sL, sR, rnd, G, H, g, h):
+    import torch
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    out = bp.batch_generate_range_proof(n, T(v), T(gam), T(sL), T(sR), T(rnd), T(G), T(H), T(g), T(h))
+    torch.cuda.synchronize()
+    return {k: (t.cpu().numpy().view(np.uint64) if k != "valid" else t.cpu().numpy())
+            for k, t in out.items() if k != "_keep"}
+
+
+@pytest.mark.parametrize("n", [16, 64])
+def test_prover_matches_reference(bp, golden, n):
+    """The GPU prover reproduces the reference's own proofs byte for byte (same values, same RNG)."""
+    d = golden(f"proofs_n{n}")
+    B = len(d["head"])
+    v, gam, sL, sR, rnd, _ = _prove_inputs(list(range(1, B + 1)), d["value"], n)
+    o = _run_prover(bp, n, v, gam, sL, sR, rnd, d["G"], d["H"], d["g"], d["h"])
+    from oracle.pyoracle import head_fields
+    for p in range(B):
+        hf = head_fields(d["head"][p])
+        assert o["valid"][p] == 1
+        for k in ("V", "A", "S", "T1", "T2", "taux", "mu", "t", "c", "x"):
+            assert np.array_equal(o[k][p], hf[k]), (p, k)
+        assert np.array_equal(o["V"][p], d["V"][p])
+        assert np.array_equal(o["a"][p], d["a"][p]) and np.array_equal(o["b"][p], d["b"][p]), p
+        assert np.array_equal(o["L"][p], d["L"][p]) and np.array_equal(o["R"][p], d["R"][p]), p
+
+
+@pytest.mark.parametrize("n,B", [(1, 3), (2, 4), (8, 5), (32, 6), (128, 2)])
+def test_prover_vs_oracle(bp, oracle, n, B):
+    """Random values (some out of range: refused like the reference) vs the oracle's prover."""
+    rng = np.random.default_rng(n * 7 + B)
+    values = []
+    for p in range(B):
+        val = np.zeros(32, np.uint8)
+        nb = max(1, n // 8)
+        val[:nb] = rng.integers(0, 256, nb)
+        if n % 8:
+            val[0] &= (1 << n) - 1
+        if p == B - 1:
+            val[min(31, n // 8)] |= 1 << (n % 8)       # bit n set: refused (rp.cu:238)
+        values.append(val)
+    seeds = [1000 + 17 * p + n for p in range(B)]
+    v, gam, sL, sR, rnd, rb = _prove_inputs(seeds, values, n)
+    G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+    g, h = oracle.gh()
+    o = _run_prover(bp, n, v, gam, sL, sR, rnd, G, H, g, h)
+    for p in range(B):
+        gamma, sLR, rnd4 = rb[p]
+        pr = oracle.generate_range_proof(values[p], gamma, sLR, rnd4, n, G, H, g, h)
+        if pr is None:
+            assert o["valid"][p] == 0, p
+            continue
+        assert o["valid"][p] == 1, p
+        from oracle.pyoracle import head_fields
+        hf = head_fields(pr["head"])
+        for k in ("V", "A", "S", "T1", "T2", "taux", "mu", "t", "c", "x"):
+            assert np.array_equal(o[k][p], hf[k]), (p, k)
+        assert np.array_equal(o["a"][p], pr["a"]) and np.array_equal(o["b"][p], pr["b"]), p
+        assert np.array_equal(o["L"][p], pr["L"]) and np.array_equal(o["R"][p], pr["R"]), p
+
+
+def test_prove_then_verify_on_gpu(bp, oracle):
+    """Proofs made on the GPU verify on the GPU exactly as the reference's verifier judges them."""
+    import torch
+    n, B = 16, 12
+    rng = np.random.default_rng(3)
+    values = [np.concatenate([rng.integers(0, 256, 2).astype(np.uint8), np.zeros(30, np.uint8)]) for _ in range(B)]
+    v, gam, sL, sR, rnd, _ = _prove_inputs([50 + p for p in range(B)], values, n)
+    G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+    g, h = oracle.gh()
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    out = bp.batch_generate_range_proof(n, T(v), T(gam), T(sL), T(sR), T(rnd), T(G), T(H), T(g), T(h))
+    batch = bp.RangeProofBatch(n, **{k: out[k] for k in bp.RangeProofBatch.FIELDS + ("taux", "mu")})
+    ok = torch.zeros(B, dtype=torch.uint8, device=dev)
+    bp.batch_range_proof_verify(batch, T(G), T(H), T(g), T(h), ok)
+    torch.cuda.synchronize()
+    o = {k: t.cpu().numpy().view(np.uint64) for k, t in out.items() if k not in ("valid", "_keep")}
+    for p in range(B):
+        head = np.concatenate([o[k][p] for k in ("V", "A", "S", "T1", "T2", "taux", "mu", "t", "c", "x")])
+        okr, _, _, _, _ = oracle.cuda_range_proof_verify(head, o["V"][p], n, o["a"][p], o["b"][p], o["L"][p],
+                                                         o["R"][p], G, H, g, h)
+        assert bool(ok[p].item()) == okr, p
