@@ -15,7 +15,8 @@ Extra fields on the JSON line:
   cpu_baseline the CPU restatement (oracle/, test infrastructure) on a bounded sample, 1 thread;
   msm          2^20-point canonical-tree MSM points/s (BASELINE configs[2], per-point semantics);
                at N > 1 one MSM sharded over all ranks (cudabulletproof_amd/shard.py), strong scaling;
-  ipa          4096-element inner-product-argument verifies/s (BASELINE configs[3]), rank 0.
+  ipa          4096-element inner-product-argument verifies/s (BASELINE configs[3]), rank 0;
+  prove        generate_range_proof batched on the GPU, proofs/s, rank 0.
 """
 import argparse
 import json
@@ -48,6 +49,9 @@ def parse():
     ap.add_argument("--ipa-batch", type=int, default=64, help="IPA proofs per pipeline tick")
     ap.add_argument("--ipa-steps", type=int, default=4)
     ap.add_argument("--no-ipa", action="store_true")
+    ap.add_argument("--prove-batch", type=int, default=16384, help="proofs per generate_range_proof batch")
+    ap.add_argument("--prove-steps", type=int, default=4)
+    ap.add_argument("--no-prove", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-msm", action="store_true")
@@ -194,6 +198,37 @@ def ipa_leg(args, dev):
             "semantics": "cuda_inner_product_verify (crv:130), P given", "pipeline_depth": pipe.depth}
 
 
+def prove_leg(args, dev):
+    """§8(f) rank 1: generate_range_proof (rp.cu:1159) batched on the GPU, n = args.n, synthetic
+    values and random scalars; proofs/s over whole batches (inputs resident in HBM)."""
+    import torch
+    import cudabulletproof_amd as bp
+    from cudabulletproof_amd import synth
+    n, B = args.n, args.prove_batch
+    G, H, g, h = synth.generators(n, dev)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)
+    Gd, Hd, gd, hd = T(G), T(H), T(g), T(h)
+    pi = {k: T(v) for k, v in synth.prove_inputs(B, n).items()}
+    # two streams: one batch's latency-bound stages (T terms, IPA rounds, chains) run under the
+    # other batch's term launches (each stream has its own prover workspace in the engine)
+    streams = [torch.cuda.Stream(dev) for _ in range(2)]
+    torch.cuda.synchronize(dev)
+    run = lambda k: bp.batch_generate_range_proof(n, pi["v"], pi["gamma"], pi["sL"], pi["sR"], pi["rnd"], Gd, Hd,
+                                                  gd, hd, stream=streams[k % 2])
+    outs = [run(0), run(1)]
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.prove_steps):
+        outs[k % 2] = run(k)
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / args.prove_steps
+    same = all(torch.equal(outs[0][k], outs[1][k]) for k in ("A", "S", "T1", "L", "R"))
+    return {"metric": f"{n}-bit range proofs generated/sec", "value": B / dt, "unit": "proofs/s", "batch": B,
+            "streams": 2, "ms_per_batch": dt * 1e3, "valid": int(outs[0]["valid"].sum().item()),
+            "deterministic_across_streams": same,
+            "semantics": "generate_range_proof + inner_product_prove + fix_inner_product_proof (rp.cu:1159)"}
+
+
 def main():
     args = parse()
     import torch
@@ -308,6 +343,10 @@ def main():
     if not args.no_ipa and rank == 0:   # configs[3]: single-GPU
         ipa = ipa_leg(args, dev)
 
+    prove = None
+    if not args.no_prove and rank == 0:
+        prove = prove_leg(args, dev)
+
     cpu = None
     if not args.no_cpu and rank == 0 and world == 1:
         cpu = cpu_baseline(n, args.cpu_seconds)
@@ -324,7 +363,7 @@ def main():
                        "parallelism": f"independent proof shards x{world}", "mode": args.mode,
                        "pipeline_depth": pipe.depth if pipe else None,
                        "proof_bytes": proof_bytes(n, 1), "passes_in_warmup_batch": passes_warm},
-            "roofline": roofline, "valu_roofline": valu_roofline, "cpu_baseline": cpu, "msm": msm, "ipa": ipa,
+            "roofline": roofline, "valu_roofline": valu_roofline, "cpu_baseline": cpu, "msm": msm, "ipa": ipa, "prove": prove,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -364,14 +364,19 @@ def batch_generate_range_proof(n, v, gamma, sL, sR, rnd, G, H, g, h, stream=None
     u64 limbs (the random scalars exactly as generate_random_scalar produced them).  Returns a dict
     of CUDA tensors in RangeProofBatch layout (V, A, S, T1, T2, t, a, b, c, x, L, R, taux, mu) plus
     "valid" (B,) uint8; RangeProofBatch(n, **out) verifies it directly."""
+    import contextlib
+
     import torch
     B = int(v.shape[0])
     Lr = int(n).bit_length() - 1
     dev = v.device
-    z = lambda *shape: torch.zeros(*shape, dtype=torch.int64, device=dev)
-    out = dict(V=z(B, 16), A=z(B, 16), S=z(B, 16), T1=z(B, 16), T2=z(B, 16), taux=z(B, 4), mu=z(B, 4), t=z(B, 4),
-               c=z(B, 4), x=z(B, 4), a=z(B, 1, 4), b=z(B, 1, 4), L=z(B, max(Lr, 0), 16), R=z(B, max(Lr, 0), 16),
-               valid=torch.zeros(B, dtype=torch.uint8, device=dev))
+    # every output element is written by the prover (refused proofs get the reference's zeroed
+    # proof), so the buffers are allocated uninitialised on the stream the prover runs on
+    with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
+        z = lambda *shape: torch.empty(*shape, dtype=torch.int64, device=dev)
+        out = dict(V=z(B, 16), A=z(B, 16), S=z(B, 16), T1=z(B, 16), T2=z(B, 16), taux=z(B, 4), mu=z(B, 4),
+                   t=z(B, 4), c=z(B, 4), x=z(B, 4), a=z(B, 1, 4), b=z(B, 1, 4), L=z(B, max(Lr, 0), 16),
+                   R=z(B, max(Lr, 0), 16), valid=torch.empty(B, dtype=torch.uint8, device=dev))
     ins = [t.contiguous() for t in (v, gamma, sL, sR, rnd)]
     ic = ProveInputC(B, int(n), *[t.data_ptr() for t in ins])
     oc = ProofOutC(*[out[k].data_ptr() if out[k].numel() else None for k in

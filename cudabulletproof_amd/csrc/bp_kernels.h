@@ -137,6 +137,12 @@ struct ProveWs {
     ge* iterm;    // [B*(2n+2)] round terms + c_L Q, c_R Q
     fe* misc;     // [B*4]     taux, mu, x
     uint8_t* valid;   // [B]
+    // work lists of the term launches: item ids of the non-zero scalars, heavy (> 64 bits) at
+    // list[0..), light at list[cap..); cnt[0], cnt[1] their counts (zero scalars need no launch:
+    // their term is a constant, dtab[256] raw / dtab[257] normalized)
+    uint32_t* list;   // [2*cap], cap = B*(4n+4)
+    unsigned* cnt;    // [2]
+    size_t cap;
 };
 enum ProveStage { PS_PREP = 0, PS_TERMS0, PS_CHAIN0, PS_COMMIT, PS_TERMS1, PS_TX, PS_RTERMS, PS_RCHAIN, PS_ROUND,
                   PS_FINAL };

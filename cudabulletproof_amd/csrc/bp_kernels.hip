@@ -18,7 +18,8 @@ __device__ __forceinline__ size_t gid() { return (size_t)blockIdx.x * blockDim.x
 
 // ------------------------------------------------------------------ tables
 // dtab[k] = k successive ge25519_add(r, r) of the identity (0,1,1,0): the state of
-// ge25519_scalarmult after k leading zero bits (curve25519_ops.cu:399-414).
+// ge25519_scalarmult after k leading zero bits (curve25519_ops.cu:399-414); dtab[257] =
+// ge25519_normalize(dtab[256]), the normalized result of any point times the zero scalar.
 // two_i[i] = i successive fe25519_mul(., 2) from 1 (bulletproof_range_proof.cu:705-712).
 __global__ void k_init_tables(ge* dtab, fe* two_i, int nmax) {
     if (gid() != 0) return;
@@ -28,6 +29,7 @@ __global__ void k_init_tables(ge* dtab, fe* two_i, int nmax) {
         r = ge_dbl(r);
         dtab[k] = r;
     }
+    dtab[257] = ge_norm_host(r);   // a zero scalar's host-normalized term, whatever the point
     fe two = fe_add(fe_set(1), fe_set(1));
     fe t = fe_set(1);
     for (int i = 0; i < nmax; i++) {

@@ -51,8 +51,53 @@ __device__ __forceinline__ bool validate_range(const fe& vc, int n) {
 
 __device__ __forceinline__ fe bit_fe(const fe& vc, int i) { return fe_set((vc.v[i >> 6] >> (i & 63)) & 1); }
 
+// Work lists.  A zero scalar's term is a constant (ge25519_scalarmult leaves the identity
+// doubled 256 times whatever the point: dtab[256], normalized dtab[257]), so those items are
+// written directly; the rest are queued by cost class — light (<= 64 significant bits: the
+// aL bits, the value) and heavy — so that a wave does not run a 255-bit scalar-mult for one
+// lane while 63 others idle.  One lane per proof reserves its items with one atomic per class.
+__device__ __forceinline__ int sclass(const fe& s) {
+    if (s.v[3] | s.v[2] | s.v[1]) return 2;
+    return s.v[0] ? 1 : 0;
+}
+
+template <typename ScalarOf>
+__device__ __forceinline__ void queue_items(const ProveWs& ws, size_t p, int per, ScalarOf scalar_of) {
+    unsigned nh = 0, nl = 0;
+    for (int k = 0; k < per; k++) {
+        int c = sclass(scalar_of(k));
+        nh += c == 2;
+        nl += c == 1;
+    }
+    unsigned bh = nh ? atomicAdd(&ws.cnt[0], nh) : 0, bl = nl ? atomicAdd(&ws.cnt[1], nl) : 0;
+    for (int k = 0; k < per; k++) {
+        int c = sclass(scalar_of(k));
+        uint32_t id = (uint32_t)(p * per + k);
+        if (c == 2) ws.list[bh++] = id;
+        else if (c == 1) ws.list[ws.cap + bl++] = id;
+    }
+}
+
+// The i-th queued item of a list-driven launch (heavy first), or false past the end.
+__device__ __forceinline__ bool next_item(const ProveWs& ws, size_t i, uint32_t& id) {
+    const unsigned ch = ws.cnt[0], cl = ws.cnt[1];
+    if (i < ch) { id = ws.list[i]; return true; }
+    if (i < (size_t)ch + cl) { id = ws.list[ws.cap + (i - ch)]; return true; }
+    return false;
+}
+
+// terms0 item k's scalar (tobytes form, or the raw alpha / rho bytes)
+__device__ __forceinline__ fe terms0_scalar(const ProveIn& in, const ProveWs& ws, size_t p, int k) {
+    const int n = in.n;
+    if (k < 4 * n) return ws.ps[p * 4 * n + k];
+    k -= 4 * n;
+    if (k == 0) return fe_canon(in.v[p]);
+    if (k == 1) return fe_canon(in.gamma[p]);
+    return in.rnd[p * 4 + (k - 2)];
+}
+
 // ---------------------------------------------------------------- PS_PREP
-__global__ __launch_bounds__(TPB) void k_prove_prep(ProveIn in, ProveWs ws) {
+__global__ __launch_bounds__(TPB) void k_prove_prep(ProveIn in, ProveWs ws, const ge* __restrict__ dtab) {
     size_t p = gid();
     if (p >= (size_t)in.B) return;
     const int n = in.n;
@@ -67,6 +112,11 @@ __global__ __launch_bounds__(TPB) void k_prove_prep(ProveIn in, ProveWs ws) {
         ps[2 * n + i] = fe_canon(in.sL[p * n + i]);
         ps[3 * n + i] = fe_canon(in.sR[p * n + i]);
     }
+    const int per = 4 * n + 4;
+    ge* pt = ws.pterm + p * per;
+    for (int k = 0; k < per; k++)   // zero scalars: the constant term (raw for h^alpha, h^rho)
+        if (sclass(terms0_scalar(in, ws, p, k)) == 0) pt[k] = dtab[k < 4 * n + 2 ? 257 : 256];
+    queue_items(ws, p, per, [&](int k) { return terms0_scalar(in, ws, p, k); });
 }
 
 // ---------------------------------------------------------------- PS_TERMS0
@@ -79,25 +129,27 @@ __global__ __launch_bounds__(TPB, 3) void k_prove_terms0(ProveIn in, ProveWs ws,
     __shared__ geq qs[TPB];
     const int n = in.n;
     const size_t per = 4 * (size_t)n + 4;
-    size_t i = gid();
-    if (i >= (size_t)in.B * per) return;
-    size_t p = i / per;
-    int k = (int)(i % per);
-    ge* out = ws.pterm + i;
-    if (k < 4 * n) {
-        int blk = k / n, j = k % n;
-        ge P = (blk & 1) ? H[j] : G[j];
-        *out = sm_norm(ws.ps[p * 4 * n + k], P, &qs[threadIdx.x], dtab);
-        return;
-    }
-    k -= 4 * n;
+    uint32_t id;
+    if (!next_item(ws, gid(), id)) return;
+    size_t p = id / per;
+    int k = (int)(id % per);
+    // operands are selected per lane and ONE scalar-mult follows: two call sites in one wave
+    // would run both loops back to back (divergence), ~1.6x the instructions
     fe s;
     ge P;
-    if (k == 0) { s = fe_canon(in.v[p]); P = *g; }
-    else if (k == 1) { s = fe_canon(in.gamma[p]); P = *h; }
-    else { s = in.rnd[p * 4 + (k - 2)]; P = *h; }   // alpha_bytes / rho_bytes used raw
+    bool norm = true;
+    if (k < 4 * n) {
+        int blk = k / n, j = k % n;
+        P = (blk & 1) ? H[j] : G[j];
+        s = ws.ps[p * 4 * n + k];
+    } else {
+        k -= 4 * n;
+        P = k == 0 ? *g : *h;
+        s = terms0_scalar(in, ws, p, 4 * n + k);
+        norm = k < 2;                               // alpha_bytes / rho_bytes: raw, not normalized
+    }
     ge r = scalarmult<true>(s, P, &qs[threadIdx.x], dtab);
-    *out = (k < 2) ? ge_norm_host(r) : r;
+    ws.pterm[id] = norm ? ge_norm_host(r) : r;
 }
 
 // ---------------------------------------------------------------- chains
@@ -182,11 +234,12 @@ __global__ __launch_bounds__(TPB, 3) void k_prove_terms1(ProveIn in, ProveWs ws,
 
 // round-r scalars (inner_product_prove, vectors.cu:345-376): c_L = <a_L, b_R>, c_R = <a_R, b_L> and the
 // four MSMs' scalars in tobytes form: a_L | b_R | a_R | b_L.
-__device__ __forceinline__ void round_prep(const ProveWs& ws, size_t p, int n, int np) {
+__device__ __forceinline__ void round_prep(const ProveWs& ws, size_t p, int n, int np, const ge* __restrict__ dtab) {
     const fe* a = ws.acur + p * n;
     const fe* b = ws.bcur + p * n;
-    ws.csc[p * 2 + 0] = fe_canon(ip_seq(a, b + np, np));
-    ws.csc[p * 2 + 1] = fe_canon(ip_seq(a + np, b, np));
+    fe* cs = ws.csc + p * 2;
+    cs[0] = fe_canon(ip_seq(a, b + np, np));
+    cs[1] = fe_canon(ip_seq(a + np, b, np));
     fe* sc = ws.iscal + p * 2 * n;
     for (int j = 0; j < np; j++) {
         sc[j] = fe_canon(a[j]);
@@ -194,10 +247,17 @@ __device__ __forceinline__ void round_prep(const ProveWs& ws, size_t p, int n, i
         sc[2 * np + j] = fe_canon(a[np + j]);
         sc[3 * np + j] = fe_canon(b[j]);
     }
+    const int per = 4 * np + 2;
+    auto scalar_of = [&](int k) { return k < 4 * np ? sc[k] : cs[k - 4 * np]; };
+    ge* it = ws.iterm + p * (2 * (size_t)n + 2);
+    for (int k = 0; k < per; k++)   // zero scalars: the constant term (raw for c_L Q, c_R Q)
+        if (sclass(scalar_of(k)) == 0) it[k] = dtab[k < 4 * np ? 257 : 256];
+    queue_items(ws, p, per, scalar_of);
 }
 
 // ---------------------------------------------------------------- PS_TX
-__global__ __launch_bounds__(TPB) void k_prove_tx(ProveIn in, ProveWs ws, const fe* __restrict__ two_i) {
+__global__ __launch_bounds__(TPB) void k_prove_tx(ProveIn in, ProveWs ws, const fe* __restrict__ two_i,
+                                                  const ge* __restrict__ dtab) {
     size_t p = gid();
     if (p >= (size_t)in.B) return;
     const int n = in.n;
@@ -254,7 +314,7 @@ __global__ __launch_bounds__(TPB) void k_prove_tx(ProveIn in, ProveWs ws, const 
     m[0] = taux;
     m[1] = mu;
     m[2] = fe_set(0);                                               // x (ip_proof.x) until round 0
-    if (in.L > 0) round_prep(ws, p, n, n >> 1);
+    if (in.L > 0) round_prep(ws, p, n, n >> 1, dtab);
 }
 
 // ---------------------------------------------------------------- IPA round r
@@ -267,21 +327,27 @@ __global__ __launch_bounds__(TPB, 3) void k_prove_rterms(ProveIn in, ProveWs ws,
     __shared__ geq qs[TPB];
     const int n = in.n;
     const size_t per = 4 * (size_t)np + 2;
-    size_t i = gid();
-    if (i >= (size_t)in.B * per) return;
-    size_t p = i / per;
-    int k = (int)(i % per);
-    ge* out = ws.iterm + p * (2 * (size_t)n + 2) + k;
-    if (k < 4 * np) {
+    uint32_t id;
+    if (!next_item(ws, gid(), id)) return;
+    size_t p = id / per;
+    int k = (int)(id % per);
+    fe s;
+    ge P;
+    const bool msm = k < 4 * np;
+    if (msm) {
         int blk = k / np, j = k % np;
-        ge P = blk == 0 ? G[np + j] : blk == 1 ? H[j] : blk == 2 ? G[j] : H[np + j];
-        *out = sm_norm(ws.iscal[p * 2 * n + k], P, &qs[threadIdx.x], dtab);
-        return;
+        P = blk == 0 ? G[np + j] : blk == 1 ? H[j] : blk == 2 ? G[j] : H[np + j];
+        s = ws.iscal[p * 2 * n + k];
+    } else {
+        P = *Q;
+        s = ws.csc[p * 2 + (k - 4 * np)];
     }
-    *out = scalarmult<true>(ws.csc[p * 2 + (k - 4 * np)], *Q, &qs[threadIdx.x], dtab);
+    ge r = scalarmult<true>(s, P, &qs[threadIdx.x], dtab);   // one call site (see k_prove_terms0)
+    ws.iterm[p * (2 * (size_t)n + 2) + k] = msm ? ge_norm_host(r) : r;
 }
 
-__global__ __launch_bounds__(TPB) void k_prove_round(ProveIn in, ProveWs ws, ProveOut out, int r) {
+__global__ __launch_bounds__(TPB) void k_prove_round(ProveIn in, ProveWs ws, ProveOut out, int r,
+                                                     const ge* __restrict__ dtab) {
     size_t p = gid();
     if (p >= (size_t)in.B) return;
     const int n = in.n, np = n >> (r + 1);
@@ -310,7 +376,7 @@ __global__ __launch_bounds__(TPB) void k_prove_round(ProveIn in, ProveWs ws, Pro
         a[j] = na;
         b[j] = nb;
     }
-    if (r + 1 < in.L) round_prep(ws, p, n, np >> 1);
+    if (r + 1 < in.L) round_prep(ws, p, n, np >> 1, dtab);
 }
 
 // ---------------------------------------------------------------- PS_FINAL (+ fix_inner_product_proof)
@@ -351,14 +417,20 @@ void launch_prove(int stage, int r, const ProveIn& in, const ProveWs& ws, const 
     const size_t B = in.B;
     const int n = in.n;
     switch (stage) {
-        case PS_PREP: k_prove_prep<<<nblk(B), TPB, 0, s>>>(in, ws); break;
+        case PS_PREP:
+            (void)hipMemsetAsync(ws.cnt, 0, 2 * sizeof(unsigned), s);
+            k_prove_prep<<<nblk(B), TPB, 0, s>>>(in, ws, dtab);
+            break;
         case PS_TERMS0: k_prove_terms0<<<nblk(B * (4 * (size_t)n + 4)), TPB, 0, s>>>(in, ws, G, H, g, h, dtab); break;
         case PS_CHAIN0:
             k_prove_chain<<<nblk(B * 4), TPB, 0, s>>>(ws.pterm, 4 * (size_t)n + 4, n, n, 4, ws.chain, in.B);
             break;
         case PS_COMMIT: k_prove_commit<<<nblk(B), TPB, 0, s>>>(in, ws, two_i); break;
         case PS_TERMS1: k_prove_terms1<<<nblk(B * 4), TPB, 0, s>>>(in, ws, g, h, dtab); break;
-        case PS_TX: k_prove_tx<<<nblk(B), TPB, 0, s>>>(in, ws, two_i); break;
+        case PS_TX:
+            (void)hipMemsetAsync(ws.cnt, 0, 2 * sizeof(unsigned), s);
+            k_prove_tx<<<nblk(B), TPB, 0, s>>>(in, ws, two_i, dtab);
+            break;
         case PS_RTERMS: {
             int np = n >> (r + 1);
             k_prove_rterms<<<nblk(B * (4 * (size_t)np + 2)), TPB, 0, s>>>(in, ws, np, G, H, h, dtab);
@@ -369,7 +441,10 @@ void launch_prove(int stage, int r, const ProveIn& in, const ProveWs& ws, const 
             k_prove_chain<<<nblk(B * 4), TPB, 0, s>>>(ws.iterm, 2 * (size_t)n + 2, np, np, 4, ws.chain, in.B);
             break;
         }
-        case PS_ROUND: k_prove_round<<<nblk(B), TPB, 0, s>>>(in, ws, out, r); break;
+        case PS_ROUND:
+            (void)hipMemsetAsync(ws.cnt, 0, 2 * sizeof(unsigned), s);
+            k_prove_round<<<nblk(B), TPB, 0, s>>>(in, ws, out, r, dtab);
+            break;
         case PS_FINAL: k_prove_final<<<nblk(B), TPB, 0, s>>>(in, ws, out); break;
     }
 }

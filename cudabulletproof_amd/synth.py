@@ -103,3 +103,26 @@ def msm_inputs(n, seed=5):
     """MSM microbench inputs: points = random (X, Y, Z=1, T), scalars = 255-bit."""
     rng = np.random.default_rng(seed)
     return _rand_fe(rng, (n,)), _rand_pt(rng, (n,))
+
+
+def _rand_scalar(rng, shape):
+    """Random scalars as generate_random_scalar (rp.cu:153-159) shapes them: byte 0 &= 0xF8,
+    byte 31 &= 0x7F then |= 0x40 — as LE u64 limbs."""
+    v = rng.integers(0, 2**64, size=shape + (4,), dtype=np.uint64)
+    v[..., 0] &= np.uint64(0xFFFFFFFFFFFFFFF8)
+    v[..., 3] = (v[..., 3] & np.uint64(0x7FFFFFFFFFFFFFFF)) | np.uint64(0x4000000000000000)
+    return v
+
+
+def prove_inputs(count, n, seed=11):
+    """Prover inputs (hipbp_prove_input layout): values uniform in [0, 2^n), random scalars."""
+    rng = np.random.default_rng(seed)
+    v = np.zeros((count, 4), np.uint64)
+    if n >= 64:
+        v[:, 0] = rng.integers(0, 2**64, size=count, dtype=np.uint64)
+        for k in range(1, n // 64):
+            v[:, k] = rng.integers(0, 2**64, size=count, dtype=np.uint64)
+    else:
+        v[:, 0] = rng.integers(0, 2**n, size=count, dtype=np.uint64)
+    return dict(v=v, gamma=_rand_scalar(rng, (count,)), sL=_rand_scalar(rng, (count, n)),
+                sR=_rand_scalar(rng, (count, n)), rnd=_rand_scalar(rng, (count, 4)))
