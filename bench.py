@@ -19,6 +19,7 @@ Extra fields on the JSON line:
   prove        generate_range_proof batched on the GPU, proofs/s, rank 0.
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -55,6 +56,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-msm", action="store_true")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="exercise the N>1 path on one GPU (all ranks on cuda:0, gloo collectives); not a measurement")
     return ap.parse_args()
 
 
@@ -161,7 +164,7 @@ def msm_leg(args, dev, world, rank, T):
     return {"metric": "MSM points/sec", "value": nm / mdt, "unit": "points/s", "points": nm,
             "ms_per_msm": mdt * 1e3, "n_gpus": world, "scaling": "strong" if world > 1 else None,
             "semantics": "canonical-tree per-point double-and-add (SURVEY A9); shards + all_gather + tree at N>1",
-            "result_digest": hex(int(res[0].item()) & 0xFFFFFFFF)}
+            "result_sha256": hashlib.sha256(res.cpu().numpy().tobytes()).hexdigest()[:16]}
 
 
 def ipa_leg(args, dev):
@@ -240,9 +243,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.rehearse:   # N>1 code path on a 1-GPU box: every rank on cuda:0, gloo instead of RCCL
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     bp.lib()

@@ -1,0 +1,35 @@
+"""bench.py's N>1 path (torchrun, one process per rank) rehearsed on one GPU: every rank on cuda:0
+with gloo collectives (--rehearse).  The sharded MSM (shard roots + all_gather + canonical tree)
+must give the same point as the single-rank run, and the line must carry the N=2 fields."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SMALL = ["--steps", "2", "--warmup", "1", "--batch", "128", "--msm-log2", "12", "--no-cpu", "--no-ipa",
+         "--no-prove"]
+
+
+def _line(out):
+    return json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_rehearsal_matches_one_rank():
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    one = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + SMALL, capture_output=True, text=True,
+                         timeout=600, cwd=ROOT, env=env)
+    assert one.returncode == 0, one.stderr[-2000:]
+    two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", "29561", os.path.join(ROOT, "bench.py"),
+                          "--gpus", "2", "--rehearse"] + SMALL, capture_output=True, text=True, timeout=600, cwd=ROOT,
+                         env=env)
+    assert two.returncode == 0, two.stderr[-2000:]
+    l1, l2 = _line(one.stdout), _line(two.stdout)
+    assert l1["n_gpus"] == 1 and l2["n_gpus"] == 2
+    assert l2["msm"]["scaling"] == "strong" and l2["scaling"] == "weak"
+    assert l1["msm"]["result_sha256"] == l2["msm"]["result_sha256"]
+    assert l2["config"]["passes_in_warmup_batch"] >= l1["config"]["passes_in_warmup_batch"]
