@@ -55,6 +55,7 @@ def parse():
     ap.add_argument("--no-prove", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-procs", type=int, default=16, help="processes for the parallel CPU baseline")
     ap.add_argument("--no-msm", action="store_true")
     ap.add_argument("--rehearse", action="store_true",
                     help="exercise the N>1 path on one GPU (all ranks on cuda:0, gloo collectives); not a measurement")
@@ -81,27 +82,68 @@ def proof_bytes(n, ab_len):
     return 5 * GE_B + 3 * FE_B + 2 * ab_len * FE_B + 2 * Lr * GE_B   # V,A,S,T1,T2, t,c,x, a,b, L,R
 
 
-def cpu_baseline(n, seconds):
-    """The CPU restatement (oracle/, test infrastructure) verifying synthetic proofs, 1 thread."""
+def _cpu_sample(n, count):
     from cudabulletproof_amd import synth
+    s = synth.proofs(count, n, seed=777)
+    heads = [np.concatenate([s[k][p] for k in ("V", "A", "S", "T1", "T2")] +
+                            [np.zeros(8, np.uint64), s["t"][p], s["c"][p], s["x"][p]]) for p in range(count)]
+    return s, heads
+
+
+def _cpu_worker(args):
+    """One process of the parallel CPU baseline: verify proofs [lo, hi) with the reference build."""
+    n, lo, hi, seconds = args
     from oracle import pyoracle
-    O = pyoracle.Oracle()
-    G, H = O.base_points(n, 1), O.base_points(n, 2)
-    g, h = O.gh()
-    s = synth.proofs(64, n, seed=777)
+    R = pyoracle.Reference()
+    G, H = R.base_points(n, 1), R.base_points(n, 2)
+    g, h = R.gh()
+    s, heads = _cpu_sample(n, hi)
     done, t0 = 0, time.perf_counter()
-    while done < 64:
-        p = done
-        head = np.concatenate([s[k][p] for k in ("V", "A", "S", "T1", "T2")] +
-                              [np.zeros(8, np.uint64), s["t"][p], s["c"][p], s["x"][p]])
-        O.cuda_range_proof_verify(head, s["V"][p], n, s["a"][p], s["b"][p], s["L"][p], s["R"][p], G, H, g, h)
+    for p in range(lo, hi):
+        R.cuda_range_proof_verify(dict(head=heads[p], V=s["V"][p], a=s["a"][p], b=s["b"][p], L=s["L"][p],
+                                       R=s["R"][p]), n, G, H, g, h)
         done += 1
         if time.perf_counter() - t0 > seconds:
             break
-    dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "verifies/s", "cores": 1, "kind": "port",
-            "sample": f"{done} synthetic {n}-bit proofs, cuda_range_proof_verify semantics, oracle/bp_oracle.c, "
-                      f"1 thread, {dt:.1f} s", "cpu": cpu_model()}
+    return done, time.perf_counter() - t0
+
+
+def cpu_baseline(n, seconds, procs):
+    """The reference's own cuda_range_proof_verify (its host sources compiled by oracle/build_ref.sh
+    into oracle/_ref/libbpref.so, the two MSMs host-emulated with the canonical tree) on this host:
+    1 thread on a bounded sample (`value`), and `procs` processes side by side (`parallel`).
+    Falls back to the CPU restatement (oracle/bp_oracle.c, kind "port") if the build is absent."""
+    from oracle import pyoracle
+    if not pyoracle.have_reference():
+        O = pyoracle.Oracle()
+        G, H = O.base_points(n, 1), O.base_points(n, 2)
+        g, h = O.gh()
+        s, heads = _cpu_sample(n, 64)
+        done, t0 = 0, time.perf_counter()
+        for p in range(64):
+            O.cuda_range_proof_verify(heads[p], s["V"][p], n, s["a"][p], s["b"][p], s["L"][p], s["R"][p], G, H, g, h)
+            done += 1
+            if time.perf_counter() - t0 > seconds:
+                break
+        dt = time.perf_counter() - t0
+        return {"value": done / dt, "unit": "verifies/s", "cores": 1, "kind": "port",
+                "sample": f"{done} synthetic {n}-bit proofs, oracle/bp_oracle.c, 1 thread, {dt:.1f} s",
+                "cpu": cpu_model()}
+    done, dt = _cpu_worker((n, 0, 512, seconds))
+    out = {"value": done / dt, "unit": "verifies/s", "cores": 1, "kind": "reference",
+           "sample": f"{done} synthetic {n}-bit proofs, the reference's cuda_range_proof_verify (oracle/_ref), "
+                     f"1 thread, {dt:.1f} s", "cpu": cpu_model()}
+    if procs > 1:
+        import multiprocessing as mp
+        per = 16
+        with mp.get_context("spawn").Pool(procs) as pool:
+            t0 = time.perf_counter()
+            res = pool.map(_cpu_worker, [(n, k * per, (k + 1) * per, seconds) for k in range(procs)])
+            wall = time.perf_counter() - t0
+        tot = sum(r[0] for r in res)
+        out["parallel"] = {"value": sum(r[0] / r[1] for r in res), "unit": "verifies/s", "cores": procs,
+                           "sample": f"{tot} proofs over {procs} processes ({per} each), {wall:.1f} s wall"}
+    return out
 
 
 def cpu_model():
@@ -243,6 +285,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # CPU baseline first, before this process touches the GPU: its worker processes are started
+    # from a process with no HIP state (no fork/exec of a GPU-initialised process)
+    cpu = None
+    if not args.no_cpu and rank == 0 and world == 1:
+        cpu = cpu_baseline(args.n, args.cpu_seconds, args.cpu_procs)
     if args.rehearse:   # N>1 code path on a 1-GPU box: every rank on cuda:0, gloo instead of RCCL
         local = 0
     if world > 1:
@@ -355,9 +402,6 @@ def main():
     if not args.no_prove and rank == 0:
         prove = prove_leg(args, dev)
 
-    cpu = None
-    if not args.no_cpu and rank == 0 and world == 1:
-        cpu = cpu_baseline(n, args.cpu_seconds)
 
     if rank == 0:
         line = {
