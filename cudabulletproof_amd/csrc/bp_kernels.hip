@@ -552,13 +552,19 @@ __global__ __launch_bounds__(TPB) void k_field_op(int op, fe* r, const fe* __res
     size_t i = gid();
     if (i >= count) return;
     fe x = a[i], y;
-    if (op != 3) y = b[i];
+    if (op != 3 && op != 7) y = b[i];   // unary ops take no b
     fe z;
     switch (op) {
         case 0: z = fe_add(x, y); break;
         case 1: z = fe_sub(x, y); break;
         case 2: z = fe_mul(x, y); break;
         case 3: z = fe_square_kernel_quirk(x); break;
+        case 6: {   // the product fold alone on t = a || b (fe25519_mul's reduction, for its KATs)
+            uint64_t t[8] = {x.v[0], x.v[1], x.v[2], x.v[3], y.v[0], y.v[1], y.v[2], y.v[3]};
+            z = fe_fold512(t);
+            break;
+        }
+        case 7: z = fe_sq(x); break;   // fe25519_sq (dedicated squaring; == mul(x, x))
         default:
 #pragma unroll
             for (int k = 0; k < 4; k++) z.v[k] = x.v[k] + y.v[k];

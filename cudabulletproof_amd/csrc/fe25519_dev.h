@@ -16,6 +16,10 @@
 #define BP_MUL_ASM 1
 #endif
 #include "mul512_asm.h"
+#ifndef BP_FIELD_ASM
+#define BP_FIELD_ASM 1
+#endif
+#include "field_asm.h"
 
 namespace bp {
 
@@ -109,6 +113,16 @@ BP_DEV uint64_t cat64(uint32_t lo, uint32_t hi) { return (uint64_t)lo | ((uint64
 // fe25519_add (curve25519_ops.cu:41-68): exact 257-bit sum (one 32-bit carry chain), then
 // one lossy "- p" when the sum carried out or is >= p.
 BP_DEV fe fe_add(const fe& f, const fe& g) {
+#if BP_FIELD_ASM && defined(__HIP_DEVICE_COMPILE__)   // generated gfx950 form (field_asm.h), same bits
+    uint32_t a[8], b[8], o[8];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        a[2 * i] = lo32(f.v[i]); a[2 * i + 1] = hi32(f.v[i]);
+        b[2 * i] = lo32(g.v[i]); b[2 * i + 1] = hi32(g.v[i]);
+    }
+    fe_add_asm(o, a, b);
+    return fe{{cat64(o[0], o[1]), cat64(o[2], o[3]), cat64(o[4], o[5]), cat64(o[6], o[7])}};
+#else
     fe h;
     unsigned c = 0;
 #pragma unroll
@@ -118,6 +132,7 @@ BP_DEV fe fe_add(const fe& f, const fe& g) {
         h.v[i] = cat64(l, u);
     }
     return fe_fix(h, c != 0);
+#endif
 }
 
 // fe25519_sub (curve25519_ops.cu:71-90): t_i = f_i - g_i - br;  br = f_i < lo64(g_i + br).
@@ -126,6 +141,16 @@ BP_DEV fe fe_add(const fe& f, const fe& g) {
 //   a0 = t0 + p0, cy = a0 < p0 (= t0 >= 19);  a_i = t_i + lo64(p_i + cy), cy = a_i < p_i
 // i.e. a_i = cy ? t_i : t_i - 1 and cy = a_i != 2^64-1 for i = 1, 2;  a3 = t3 + p3 + cy.
 BP_DEV fe fe_sub(const fe& f, const fe& g) {
+#if BP_FIELD_ASM && defined(__HIP_DEVICE_COMPILE__)   // generated gfx950 form (field_asm.h), same bits
+    uint32_t a[8], b[8], o[8];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        a[2 * i] = lo32(f.v[i]); a[2 * i + 1] = hi32(f.v[i]);
+        b[2 * i] = lo32(g.v[i]); b[2 * i + 1] = hi32(g.v[i]);
+    }
+    fe_sub_asm(o, a, b);
+    return fe{{cat64(o[0], o[1]), cat64(o[2], o[3]), cat64(o[4], o[5]), cat64(o[6], o[7])}};
+#else
     fe t;
     unsigned br = 0;
 #pragma unroll
@@ -146,6 +171,7 @@ BP_DEV fe fe_sub(const fe& f, const fe& g) {
     bool cy2 = o.v[2] != M64;
     o.v[3] = t.v[3] + (m ? (cy2 ? 0x8000000000000000ull : P3) : 0ull);
     return o;
+#endif
 }
 
 // Fold of the exact 512-bit product (curve25519_ops.cu:114-145):
@@ -155,6 +181,17 @@ BP_DEV fe fe_sub(const fe& f, const fe& g) {
 // Computed as one carry chain t_i + x_i + cy (x_i = lo64(19 t_{i+4})): the same sum; the
 // carry differs only when x_i = 2^64-1 and cy = 1 (c wraps to 0, the reference carries 0).
 BP_DEV fe fe_fold512(const uint64_t t[8]) {
+#if BP_FIELD_ASM && defined(__HIP_DEVICE_COMPILE__)   // generated gfx950 form (field_asm.h), same bits
+    uint32_t a[8], xh[8], o[8];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        uint64_t x = mul19(t[i + 4]);
+        a[2 * i] = lo32(t[i]); a[2 * i + 1] = hi32(t[i]);
+        xh[2 * i] = lo32(x); xh[2 * i + 1] = hi32(x);
+    }
+    fe_fold_asm(o, a, xh);
+    return fe{{cat64(o[0], o[1]), cat64(o[2], o[3]), cat64(o[4], o[5]), cat64(o[6], o[7])}};
+#else
     fe h;
     unsigned cy = 0;
 #pragma unroll
@@ -167,6 +204,7 @@ BP_DEV fe fe_fold512(const uint64_t t[8]) {
         cy = c & !((x == M64) & (cy != 0));
     }
     return fe_fix(h, cy != 0);
+#endif
 }
 
 // Exact 256x256 -> 512-bit product, product scanning over 32-bit words with a

@@ -201,7 +201,8 @@ int hipbp_msm(ge25519* result, const fe25519* scalars, const ge25519* points, si
  * terms; a multi-GPU MSM combines per-rank shard roots with it. */
 int hipbp_point_tree(ge25519* result, const ge25519* points, size_t n, void* stream);
 /* Elementwise device field ops: op 0 add, 1 sub, 2 mul, 3 square (reference kernel quirk),
- * 4 SoA add (limbwise, no carry), 5 invert (host chain). */
+ * 4 SoA add (limbwise, no carry), 5 invert (host chain), 6 the product fold alone on the
+ * 512-bit t = a || b (fe25519_mul's reduction, curve25519_ops.cu:114-145), 7 fe25519_sq. */
 int hipbp_field_op(int op, fe25519* r, const fe25519* a, const fe25519* b, size_t count, void* stream);
 /* Wait for `stream`. */
 int hipbp_sync(void* stream);

@@ -502,3 +502,80 @@ def test_prove_then_verify_on_gpu(bp, oracle):
         okr, _, _, _, _ = oracle.cuda_range_proof_verify(head, o["V"][p], n, o["a"][p], o["b"][p], o["L"][p],
                                                          o["R"][p], G, H, g, h)
         assert bool(ok[p].item()) == okr, p
+
+
+# ----------------------------------------------------------------------------- field arithmetic corners
+M64 = (1 << 64) - 1
+P_LIMBS = [0xFFFFFFFFFFFFFFED, M64, M64, 0x7FFFFFFFFFFFFFFF]
+WRAP19 = 0x79435E50D79435E5                      # 19 * WRAP19 = 2^64 - 1 (mod 2^64)
+
+
+def _lossy_sub_p(h):
+    """curve25519_ops.cu:62-66 / :137-141: d_i = h_i - p_i - br; br = h_i < lo64(p_i + br)."""
+    out, br = [], 0
+    for i in range(4):
+        out.append((h[i] - P_LIMBS[i] - br) & M64)
+        br = int(h[i] < ((P_LIMBS[i] + br) & M64))
+    return out
+
+
+def _ge_p(h):
+    for i in (3, 2, 1, 0):
+        if h[i] != P_LIMBS[i]:
+            return h[i] > P_LIMBS[i]
+    return True
+
+
+def _ref_fold(t):
+    """curve25519_ops.cu:114-145 restated on Python ints (the reference's exact carry rules)."""
+    h, cy = list(t[:4]), 0
+    for i in range(4):
+        c = (t[i + 4] * 19 + cy) & M64
+        h[i] = (h[i] + c) & M64
+        cy = int(h[i] < c)
+    return _lossy_sub_p(h) if (cy or _ge_p(h)) else h
+
+
+def test_fold_corners_vs_reference_rule(bp):
+    """The product fold (device asm form) on crafted 512-bit inputs: 19 t_{i+4} = 2^64-1 with and without a
+    carry in (the reference drops that carry), sums at and around p, carries out of the top limb."""
+    import torch
+    rng = np.random.default_rng(19)
+    cands = [0, 1, 2, 18, 19, 20, M64, M64 - 1, WRAP19, WRAP19 - 1, WRAP19 + 1, P_LIMBS[0], P_LIMBS[0] - 1,
+             P_LIMBS[3], 1 << 63, (1 << 63) - 1, 0xFFFFFFFF, 1 << 32]
+    ts = []
+    for k in range(4000):
+        if k % 4 == 0:
+            t = [int(x) for x in rng.integers(0, 2**63, 8, dtype=np.uint64) * 2 + rng.integers(0, 2, 8, dtype=np.uint64)]
+        else:
+            t = [cands[int(rng.integers(0, len(cands)))] if rng.random() < 0.7 else
+                 int(rng.integers(0, 2**63, dtype=np.uint64)) * 2 for _ in range(8)]
+        ts.append(t)
+    ts.append([M64, M64, M64, M64, WRAP19, WRAP19, WRAP19, WRAP19])
+    ts.append([M64 - 18, M64, M64, P_LIMBS[3], 0, 0, 0, 0])
+    arr = np.array(ts, dtype=np.uint64)
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)
+    r = torch.empty(len(ts), 4, dtype=torch.int64, device=dev)
+    bp.field_op("fold", r, T(arr[:, :4]), T(arr[:, 4:]))
+    torch.cuda.synchronize()
+    got = r.cpu().numpy().view(np.uint64)
+    for i, t in enumerate(ts):
+        assert [int(x) for x in got[i]] == _ref_fold(t), (i, [hex(x) for x in t])
+
+
+def test_sq_matches_mul(bp, oracle):
+    """Dedicated squaring (36 products) == fe25519_mul(x, x) on edge-heavy limbs."""
+    import torch
+    rng = np.random.default_rng(7)
+    x = rng.integers(0, 2**64, size=(3000, 4), dtype=np.uint64)
+    x[::3] = np.array([M64, M64, M64, M64], np.uint64)
+    x[1::7, 1:3] = np.uint64(M64)
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)
+    r = torch.empty(len(x), 4, dtype=torch.int64, device=dev)
+    bp.field_op("sq", r, T(x))
+    torch.cuda.synchronize()
+    got = r.cpu().numpy().view(np.uint64)
+    for i in range(0, len(x), 13):
+        assert np.array_equal(got[i], oracle.fe_mul(x[i], x[i])), i

@@ -1,0 +1,214 @@
+"""Generate cudabulletproof_amd/csrc/field_asm.h: gfx950 inline-asm forms of the reference's
+lossy field add / product fold (curve25519_ops.cu:41-146), SAME bits as the C forms in
+fe25519_dev.h (which stay the host-pass / reference formulation).
+
+Why asm: the fix-up "(carry || h >= p) ? lossy - p : h" is a data-dependent select.  Written in
+C the compiler materialises each mask with v_cmp + v_cndmask (4.5-4.6 cycles per wave
+instruction, tools/ubench_enc.hip) and adds through 64-bit v_lshl_add_u64 (4.7); here the masks
+stay in SGPRs, are combined by SALU (its own issue port) and enter the arithmetic as the carry-ins
+of v_addc.  Every operand is a 32-bit VGPR: the C side passes limb halves (free sub-registers),
+so no register pair has to be formed.
+
+Hazard rule these sequences meet (gfx940/gfx950): an SGPR written by a VALU instruction
+(carry-out, v_cmp) and read by a VALU instruction (carry-in, mask) needs 2 wait states in
+between; SALU-written masks can be read at once.  `schedule` inserts the s_nop.  Outputs are
+VGPRs only, inputs are VGPRs or constants, so nothing crosses the asm boundary in an SGPR.
+"""
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+OUT = os.path.join(HERE, "..", "cudabulletproof_amd", "csrc", "field_asm.h")
+
+
+def schedule(ins):
+    """ins: (text, sgpr_writes, sgpr_reads, is_valu).  Returns the lines with s_nop inserted."""
+    lines, pos, wpos = [], 0, {}
+    for text, writes, reads, is_valu in ins:
+        if is_valu:
+            need = 0
+            for r in reads:
+                if r in wpos:
+                    need = max(need, 2 - (pos - wpos[r] - 1))
+            if need > 0:
+                lines.append(f"s_nop {need - 1}")
+                pos += need
+        lines.append(text)
+        for w in writes:
+            if is_valu:
+                wpos[w] = pos
+            else:
+                wpos.pop(w, None)
+        pos += 1
+    return lines
+
+
+def V(t, w=(), r=()):
+    return (t, list(w), list(r), True)
+
+
+def S(t, w=()):
+    return (t, list(w), [], False)
+
+
+def fix_seq(h, o, carry):
+    """(carry || h >= p) ? lossy "- p" : h (curve25519_ops.cu:54-66), halves h[0..7] -> o[0..7].
+    m = carry | top | (h3 == P3 & h2 == M & h1 == M & h0 >= P0);
+    out_i = h_i + m * (19, !br1, !br2, 2^63 + !br3)_i, no carries between limbs, with
+    br1 = h0 < P0, br2 = !br1 & h1 != M, br3 = !br2 & h2 != M (fe25519_dev.h fe_fix)."""
+    q = [V(f"v_and_b32 %[vt1], %[{h[2]}], %[{h[3]}]"),
+         V(f"v_and_b32 %[vt2], %[{h[4]}], %[{h[5]}]"),
+         V(f"v_or_b32 %[vt3], %[c80], %[{h[7]}]"),
+         V("v_cmp_eq_u32 %[sf1], -1, %[vt1]", ["sf1"]),                   # h1 == M
+         V("v_cmp_eq_u32 %[sf2], -1, %[vt2]", ["sf2"]),                   # h2 == M
+         V(f"v_and_b32 %[vt3], %[vt3], %[{h[6]}]"),
+         V("v_cmp_eq_u32 %[se3], -1, %[vt3]", ["se3"]),                   # h3 == P3 (or M: top set too)
+         V(f"v_cmp_gt_i32 %[stp], 0, %[{h[7]}]", ["stp"]),                # bit 255
+         V(f"v_cmp_eq_u32 %[sg0], -1, %[{h[1]}]", ["sg0"]),
+         V(f"v_cmp_le_u32 %[sg1], %[p0l], %[{h[0]}]", ["sg1"]),
+         S("s_and_b64 %[sg0], %[sg0], %[sg1]", ["sg0"]),                  # ge0 = h0 >= P0 = !br1
+         S("s_and_b64 %[se3], %[se3], %[sf1]", ["se3"]),
+         S("s_and_b64 %[se3], %[se3], %[sf2]", ["se3"]),
+         S("s_and_b64 %[se3], %[se3], %[sg0]", ["se3"]),
+         S(f"s_or_b64 %[sm], %[{carry}], %[stp]", ["sm"]),
+         S("s_or_b64 %[sm], %[sm], %[se3]", ["sm"]),                      # m
+         S("s_and_b64 %[sd1], %[sm], %[sg0]", ["sd1"]),                   # m & !br1
+         S("s_orn2_b64 %[sg1], %[sf1], %[sg0]", ["sg1"]),                 # !br2 = f1 | !ge0
+         S("s_and_b64 %[sd2], %[sm], %[sg1]", ["sd2"]),                   # m & !br2
+         S("s_andn2_b64 %[sg1], %[sg0], %[sf1]", ["sg1"]),                # br2 = ge0 & !f1
+         S("s_or_b64 %[sg1], %[sg1], %[sf2]", ["sg1"]),                   # !br3 = br2 | f2
+         S("s_and_b64 %[sd3], %[sm], %[sg1]", ["sd3"]),                   # m & !br3
+         V("v_cndmask_b32 %[vt1], 0, 19, %[sm]", [], ["sm"]),
+         V("v_cndmask_b32 %[vt2], 0, %[c80], %[sm]", [], ["sm"]),
+         V(f"v_add_co_u32 %[{o[0]}], %[sk0], %[{h[0]}], %[vt1]", ["sk0"]),
+         V(f"v_addc_co_u32 %[{o[2]}], %[sk1], %[{h[2]}], 0, %[sd1]", ["sk1"], ["sd1"]),
+         V(f"v_addc_co_u32 %[{o[4]}], %[sk2], %[{h[4]}], 0, %[sd2]", ["sk2"], ["sd2"]),
+         V(f"v_addc_co_u32 %[{o[6]}], %[sk3], %[{h[6]}], 0, %[sd3]", ["sk3"], ["sd3"]),
+         V(f"v_addc_co_u32 %[{o[1]}], %[sk0], %[{h[1]}], 0, %[sk0]", ["sk0"], ["sk0"]),
+         V(f"v_addc_co_u32 %[{o[3]}], %[sk1], %[{h[3]}], 0, %[sk1]", ["sk1"], ["sk1"]),
+         V(f"v_addc_co_u32 %[{o[5]}], %[sk2], %[{h[5]}], 0, %[sk2]", ["sk2"], ["sk2"]),
+         V(f"v_addc_co_u32 %[{o[7]}], %[sk3], %[{h[7]}], %[vt2], %[sk3]", ["sk3"], ["sk3"])]
+    return q
+
+
+FIX_SGPRS = ["sf1", "sf2", "se3", "stp", "sg0", "sg1", "sm", "sd1", "sd2", "sd3", "sk0", "sk1", "sk2", "sk3"]
+
+
+def emit(name, doc, args, ins, outs, vtemps, sgprs, body):
+    """args: [(param, prefix)] array params bound to scalars prefix0..7."""
+    # the block's last VALU instructions write SGPRs (carry-outs) that the compiler may reuse at once
+    # for a VMEM address: a VALU SGPR write followed by a VMEM read of it needs 5 wait states
+    # (gfx940/gfx950), and the compiler does not see inside the block
+    text = "\\n\\t".join(schedule(body) + ["s_nop 4"])
+    out = [f"// {d}" for d in doc]
+    out.append(f"__device__ __forceinline__ void {name}(uint32_t out[8], " +
+               ", ".join(f"const uint32_t {p}[8]" for p, _ in args) + ") {")
+    for p, pre in args:
+        out.append("    const uint32_t " + ", ".join(f"{pre}{i} = {p}[{i}]" for i in range(8)) + ";")
+    out.append("    uint32_t " + ", ".join(outs + vtemps) + ";")
+    out.append("    uint64_t " + ", ".join(sgprs) + ";")
+    out.append(f'    asm volatile("{text}"')
+    out.append("                 : " + ", ".join([f'[{x}] "=&v"({x})' for x in outs + vtemps] +
+                                          [f'[{x}] "=&s"({x})' for x in sgprs]))
+    out.append("                 : " + ", ".join([f'[{x}] "v"({x})' for x in ins] +
+                                          ['[c80] "v"(0x80000000u)', '[p0l] "s"(0xFFFFFFEDu)']))
+    # the SALU mask logic overwrites SCC; without the clobber the compiler keeps a compare's SCC
+    # live across the block (seen: s_cmp before the block, s_cbranch_scc1 after it)
+    out.append('                 : "scc");')
+    for i in range(8):
+        out.append(f"    out[{i}] = {outs[i]};")
+    out.append("    (void)" + "; (void)".join(sgprs + vtemps) + ";")
+    out.append("}")
+    return out
+
+
+def gen_add():
+    h = [f"h{i}" for i in range(8)]
+    o = [f"o{i}" for i in range(8)]
+    q = [V("v_add_co_u32 %[h0], %[scy], %[a0], %[b0]", ["scy"])]
+    for i in range(1, 8):
+        q.append(V(f"v_addc_co_u32 %[h{i}], %[scy], %[a{i}], %[b{i}], %[scy]", ["scy"], ["scy"]))
+    q += fix_seq(h, o, "scy")
+    return emit("fe_add_asm", ["fe25519_add (curve25519_ops.cu:41-68) on limb halves: exact 257-bit sum, then",
+                               "one lossy \"- p\" when it carried out or is >= p."],
+                [("fa", "a"), ("ga", "b")], [f"a{i}" for i in range(8)] + [f"b{i}" for i in range(8)],
+                o, h + ["vt1", "vt2", "vt3"], FIX_SGPRS + ["scy"], q)
+
+
+def gen_fold():
+    h = [f"h{i}" for i in range(8)]
+    o = [f"o{i}" for i in range(8)]
+    q = []
+    for i in (1, 2, 3):   # x_i == 2^64-1 (limb 0 has no carry-in)
+        q.append(V(f"v_and_b32 %[vt1], %[x{2 * i}], %[x{2 * i + 1}]"))
+        q.append(V(f"v_cmp_eq_u32 %[sq{i}], -1, %[vt1]", [f"sq{i}"]))
+    q.append(V("v_add_co_u32 %[h0], %[sk0], %[a0], %[x0]", ["sk0"]))
+    q.append(V("v_addc_co_u32 %[h1], %[scy], %[a1], %[x1], %[sk0]", ["scy"], ["sk0"]))
+    for i in (1, 2, 3):
+        q.append(V(f"v_addc_co_u32 %[h{2 * i}], %[sk0], %[a{2 * i}], %[x{2 * i}], %[scy]", ["sk0"], ["scy"]))
+        q.append(V(f"v_addc_co_u32 %[h{2 * i + 1}], %[sk1], %[a{2 * i + 1}], %[x{2 * i + 1}], %[sk0]", ["sk1"],
+                   ["sk0"]))
+        q.append(S(f"s_and_b64 %[sq{i}], %[sq{i}], %[scy]", [f"sq{i}"]))   # x_i == M & carry-in
+        q.append(S(f"s_andn2_b64 %[scy], %[sk1], %[sq{i}]", ["scy"]))      # the reference's carry
+    q += fix_seq(h, o, "scy")
+    return emit("fe_fold_asm", ["Fold of the exact 512-bit product (curve25519_ops.cu:114-145): t_lo as halves",
+                                "ta[0..7], x_i = lo64(19 t_{i+4}) as halves xa[0..7]; carry chain with the lossy",
+                                "carry cy_i = c_i & !(x_i == 2^64-1 & cy_{i-1}), then the fix-up."],
+                [("ta", "a"), ("xa", "x")], [f"a{i}" for i in range(8)] + [f"x{i}" for i in range(8)],
+                o, h + ["vt1", "vt2", "vt3"], FIX_SGPRS + ["scy", "sq1", "sq2", "sq3"], q)
+
+
+def gen_sub():
+    """fe25519_sub (curve25519_ops.cu:71-90): t = f - g with the lossy borrow
+    br_i = b_i & !(g_i == 2^64-1 & br_{i-1}); on a final borrow m, the literal "+ p" pass:
+    o0 = t0 - 19m; o1 = t1 - (m & t0 < 19); o2 = t2 - (m & o1 == M); o3 = t3 + m 2^63 - (m & o2 == M)
+    (fe25519_dev.h fe_sub).  m & t0 < 19 is exactly the borrow out of o0's subtraction."""
+    t = [f"h{i}" for i in range(8)]
+    o = [f"o{i}" for i in range(8)]
+    q = []
+    for i in (1, 2, 3):   # g_i == 2^64-1
+        q.append(V(f"v_and_b32 %[vt1], %[b{2 * i}], %[b{2 * i + 1}]"))
+        q.append(V(f"v_cmp_eq_u32 %[sq{i}], -1, %[vt1]", [f"sq{i}"]))
+    q.append(V("v_sub_co_u32 %[h0], %[sk0], %[a0], %[b0]", ["sk0"]))
+    q.append(V("v_subb_co_u32 %[h1], %[scy], %[a1], %[b1], %[sk0]", ["scy"], ["sk0"]))
+    for i in (1, 2, 3):
+        q.append(V(f"v_subb_co_u32 %[h{2 * i}], %[sk0], %[a{2 * i}], %[b{2 * i}], %[scy]", ["sk0"], ["scy"]))
+        q.append(V(f"v_subb_co_u32 %[h{2 * i + 1}], %[sk1], %[a{2 * i + 1}], %[b{2 * i + 1}], %[sk0]", ["sk1"],
+                   ["sk0"]))
+        q.append(S(f"s_and_b64 %[sq{i}], %[sq{i}], %[scy]", [f"sq{i}"]))
+        q.append(S(f"s_andn2_b64 %[scy], %[sk1], %[sq{i}]", ["scy"]))      # lossy borrow
+    q += [V("v_cndmask_b32 %[vt1], 0, 19, %[scy]", [], ["scy"]),
+          V("v_cndmask_b32 %[vt2], 0, %[c80], %[scy]", [], ["scy"]),
+          V("v_sub_co_u32 %[o0], %[sk0], %[h0], %[vt1]", ["sk0"]),
+          V("v_subb_co_u32 %[o1], %[sd1], %[h1], 0, %[sk0]", ["sd1"], ["sk0"]),        # d1 = m & t0 < 19
+          V("v_subb_co_u32 %[o2], %[sk1], %[h2], 0, %[sd1]", ["sk1"], ["sd1"]),
+          V("v_subb_co_u32 %[o3], %[sk1], %[h3], 0, %[sk1]", ["sk1"], ["sk1"]),
+          V("v_and_b32 %[vt1], %[o2], %[o3]"),
+          V("v_cmp_eq_u32 %[sd2], -1, %[vt1]", ["sd2"]),
+          S("s_and_b64 %[sd2], %[sd2], %[scy]", ["sd2"]),                              # d2 = m & o1 == M
+          V("v_subb_co_u32 %[o4], %[sk2], %[h4], 0, %[sd2]", ["sk2"], ["sd2"]),
+          V("v_subb_co_u32 %[o5], %[sk2], %[h5], 0, %[sk2]", ["sk2"], ["sk2"]),
+          V("v_and_b32 %[vt1], %[o4], %[o5]"),
+          V("v_cmp_eq_u32 %[sd3], -1, %[vt1]", ["sd3"]),
+          S("s_and_b64 %[sd3], %[sd3], %[scy]", ["sd3"]),                              # d3 = m & o2 == M
+          V("v_subb_co_u32 %[o6], %[sk3], %[h6], 0, %[sd3]", ["sk3"], ["sd3"]),
+          V("v_subb_co_u32 %[vt3], %[sk3], %[h7], 0, %[sk3]", ["sk3"], ["sk3"]),
+          V("v_add_u32 %[o7], %[vt3], %[vt2]")]                                         # + m 2^63
+    return emit("fe_sub_asm", ["fe25519_sub (curve25519_ops.cu:71-90) on limb halves: lossy borrow chain, then the",
+                               "literal \"+ p\" pass on a final borrow."],
+                [("fa", "a"), ("ga", "b")], [f"a{i}" for i in range(8)] + [f"b{i}" for i in range(8)],
+                o, t + ["vt1", "vt2", "vt3"], ["sk0", "sk1", "sk2", "sk3", "sd1", "sd2", "sd3", "scy", "sq1", "sq2",
+                                               "sq3"], q)
+
+
+def main():
+    out = ["// GENERATED by tools/gen_field_asm.py -- do not edit by hand.",
+           "// gfx950 inline-asm fe25519 add and product fold: the same bits as the C forms in fe25519_dev.h.",
+           "#pragma once", "#include <stdint.h>", "namespace bp {"]
+    out += gen_add() + [""] + gen_sub() + [""] + gen_fold()
+    out.append("}  // namespace bp")
+    open(OUT, "w").write("\n".join(out) + "\n")
+    print("wrote", OUT)
+
+
+if __name__ == "__main__":
+    main()

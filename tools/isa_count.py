@@ -10,6 +10,22 @@ import tempfile
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 
+# issue cost per wave64 instruction, cycles at 8 waves/SIMD (tools/ubench_enc.hip on MI355X, nominal clock)
+FULL = ("v_add_u32", "v_sub_u32", "v_and_b32", "v_or_b32", "v_xor_b32", "v_mov_b32", "v_not_b32", "v_subrev_u32")
+
+
+def cost(op):
+    base = op.split("_e32")[0].split("_e64")[0]
+    if base in FULL:
+        return 2.4
+    if base == "v_mad_u64_u32":
+        return 5.1
+    if base in ("v_lshl_add_u64",):
+        return 4.7
+    if base.startswith("v_"):
+        return 4.5
+    return 0.0
+
 
 def main():
     with tempfile.TemporaryDirectory() as d:
@@ -25,7 +41,9 @@ def main():
         c = collections.Counter(ins)
         valu = sum(n for i, n in c.items() if i.startswith("v_"))
         top = ", ".join(f"{k}:{v}" for k, v in c.most_common(8))
-        print(f"{name:14s} VALU {valu:5d}  s_nop {c['s_nop']:4d}  SALU {sum(n for i, n in c.items() if i.startswith('s_') and i != 's_nop'):4d}  | {top}")
+        cyc = sum(cost(i) * n for i, n in c.items() if not i.startswith(("global_", "ds_", "buffer_", "scratch_")))
+        print(f"{name:14s} VALU {valu:5d}  ~cyc {cyc:7.0f}  s_nop {c['s_nop']:4d}  "
+              f"SALU {sum(n for i, n in c.items() if i.startswith('s_') and i != 's_nop'):4d}  | {top}")
 
 
 if __name__ == "__main__":
