@@ -256,7 +256,9 @@ def prove_leg(args, dev):
     pi = {k: T(v) for k, v in synth.prove_inputs(B, n).items()}
     # two streams: one batch's latency-bound stages (T terms, IPA rounds, chains) run under the
     # other batch's term launches (each stream has its own prover workspace in the engine)
-    streams = [torch.cuda.Stream(dev) for _ in range(2)]
+    # (different priorities: HIP maps streams onto at most GPU_MAX_HW_QUEUES hardware queues and two
+    # same-priority streams created after the verify legs' streams can share one, which serializes them)
+    streams = [torch.cuda.Stream(dev, priority=0), torch.cuda.Stream(dev, priority=-1)]
     torch.cuda.synchronize(dev)
     run = lambda k: bp.batch_generate_range_proof(n, pi["v"], pi["gamma"], pi["sL"], pi["sR"], pi["rnd"], Gd, Hd,
                                                   gd, hd, stream=streams[k % 2])

@@ -130,7 +130,7 @@ struct Engine {
     Buf h2d[8], scratch[8];
     // prover workspaces (hipbp_batch_generate_range_proof), one per stream so batches on
     // different streams overlap (one batch's latency-bound stages under another's term launch)
-    struct ProverBufs { Buf b[16]; };
+    struct ProverBufs { Buf b[17]; };
     std::map<hipStream_t, ProverBufs*> provers;
     // pinned host staging for the single-proof entry points (a pageable source of an
     // async copy must outlive the copy; this one does, and the stream is synced after use)
@@ -623,18 +623,19 @@ int hipbp_batch_generate_range_proof(const hipbp_prove_input* in, const ge25519*
     // workspace: prover buffers are the engine's prv[] (reused across calls on the engine's lock)
     const size_t FE = sizeof(bp::fe), GE = sizeof(bp::ge);
     const size_t cap = B * (4 * n + 4);
-    size_t sz[16] = {B * 4 * n * FE, cap * GE, B * 4 * GE, B * 5 * GE, B * 8 * FE, B * 4 * FE, B * 4 * GE,
+    size_t sz[17] = {B * 4 * n * FE, cap * GE, B * 4 * GE, B * 5 * GE, B * 8 * FE, B * 4 * FE, B * 4 * GE,
                      B * n * FE, B * n * FE, B * 2 * n * FE, B * 2 * FE, B * (2 * n + 2) * GE, B * 4 * FE, B,
-                     2 * cap * sizeof(uint32_t), 2 * sizeof(unsigned)};
+                     2 * cap * sizeof(uint32_t), 2 * sizeof(unsigned), 2 * n * GE};
     hipStream_t s = pick(stream, *e);
     Engine::ProverBufs*& pb = e->provers[s];
     if (!pb) pb = new Engine::ProverBufs();
     Buf* prv = pb->b;
-    for (int i = 0; i < 16; i++) BP_RET_ON(prv[i].need(sz[i]));
+    for (int i = 0; i < 17; i++) BP_RET_ON(prv[i].need(sz[i]));
     bp::ProveWs w{prv[0].as<bp::fe>(), prv[1].as<bp::ge>(), prv[2].as<bp::ge>(), prv[3].as<bp::ge>(),
                   prv[4].as<bp::fe>(), prv[5].as<bp::fe>(), prv[6].as<bp::ge>(), prv[7].as<bp::fe>(),
                   prv[8].as<bp::fe>(), prv[9].as<bp::fe>(), prv[10].as<bp::fe>(), prv[11].as<bp::ge>(),
-                  prv[12].as<bp::fe>(), prv[13].as<uint8_t>(), prv[14].as<uint32_t>(), prv[15].as<unsigned>(), cap};
+                  prv[12].as<bp::fe>(), prv[13].as<uint8_t>(), prv[14].as<uint32_t>(), prv[15].as<unsigned>(), cap,
+                  prv[16].as<bp::ge>()};
     auto run = [&](int stage, int r) {
         bp::launch_prove(stage, r, pin, w, po, (const bp::ge*)G, (const bp::ge*)H, (const bp::ge*)g,
                          (const bp::ge*)h, e->dtab, e->two_i, s);

@@ -143,6 +143,8 @@ struct ProveWs {
     uint32_t* list;   // [2*cap], cap = B*(4n+4)
     unsigned* cnt;    // [2]
     size_t cap;
+    ge* ctab;     // [2n]      N(sm(tobytes(sub(0, 1)), H_i)) | N(sm(1, G_i)): the aR_i H_i term where
+                  //           aL_i = 0 and the aL_i G_i term where aL_i = 1, once per batch
 };
 enum ProveStage { PS_PREP = 0, PS_TERMS0, PS_CHAIN0, PS_COMMIT, PS_TERMS1, PS_TX, PS_RTERMS, PS_RCHAIN, PS_ROUND,
                   PS_FINAL };

@@ -20,6 +20,10 @@
 #include "ge25519_dev.h"
 #include "sha256_dev.h"
 
+#ifndef BP_GTAB
+#define BP_GTAB 1
+#endif
+
 namespace bp {
 
 namespace {
@@ -61,17 +65,18 @@ __device__ __forceinline__ int sclass(const fe& s) {
     return s.v[0] ? 1 : 0;
 }
 
-template <typename ScalarOf>
-__device__ __forceinline__ void queue_items(const ProveWs& ws, size_t p, int per, ScalarOf scalar_of) {
+// class_of(k): 0 constant (written by the caller), 1 light, 2 heavy, 3 from the per-batch table
+template <typename ClassOf>
+__device__ __forceinline__ void queue_items(const ProveWs& ws, size_t p, int per, ClassOf class_of) {
     unsigned nh = 0, nl = 0;
     for (int k = 0; k < per; k++) {
-        int c = sclass(scalar_of(k));
+        int c = class_of(k);
         nh += c == 2;
         nl += c == 1;
     }
     unsigned bh = nh ? atomicAdd(&ws.cnt[0], nh) : 0, bl = nl ? atomicAdd(&ws.cnt[1], nl) : 0;
     for (int k = 0; k < per; k++) {
-        int c = sclass(scalar_of(k));
+        int c = class_of(k);
         uint32_t id = (uint32_t)(p * per + k);
         if (c == 2) ws.list[bh++] = id;
         else if (c == 1) ws.list[ws.cap + bl++] = id;
@@ -116,7 +121,14 @@ __global__ __launch_bounds__(TPB) void k_prove_prep(ProveIn in, ProveWs ws, cons
     ge* pt = ws.pterm + p * per;
     for (int k = 0; k < per; k++)   // zero scalars: the constant term (raw for h^alpha, h^rho)
         if (sclass(terms0_scalar(in, ws, p, k)) == 0) pt[k] = dtab[k < 4 * n + 2 ? 257 : 256];
-    queue_items(ws, p, per, [&](int k) { return terms0_scalar(in, ws, p, k); });
+    // aR_i = sub(0, 1) wherever aL_i = 0, and aL_i = 1 otherwise: the same scalar on the same
+    // generator in every proof, so those terms are ws.ctab[i] (aR H_i) and ws.ctab[n + i] (1 G_i),
+    // computed once per batch by the first 2n lanes of k_prove_terms0
+    queue_items(ws, p, per, [&](int k) {
+        if (BP_GTAB && k < n && ps[k].v[0]) return 3;
+        if (k >= n && k < 2 * n && !(ps[k - n].v[0])) return 3;
+        return sclass(terms0_scalar(in, ws, p, k));
+    });
 }
 
 // ---------------------------------------------------------------- PS_TERMS0
@@ -129,8 +141,12 @@ __global__ __launch_bounds__(TPB, 3) void k_prove_terms0(ProveIn in, ProveWs ws,
     __shared__ geq qs[TPB];
     const int n = in.n;
     const size_t per = 4 * (size_t)n + 4;
-    uint32_t id;
-    if (!next_item(ws, gid(), id)) return;
+    // lanes [0, 2n): the table ws.ctab[j] = N(sm(tobytes(sub(0, 1)), H_j)) (the aR_j term of every
+    // proof with aL_j = 0), ws.ctab[n + j] = N(sm(1, G_j)) (the aL_j term where aL_j = 1); then the
+    // queued items
+    const size_t i = gid();
+    uint32_t id = 0;
+    if (i >= 2 * (size_t)n && !next_item(ws, i - 2 * n, id)) return;
     size_t p = id / per;
     int k = (int)(id % per);
     // operands are selected per lane and ONE scalar-mult follows: two call sites in one wave
@@ -138,7 +154,13 @@ __global__ __launch_bounds__(TPB, 3) void k_prove_terms0(ProveIn in, ProveWs ws,
     fe s;
     ge P;
     bool norm = true;
-    if (k < 4 * n) {
+    ge* dst = ws.pterm + id;
+    if (i < 2 * (size_t)n) {
+        const bool hs = i < (size_t)n;
+        P = hs ? H[i] : G[i - n];
+        s = hs ? fe_canon(fe_sub(fe_set(0), fe_set(1))) : fe_set(1);   // k_prove_prep's aR (aL = 0), aL = 1
+        dst = ws.ctab + i;
+    } else if (k < 4 * n) {
         int blk = k / n, j = k % n;
         P = (blk & 1) ? H[j] : G[j];
         s = ws.ps[p * 4 * n + k];
@@ -149,7 +171,7 @@ __global__ __launch_bounds__(TPB, 3) void k_prove_terms0(ProveIn in, ProveWs ws,
         norm = k < 2;                               // alpha_bytes / rho_bytes: raw, not normalized
     }
     ge r = scalarmult<true>(s, P, &qs[threadIdx.x], dtab);
-    ws.pterm[id] = norm ? ge_norm_host(r) : r;
+    *dst = norm ? ge_norm_host(r) : r;
 }
 
 // ---------------------------------------------------------------- chains
@@ -165,6 +187,24 @@ __global__ __launch_bounds__(TPB) void k_prove_chain(const ge* __restrict__ term
     ge acc = t[0];
     for (int i = 1; i < count; i++) acc = ge_norm_host(ge_add(acc, t[i]));
     out[c] = ge_norm_host(acc);
+}
+
+// chain set 0 (aL G | aR H | sL G | sR H): as k_prove_chain, the table terms from ws.ctab
+__global__ __launch_bounds__(TPB) void k_prove_chain0(ProveIn in, ProveWs ws) {
+    size_t c = gid();
+    if (c >= (size_t)in.B * 4) return;
+    const int n = in.n;
+    size_t p = c / 4;
+    int j = (int)(c % 4);
+    const ge* t = ws.pterm + p * (4 * (size_t)n + 4) + (size_t)j * n;
+    const fe* aL = ws.ps + p * 4 * (size_t)n;
+    auto term = [&](int i) {
+        if (BP_GTAB && j == 0 && aL[i].v[0]) return ws.ctab[n + i];
+        return (j == 1 && !aL[i].v[0]) ? ws.ctab[i] : t[i];
+    };
+    ge acc = term(0);
+    for (int i = 1; i < n; i++) acc = ge_norm_host(ge_add(acc, term(i)));
+    ws.chain[c] = ge_norm_host(acc);
 }
 
 // ---------------------------------------------------------------- PS_COMMIT
@@ -252,7 +292,7 @@ __device__ __forceinline__ void round_prep(const ProveWs& ws, size_t p, int n, i
     ge* it = ws.iterm + p * (2 * (size_t)n + 2);
     for (int k = 0; k < per; k++)   // zero scalars: the constant term (raw for c_L Q, c_R Q)
         if (sclass(scalar_of(k)) == 0) it[k] = dtab[k < 4 * np ? 257 : 256];
-    queue_items(ws, p, per, scalar_of);
+    queue_items(ws, p, per, [&](int k) { return sclass(scalar_of(k)); });
 }
 
 // ---------------------------------------------------------------- PS_TX
@@ -421,10 +461,10 @@ void launch_prove(int stage, int r, const ProveIn& in, const ProveWs& ws, const 
             (void)hipMemsetAsync(ws.cnt, 0, 2 * sizeof(unsigned), s);
             k_prove_prep<<<nblk(B), TPB, 0, s>>>(in, ws, dtab);
             break;
-        case PS_TERMS0: k_prove_terms0<<<nblk(B * (4 * (size_t)n + 4)), TPB, 0, s>>>(in, ws, G, H, g, h, dtab); break;
-        case PS_CHAIN0:
-            k_prove_chain<<<nblk(B * 4), TPB, 0, s>>>(ws.pterm, 4 * (size_t)n + 4, n, n, 4, ws.chain, in.B);
+        case PS_TERMS0:
+            k_prove_terms0<<<nblk(B * (4 * (size_t)n + 4) + 2 * n), TPB, 0, s>>>(in, ws, G, H, g, h, dtab);
             break;
+        case PS_CHAIN0: k_prove_chain0<<<nblk(B * 4), TPB, 0, s>>>(in, ws); break;
         case PS_COMMIT: k_prove_commit<<<nblk(B), TPB, 0, s>>>(in, ws, two_i); break;
         case PS_TERMS1: k_prove_terms1<<<nblk(B * 4), TPB, 0, s>>>(in, ws, g, h, dtab); break;
         case PS_TX:
