@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--ipa-batch", type=int, default=64, help="IPA proofs per pipeline tick")
     ap.add_argument("--ipa-steps", type=int, default=4)
     ap.add_argument("--no-ipa", action="store_true")
-    ap.add_argument("--prove-batch", type=int, default=16384, help="proofs per generate_range_proof batch")
+    ap.add_argument("--prove-batch", type=int, default=65536, help="proofs per generate_range_proof batch")
     ap.add_argument("--prove-steps", type=int, default=4)
     ap.add_argument("--no-prove", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)

@@ -49,7 +49,36 @@ def mean(xs):
     return sum(xs) / len(xs) if xs else float("nan")
 
 
+def prove_summary(tag):
+    """tools/profile_prove.sh output -> profiles/rocprof_<tag>_prove_summary.md"""
+    base = os.path.join(ROOT, "gpurun_out", f"prof_{tag}_prove")
+    stats = list(csv.DictReader(open(os.path.join(base, "trace", "run_kernel_stats.csv"))))
+    busy = load_counters(os.path.join(base, "pmc_busy"))
+    valu = load_counters(os.path.join(base, "pmc_valu"))
+    lines = [f"# rocprofv3 summary — prover, {tag}", "",
+             "Command: `tools/profile_prove.sh " + tag + "` on one MI355X (tools/prove_probe.py 16384 random: "
+             "two batches of 16384 64-bit proofs, hipbp_batch_generate_range_proof on one stream).", "",
+             "## Kernel trace (`rocprofv3 --kernel-trace --stats`)", "",
+             "| kernel | calls | avg ms | total ms | % time | VALUBusy % (mean over launches) | VALU instr/wave |",
+             "|---|---|---|---|---|---|---|"]
+    for r in stats:
+        k = short(r["Name"])
+        b = [v.get("VALUBusy", float("nan")) for v in busy.values() if v["kernel"] == k]
+        vi = [v.get("SQ_INSTS_VALU", 0) / v["SQ_WAVES"] for v in valu.values() if v["kernel"] == k and v.get("SQ_WAVES")]
+        lines.append(f"| {k} | {r['Calls']} | {float(r['AverageNs']) / 1e6:.3f} | {float(r['TotalDurationNs']) / 1e6:.2f} | "
+                     f"{float(r['Percentage']):.1f} | {mean(b):.1f} | {mean(vi):.0f} |")
+    lines += ["", "Per-batch launches: prep, terms0 (all A/S terms: the heavy scalar-mults), chain0, commit, "
+              "terms1, tx, then per IPA round rterms/chain/round, final. rterms launches last about one "
+              "scalar-mult latency whatever their size (latency-bound tails); bench.py runs two batches on "
+              "two streams so one batch's tails run under the other's terms0."]
+    out_md = os.path.join(ROOT, "profiles", f"rocprof_{tag}_prove_summary.md")
+    open(out_md, "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
 def main():
+    if len(sys.argv) > 2 and sys.argv[2] == "prove":
+        return prove_summary(sys.argv[1])
     tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
     base = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     out_md = os.path.join(ROOT, "profiles", f"rocprof_{tag}_summary.md")
