@@ -245,15 +245,18 @@ bp::BatchView view_of(const hipbp_proof_batch* b) {
     return v;
 }
 
-// The verify pipeline: a ring of D = log2(n) + 2 batch slots.  Every tick launches ONE
-// k_terms over all in-flight batches (the newest batch's challenges/scalars, stage 0 of the
-// one before, fold round r of the batch pushed r+1 ticks earlier, the final terms of the
-// oldest), then ONE k_combine (the stage-0 batch's MSM trees, fold combinations, final
-// assembly).  Within a batch the reference's order is kept exactly; across batches nothing
-// depends on anything.  Stages of a batch with L fold rounds:
-//   0: RK_PREP            1: RK_STAGE0 | RK_TREE, RK_COMBINE r=0
-//   r+1 (1<=r<L): RK_ROUND r | RK_COMBINE r         L+1: RK_FINAL_TERMS | RK_FINAL
-// (L = 0: stage 1 also carries RK_FINAL_TERMS and RK_FINAL moves to stage 2, after the tree.)
+// The verify pipeline: a ring of D batch slots.  Every tick is ONE k_terms launch over all
+// in-flight batches, each at its own stage; within a batch the reference's order is kept
+// exactly, across batches nothing depends on anything.  Stages of a batch with L fold rounds
+// (Pipeline::stages):
+//   0: RK_PREP (challenges, MSM scalars, round challenges)
+//   1: RK_STAGE0 (both MSMs' point terms, fold round 0, t*h, c*Q [, the 7 polynomial terms])
+//   2: RK_TREE (MSM trees of n > LANE_TREE_MAX points) [, RK_POLY]   r+1 (1 <= r < L): RK_ROUND r
+//   FT = L+1 (1 when L = 0): RK_FINAL_TERMS           mode 2, max(3, FT): RK_M3
+//   FIN = 1 + the last of those: RK_FINAL (the trees of n <= LANE_TREE_MAX MSMs, P, check point,
+//   accept)
+// A round-r item forms its own input point G'/H' from two round r-1 terms (each folded point
+// has exactly one consumer), so no launch of its own is needed for the fold combinations.
 struct Pipeline {
     Engine* e = nullptr;
     hipStream_t s = nullptr;
@@ -274,10 +277,32 @@ struct Pipeline {
     bp::SlotDev* host_dev = nullptr;    // pinned staging [D]
     int head = 0;
 
+    struct Stages {
+        int ft, m3, fin;
+    };
+    Stages stages(int L) const {
+        Stages g;
+        g.ft = L > 0 ? L + 1 : 1;
+        g.m3 = range_mode == 2 ? (g.ft > 3 ? g.ft : 3) : -1;
+        int last = g.ft;
+        if (range_mode && last < 2) last = 2;       // the MSM trees (RK_TREE blocks when n > LANE_TREE_MAX)
+        if (g.m3 > last) last = g.m3;
+        g.fin = last + 1;
+        return g;
+    }
+    // Layout switches (A/B: tools/ab_pipeline.sh; defaults = the measured best on MI355X,
+    // 138.7K verifies/s lane trees + chains last vs 137.9K block trees, 130.6K lane trees + chains
+    // first): HIPBP_LANE_TREE_MAX (lane trees for n <= it), HIPBP_CHAINS_FIRST (per-proof chain
+    // regions at the start of the grid instead of the end).
+    bool lane_tree = false, chains_first = false;
     hipError_t init(Engine* eng, hipStream_t st, size_t mb, int nn, int range) {
         e = eng; s = st; maxB = mb; n = nn; range_mode = range;
+        const char* lt = getenv("HIPBP_LANE_TREE_MAX");
+        lane_tree = n <= (lt ? atoi(lt) : bp::LANE_TREE_MAX);
+        const char* cf = getenv("HIPBP_CHAINS_FIRST");
+        chains_first = cf ? atoi(cf) != 0 : false;
         Lr = log2i((size_t)n);
-        D = (Lr > 0 ? Lr : 1) + 2;
+        D = stages(Lr).fin + 1;   // batches with fewer rounds finish earlier
         slots.resize(D);
         hipError_t r;
         if ((r = hipMalloc(&slots_dev, D * sizeof(bp::SlotDev))) != hipSuccess) return r;
@@ -301,16 +326,16 @@ struct Pipeline {
     }
     hipError_t carve(Slot& sl, size_t B, size_t Lb) {
         hipError_t r;
-        size_t nh = n / 2 ? n / 2 : 1, Lc = Lb ? Lb : 1;
+        size_t Lc = Lb ? Lb : 1;
         size_t sz[14] = {B * 32, B * n * 32, B * 4 * 32, B * Lc * 32, B * Lc * 32, B, B * 2 * n * 128, B * 2 * 128,
-                         B * 4 * 128, B * 2 * n * 128, B * nh * 128, B * nh * 128, B * 2 * 128, B * 128};
+                         B * 4 * 128, B * 2 * n * 128, B * 2 * n * 128, 0, B * 2 * 128, B * 128};
         for (int i = 0; i < 14; i++)
             if ((r = sl.b[i].need(sz[i])) != hipSuccess) return r;
         bp::VerifyWs& w = sl.dev.ws;
         w.sG = sl.b[0].as<bp::fe>(); w.sH = sl.b[1].as<bp::fe>(); w.sc = sl.b[2].as<bp::fe>();
         w.u = sl.b[3].as<bp::fe>(); w.uinv = sl.b[4].as<bp::fe>(); w.ipok = sl.b[5].as<uint8_t>();
         w.msm_pts = sl.b[6].as<bp::ge>(); w.msm_part = sl.b[7].as<bp::ge>(); w.terms = sl.b[8].as<bp::ge>();
-        w.fold = sl.b[9].as<bp::ge>(); w.Gc = sl.b[10].as<bp::ge>(); w.Hc = sl.b[11].as<bp::ge>();
+        w.fold[0] = sl.b[9].as<bp::ge>(); w.fold[1] = sl.b[10].as<bp::ge>();
         w.fin = sl.b[12].as<bp::ge>(); w.Pin = sl.b[13].as<bp::ge>();
         if (range_mode == 2) {
             size_t sz2[6] = {B * 8 * 32, B * 8 * 128, B * 2 * 128, B * 32, B * 2 * 128, B};
@@ -343,6 +368,7 @@ struct Pipeline {
             nw.dev.flags_out = flags_out;
             nw.dev.poly_out = (bp::ge*)poly_out;
             nw.dev.range_mode = range_mode;
+            nw.dev.lane_tree = lane_tree ? 1 : 0;
             BP_RET_ON(hipEventSynchronize(nw.copied));   // staging slot free again
             host_dev[head] = nw.dev;
             BP_RET_ON(hipMemcpyAsync(slots_dev + head, host_dev + head, sizeof(bp::SlotDev), hipMemcpyHostToDevice, s));
@@ -353,7 +379,7 @@ struct Pipeline {
             nw.stage = 0;
             nw.B = b->count;
         }
-        bp::RegionList tr{}, cr{};
+        bp::RegionList tr{};
         bool overflow = false;
         auto add = [&overflow](bp::RegionList& rl, int kind, int slot, int r, unsigned long long items, unsigned align) {
             if (!items) return;
@@ -362,44 +388,44 @@ struct Pipeline {
             g.kind = kind; g.slot = slot; g.r = r; g.begin = rl.total; g.items = items;
             rl.total += (items + align - 1) & ~(unsigned long long)(align - 1);   // wave / block aligned
         };
-        for (int pass = 0; pass < 2; pass++) {   // pass 0: the (block-aligned) tree region first
+        // pass 0: the (block-aligned) tree region, which must start the list; pass 2: the scalar
+        // multiplications; the per-proof chains (final assembly incl. lane trees, polynomial
+        // sides, challenges) in pass 3 by default (measured faster than pass 1, the grid start)
+        const int chain_pass = chains_first ? 1 : 3;
+        for (int pass = 0; pass < 4; pass++) {
             for (int k = 0; k < D; k++) {
                 int idx = (head - k + D) % D;   // newest first
                 Slot& sl = slots[idx];
                 if (!sl.active) continue;
                 unsigned long long B = sl.dev.bv.B;
                 int L = sl.dev.bv.L_len, st = sl.stage;
+                const Stages g = stages(L);
                 if (pass == 0) {
-                    if (st == 1 && range_mode) add(cr, bp::RK_TREE, idx, 0, B * 2 * n, 256);
-                    continue;
+                    if (st == 2 && range_mode && !lane_tree) add(tr, bp::RK_TREE, idx, 0, B * 2 * n, 256);
+                } else if (pass == chain_pass) {
+                    if (st == g.fin) add(tr, bp::RK_FINAL, idx, 0, B, 64);
+                    if (st == 2 && range_mode == 2) add(tr, bp::RK_POLY, idx, 0, B, 64);
+                    if (st == 0) add(tr, bp::RK_PREP, idx, 0, range_mode ? 2 * B : B, 64);
+                } else if (pass == 2) {
+                    if (st == 1) {
+                        unsigned long long it = (range_mode ? B * 2 * n : 0) + (L > 0 ? B * 2 * n : 0) + B * 2 +
+                                                (range_mode == 2 ? B * 7 : 0);   // == stage0_items (device)
+                        add(tr, bp::RK_STAGE0, idx, 0, it, 64);
+                    }
+                    if (st >= 2 && st <= L) add(tr, bp::RK_ROUND, idx, st - 1, B * 4 * (n >> st), 64);
+                    if (st == g.ft) add(tr, bp::RK_FINAL_TERMS, idx, 0, B * 2, 64);
+                    if (st == g.m3) add(tr, bp::RK_M3, idx, 0, B * 2, 64);
                 }
-                int fin_terms = L > 0 ? L + 1 : 1, fin = L > 0 ? L + 1 : 2;
-                if (st == 0) add(tr, bp::RK_PREP, idx, 0, range_mode ? 2 * B : B, 64);
-                if (st == 1) {
-                    unsigned long long it = (range_mode ? B * 2 * n : 0) + (L > 0 ? B * 2 * n : 0) + B * 2 +
-                                            (range_mode == 2 ? B * 7 : 0);   // == stage0_items (device)
-                    add(tr, bp::RK_STAGE0, idx, 0, it, 64);
-                    if (range_mode == 2) add(cr, bp::RK_POLY, idx, 0, B, 64);
-                }
-                if (range_mode == 2 && st == fin) add(tr, bp::RK_M3, idx, 0, B * 2, 64);
-                if (st >= 2 && st <= L) add(tr, bp::RK_ROUND, idx, st - 1, B * 4 * (n >> st), 64);
-                if (st == fin_terms) add(tr, bp::RK_FINAL_TERMS, idx, 0, B * 2, 64);
-                if (st >= 1 && st <= L) add(cr, bp::RK_COMBINE, idx, st - 1, B * 2 * (n >> st), 64);
-                if (st == fin) add(cr, bp::RK_FINAL, idx, 0, B, 64);
             }
         }
         if (overflow) { g_err = "pipeline region list overflow (internal)"; return HIPBP_ERR_ARG; }
         if (tm) tm->mark(bp::KT_TERMS, false, s);
         bp::launch_terms(tr, slots_dev, G, H, g ? g : h, h, e->dtab, e->two_i, s);
         if (tm) tm->mark(bp::KT_TERMS, true, s);
-        if (tm) tm->mark(bp::KT_COMBINE, false, s);
-        bp::launch_combine(cr, slots_dev, s);
-        if (tm) tm->mark(bp::KT_COMBINE, true, s);
         BP_RET_ON(hipGetLastError());
         for (auto& sl : slots) {
             if (!sl.active) continue;
-            int L = sl.dev.bv.L_len;
-            if (sl.stage == (L > 0 ? L + 1 : 2)) sl.active = false;
+            if (sl.stage == stages(sl.dev.bv.L_len).fin) sl.active = false;
             else sl.stage++;
         }
         head = (head + 1) % D;

@@ -42,9 +42,8 @@ struct VerifyWs {
     ge* msm_pts;   // [B*2*n]  per-point MSM terms
     ge* msm_part;  // [B*2]    tree results: <sG,G>, <sH,H>
     ge* terms;     // [B*4]    slots 2,3: t*h, c*Q
-    ge* fold;      // [B*2n]   per-round scalar-mult terms
-    ge* Gc;        // [B*n/2]
-    ge* Hc;        // [B*n/2]
+    ge* fold[2];   // [B*2n]   per-round scalar-mult terms, round r in fold[r & 1]; the next round's
+                   //          tasks combine them into the folded G'/H' they consume (crv:230, :240)
     ge* fin;       // [B*2]    a0*G', b0*H'
     ge* Pin;       // [B]      given P (inner-product-only verify)
     // range_proof_verify semantics (mode 2) only:
@@ -66,14 +65,15 @@ struct SlotDev {
     uint8_t* flags_out;   // mode 2, nullable
     ge* poly_out;         // mode 2, nullable
     int range_mode;       // 0 inner product only, 1 cuda_range_proof_verify, 2 range_proof_verify
+    int lane_tree;        // MSM trees reduced by final_task's lane (n <= lane-tree limit), else RK_TREE
 };
 
-// A tick's work list: region k covers items [begin_k, begin_{k+1}) of one slot at one stage.
-// k_terms regions: RK_PREP (challenges/scalars, one lane per proof and kind), RK_STAGE0,
-// RK_ROUND, RK_FINAL_TERMS, RK_M3 (mode 2: method-3 products).  k_combine regions: RK_TREE
-// (block-level MSM tree; always first, 256-aligned), RK_COMBINE, RK_FINAL, RK_POLY (mode 2:
-// polynomial identity sides).
-enum RegionKind { RK_STAGE0 = 0, RK_ROUND = 1, RK_FINAL_TERMS = 2, RK_COMBINE = 3, RK_FINAL = 4, RK_PREP = 5,
+// A tick's work list (one k_terms launch): region k covers items [begin_k, begin_{k+1}) of one
+// slot at one stage.  RK_TREE (block-level MSM tree; always first, 256-aligned), RK_PREP
+// (challenges/scalars, one lane per proof and kind), RK_STAGE0, RK_ROUND, RK_FINAL_TERMS,
+// RK_POLY (mode 2: polynomial identity sides), RK_M3 (mode 2: method-3 products), RK_FINAL
+// (P, check point, accept).
+enum RegionKind { RK_STAGE0 = 0, RK_ROUND = 1, RK_FINAL_TERMS = 2, RK_FINAL = 4, RK_PREP = 5,
                   RK_TREE = 6, RK_POLY = 7, RK_M3 = 8 };
 struct Region {
     int kind;
@@ -83,7 +83,11 @@ struct Region {
     unsigned long long begin;
     unsigned long long items;   // lanes [begin+items, next begin) are wave-alignment padding
 };
-constexpr int MAX_REGIONS = 20;   // >= 2 + log2(MAX_N) stages in flight
+// MSMs of at most this many points (the range proofs') are reduced by final_task's lane,
+// one MSM tree per lane (63 adds for n = 64, lanes fully busy, latency well inside a tick);
+// larger ones by RK_TREE blocks (levels 1..128 with LDS barriers) + final_task's upper levels.
+constexpr int LANE_TREE_MAX = 64;
+constexpr int MAX_REGIONS = 24;   // >= log2(MAX_N) + 3 stages in flight + 3 stages with 2 regions
 struct RegionList {
     int count;
     int pad;
@@ -97,7 +101,6 @@ enum KernelKind { KT_PREP = 0, KT_TERMS, KT_TREE, KT_COMBINE, KT_COUNT };
 void launch_init_tables(ge* dtab, fe* two_i, int nmax, hipStream_t s);
 void launch_terms(const RegionList& rl, const SlotDev* slots, const ge* G, const ge* H, const ge* g, const ge* h,
                   const ge* dtab, const fe* two_i, hipStream_t s);
-void launch_combine(const RegionList& rl, const SlotDev* slots, hipStream_t s);
 
 // Generic canonical-tree MSM: out[seg] for S segments of m points each.
 void launch_msm_points(ge* pts, const fe* scal, const ge* P, size_t m, const ge* dtab, hipStream_t s);

@@ -206,24 +206,31 @@ __device__ __forceinline__ void prep_ipa_task(const BatchView& bv, const VerifyW
 // IPA fold round r (crv:220-242), n' = n >> (r+1).  Items per proof (4n'):
 //   [0,n')   u^-1 * G_j        [n',2n')  u^-1 * H_{j+n'}
 //   [2n',3n') u * G_{j+n'}     [3n',4n') u * H_j
-// (lanes sharing a scalar are adjacent).  Round 0 reads the generators, later rounds
-// the proof's folded Gc/Hc.
+// (lanes sharing a scalar are adjacent).  Round 0 reads the generators; round r >= 1 reads
+// the folded G'/H' of round r-1, each of which exactly one item of round r consumes, so the
+// item forms it itself from the two round r-1 terms (crv:230, :240):
+//   G'_m = N(term(u^-1 G_m) + term(u G_{m+n''})),  H'_m = N(term(u H_m) + term(u^-1 H_{m+n''}))
+// with n'' = 2n' and the round r-1 terms at fold[(r-1) & 1] in the item order above.
+__device__ __forceinline__ ge folded_point(const VerifyWs& ws, int n, int r, size_t p, bool isH, int m) {
+    const int npp = n >> r;   // n'' = the previous round's n'
+    const ge* f = ws.fold[(r - 1) & 1] + p * (2 * n);
+    if (!isH) return ge_norm_host(ge_add(f[m], f[2 * npp + m]));
+    return ge_norm_host(ge_add(f[3 * npp + m], f[npp + m]));
+}
+
 __device__ __forceinline__ void fold_task(const BatchView& bv, const VerifyWs& ws, int r, size_t p, int k,
                                           geq* qslot, const ge* __restrict__ G, const ge* __restrict__ H,
                                           const ge* __restrict__ dtab) {
     const int n = bv.n, np = n >> (r + 1), Lr = bv.L_len;
     int grp = k / np, j = k % np;
-    const ge* Gs = (r == 0) ? G : ws.Gc + p * (n / 2);
-    const ge* Hs = (r == 0) ? H : ws.Hc + p * (n / 2);
-    const ge* pt;
-    fe s;
-    if (grp == 0) { pt = &Gs[j];      s = ws.uinv[p * Lr + r]; }
-    else if (grp == 1) { pt = &Hs[j + np]; s = ws.uinv[p * Lr + r]; }
-    else if (grp == 2) { pt = &Gs[j + np]; s = ws.u[p * Lr + r]; }
-    else { pt = &Hs[j];      s = ws.u[p * Lr + r]; }
-    ge P = *pt;   // through registers (an aggregate copy from a flat pointer goes via scratch)
+    const bool isH = grp == 1 || grp == 3;
+    const int m = (grp == 1 || grp == 2) ? j + np : j;
+    fe s = (grp < 2) ? ws.uinv[p * Lr + r] : ws.u[p * Lr + r];
+    ge P;   // through registers (an aggregate copy from a flat pointer goes via scratch)
+    if (r == 0) P = isH ? H[m] : G[m];
+    else P = folded_point(ws, n, r, p, isH, m);
     ge t = scalarmult<true>(s, P, qslot, dtab);
-    ws.fold[p * (2 * n) + k] = ge_norm_host(t);
+    ws.fold[r & 1][p * (2 * n) + k] = ge_norm_host(t);
 }
 
 // Stage 0: every scalar multiplication that depends only on the proof (contiguous per kind,
@@ -304,9 +311,10 @@ __device__ __forceinline__ void final_terms_task(const SlotDev& sd, size_t i, ge
     size_t p = i >> 1;
     bool isH = i & 1;
     const int n = bv.n;
-    const ge* pt = (bv.L_len > 0) ? (isH ? &ws.Hc[p * (n / 2)] : &ws.Gc[p * (n / 2)]) : (isH ? &H[0] : &G[0]);
     fe s = ws.sc[p * 4 + (isH ? 2 : 1)];
-    ge P = *pt;
+    ge P;   // G'_0 / H'_0 after the last round (formed from its terms), the generators when there is none
+    if (bv.L_len > 0) P = folded_point(ws, n, bv.L_len, p, isH, 0);
+    else P = isH ? H[0] : G[0];
     ge t = scalarmult<true>(s, P, qslot, dtab);
     ws.fin[p * 2 + (isH ? 1 : 0)] = ge_norm_host(t);
 }
@@ -321,41 +329,11 @@ __device__ __forceinline__ Region find_region(const RegionList& rl, size_t i) {
     return g;
 }
 
-// One pipeline tick's scalar multiplications: every region is one in-flight batch at its
-// own stage (stage 0 / fold round r / final terms), so a launch carries a whole batch's
-// worth of independent work however deep the batch-level dependency chain is.
-__global__ __launch_bounds__(TPB, 3) void k_terms(RegionList rl, const SlotDev* __restrict__ slots,
-                                               const ge* __restrict__ G, const ge* __restrict__ H,
-                                               const ge* __restrict__ g, const ge* __restrict__ h,
-                                               const ge* __restrict__ dtab, const fe* __restrict__ two_i) {
-    __shared__ geq qs[TPB];
-    size_t i = gid();
-    if (i >= rl.total) return;
-    const Region rg = find_region(rl, i);
-    size_t l = i - rg.begin;
-    if (l >= rg.items) return;
-    const SlotDev& sd = slots[rg.slot];
-    if (rg.kind == RK_PREP) {
-        // lanes [0,B): range-proof challenges and MSM scalars (range mode only), then [.., +B): IPA
-        const size_t B = sd.bv.B;
-        if (sd.range_mode && l < B) prep_range_task(sd.bv, sd.ws, two_i, l, sd.range_mode);
-        else prep_ipa_task(sd.bv, sd.ws, sd.range_mode ? l - B : l);
-    } else if (rg.kind == RK_STAGE0) {
-        stage0_task(sd, l, &qs[threadIdx.x], G, H, g, h, dtab);
-    } else if (rg.kind == RK_M3) {
-        m3_task(sd, l, &qs[threadIdx.x], dtab);
-    } else if (rg.kind == RK_ROUND) {
-        const int np = sd.bv.n >> (rg.r + 1);
-        fold_task(sd.bv, sd.ws, rg.r, l / (4 * np), (int)(l % (4 * np)), &qs[threadIdx.x], G, H, dtab);
-    } else {
-        final_terms_task(sd, l, &qs[threadIdx.x], G, H, dtab);
-    }
-}
-
 __device__ __forceinline__ int absdiff(int a, int b) { return a > b ? a - b : b - a; }
 
-// Levels TPB, 2 TPB, ... of the canonical MSM tree over cnt chunk roots stored
-// `stride` apart (in place; the slot's own workspace).  Used when n > TPB.
+// Canonical MSM tree over cnt points stored `stride` apart, evaluated level by
+// level by one lane, in place (the slot's own workspace): stride 1 = the whole tree of an
+// n <= LANE_TREE_MAX MSM; stride TPB = levels TPB, 2 TPB, ... over the per-block chunk roots.
 __device__ __forceinline__ ge tree_upper(ge* T, int cnt, int stride) {
     for (int st = 1; st < cnt; st <<= 1)
         for (int i = 0; i + st < cnt; i += 2 * st)
@@ -370,8 +348,11 @@ __device__ __forceinline__ void final_task(const SlotDev& sd, size_t p) {
     ge P;
     if (sd.range_mode) {
         ge m0, m1;
-        if (sd.bv.n > TPB) {   // upper tree levels over the per-block chunk roots (k_combine RK_TREE)
-            const int n = sd.bv.n;
+        const int n = sd.bv.n;
+        if (sd.lane_tree) {         // the whole tree here: every add with all 64 lanes busy
+            m0 = tree_upper(ws.msm_pts + (p * 2 + 0) * n, n, 1);
+            m1 = tree_upper(ws.msm_pts + (p * 2 + 1) * n, n, 1);
+        } else if (n > TPB) {       // upper tree levels over the per-block chunk roots (RK_TREE)
             m0 = tree_upper(ws.msm_pts + (p * 2 + 0) * n, n / TPB, TPB);
             m1 = tree_upper(ws.msm_pts + (p * 2 + 1) * n, n / TPB, TPB);
         } else {
@@ -488,11 +469,19 @@ __device__ __forceinline__ void poly_task(const SlotDev& sd, size_t p) {
     }
 }
 
-// One pipeline tick's point combinations: fold round r  G'_j = N(term(u^-1 G_j) + term(u G_{j+n'})),
-// H'_j = N(term(u H_j) + term(u^-1 H_{j+n'}))  (crv:230, :240), or the final assembly.
+// One pipeline tick = ONE launch.  Every region is one in-flight batch at its own stage
+// (challenges / stage 0 / MSM trees / fold round r / final terms / final assembly), so a launch
+// carries a whole batch's worth of independent work however deep the batch-level dependency
+// chain is, and the short per-proof chains (trees, final assembly) run under the scalar
+// multiplications of the other batches instead of in a latency-bound launch of their own.
 // The RK_TREE region (if any) comes first and spans whole blocks: each block folds TPB/n
-// segments of the batch's 2B MSMs with the canonical tree of k_tree, barriers block-uniform.
-__global__ __launch_bounds__(TPB) void k_combine(RegionList rl, const SlotDev* __restrict__ slots) {
+// segments of the batch's 2B MSMs with the canonical tree of k_tree, barriers block-uniform;
+// its LDS is the q-operand array (no scalar multiplication runs in those blocks).
+__global__ __launch_bounds__(TPB, 4) void k_terms(RegionList rl, const SlotDev* __restrict__ slots,
+                                               const ge* __restrict__ G, const ge* __restrict__ H,
+                                               const ge* __restrict__ g, const ge* __restrict__ h,
+                                               const ge* __restrict__ dtab, const fe* __restrict__ two_i) {
+    __shared__ geq qs[TPB];
     size_t i = gid();
     if (i >= rl.total) return;
     const Region rg = find_region(rl, i);
@@ -502,7 +491,7 @@ __global__ __launch_bounds__(TPB) void k_combine(RegionList rl, const SlotDev* _
         // chunks of min(n, TPB) points: n <= TPB -> one MSM per chunk, root to msm_part;
         // n > TPB -> the chunk root is written back in place at the chunk's first point and
         // final_task runs the remaining levels (tree_upper).
-        __shared__ ge sh[TPB];
+        ge* sh = reinterpret_cast<ge*>(qs);
         const int n = sd.bv.n, ch = n < TPB ? n : TPB, tid = threadIdx.x, idx = tid & (ch - 1);
         const bool live = l < rg.items;
         if (live) sh[tid] = sd.ws.msm_pts[l];
@@ -518,17 +507,22 @@ __global__ __launch_bounds__(TPB) void k_combine(RegionList rl, const SlotDev* _
         return;
     }
     if (l >= rg.items) return;
-    if (rg.kind == RK_POLY) {
+    if (rg.kind == RK_PREP) {
+        // lanes [0,B): range-proof challenges and MSM scalars (range mode only), then [.., +B): IPA
+        const size_t B = sd.bv.B;
+        if (sd.range_mode && l < B) prep_range_task(sd.bv, sd.ws, two_i, l, sd.range_mode);
+        else prep_ipa_task(sd.bv, sd.ws, sd.range_mode ? l - B : l);
+    } else if (rg.kind == RK_STAGE0) {
+        stage0_task(sd, l, &qs[threadIdx.x], G, H, g, h, dtab);
+    } else if (rg.kind == RK_M3) {
+        m3_task(sd, l, &qs[threadIdx.x], dtab);
+    } else if (rg.kind == RK_ROUND) {
+        const int np = sd.bv.n >> (rg.r + 1);
+        fold_task(sd.bv, sd.ws, rg.r, l / (4 * np), (int)(l % (4 * np)), &qs[threadIdx.x], G, H, dtab);
+    } else if (rg.kind == RK_FINAL_TERMS) {
+        final_terms_task(sd, l, &qs[threadIdx.x], G, H, dtab);
+    } else if (rg.kind == RK_POLY) {
         poly_task(sd, l);
-    } else if (rg.kind == RK_COMBINE) {
-        const int n = sd.bv.n, np = n >> (rg.r + 1);
-        size_t p = l / (2 * np);
-        int k = (int)(l % (2 * np));
-        const ge* f = sd.ws.fold + p * (2 * n);
-        if (k < np)
-            sd.ws.Gc[p * (n / 2) + k] = ge_norm_host(ge_add(f[k], f[2 * np + k]));
-        else
-            sd.ws.Hc[p * (n / 2) + (k - np)] = ge_norm_host(ge_add(f[3 * np + (k - np)], f[np + (k - np)]));
     } else {
         final_task(sd, l);
     }
@@ -541,9 +535,6 @@ void launch_terms(const RegionList& rl, const SlotDev* slots, const ge* G, const
     if (rl.total) k_terms<<<nblk(rl.total), TPB, 0, s>>>(rl, slots, G, H, g, h, dtab, two_i);
 }
 
-void launch_combine(const RegionList& rl, const SlotDev* slots, hipStream_t s) {
-    if (rl.total) k_combine<<<nblk(rl.total), TPB, 0, s>>>(rl, slots);
-}
 
 // ------------------------------------------------------------------ batch field ops
 // cuda_field_ops.cu:37-73 (add/sub/mul), :147 (square quirk), :521 (SoA add: limbwise, no carry)
