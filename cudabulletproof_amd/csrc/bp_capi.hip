@@ -617,8 +617,11 @@ int hipbp_msm(ge25519* result, const fe25519* scalars, const ge25519* points, si
     BP_RET_ON(e->scratch[0].need(n * sizeof(bp::ge)));
     BP_RET_ON(e->scratch[1].need(nb * sizeof(bp::ge)));
     BP_RET_ON(e->scratch[2].need(nb * sizeof(bp::ge)));
+    BP_RET_ON(e->scratch[6].need(n * sizeof(uint32_t)));
+    BP_RET_ON(e->scratch[7].need(bp::MSM_BINS * sizeof(unsigned)));
     bp::launch_msm_full((bp::ge*)result, (const bp::fe*)scalars, (const bp::ge*)points, n, e->scratch[0].as<bp::ge>(),
-                        e->scratch[1].as<bp::ge>(), e->scratch[2].as<bp::ge>(), e->dtab, pick(stream, *e));
+                        e->scratch[1].as<bp::ge>(), e->scratch[2].as<bp::ge>(), e->scratch[6].as<uint32_t>(),
+                        e->scratch[7].as<unsigned>(), e->dtab, pick(stream, *e));
     BP_RET_ON(hipGetLastError());
     return HIPBP_OK;
 }
@@ -734,9 +737,11 @@ void cuda_point_vector_multi_scalar_mul(ge25519* result, const FieldVector* scal
     BP_EXIT_ON(e.scratch[0].need(n * sizeof(bp::ge)));
     BP_EXIT_ON(e.scratch[1].need(nb * sizeof(bp::ge)));
     BP_EXIT_ON(e.scratch[2].need(nb * sizeof(bp::ge)));
+    BP_EXIT_ON(e.scratch[6].need(n * sizeof(uint32_t)));
+    BP_EXIT_ON(e.scratch[7].need(bp::MSM_BINS * sizeof(unsigned)));
     bp::launch_msm_full(e.h2d[2].as<bp::ge>(), e.h2d[0].as<bp::fe>(), e.h2d[1].as<bp::ge>(), n,
-                        e.scratch[0].as<bp::ge>(), e.scratch[1].as<bp::ge>(), e.scratch[2].as<bp::ge>(), e.dtab,
-                        e.stream);
+                        e.scratch[0].as<bp::ge>(), e.scratch[1].as<bp::ge>(), e.scratch[2].as<bp::ge>(),
+                        e.scratch[6].as<uint32_t>(), e.scratch[7].as<unsigned>(), e.dtab, e.stream);
     BP_EXIT_ON(hipGetLastError());
     BP_EXIT_ON(hipMemcpyAsync(result, e.h2d[2].p, sizeof(ge25519), hipMemcpyDeviceToHost, e.stream));
     BP_EXIT_ON(hipStreamSynchronize(e.stream));

@@ -102,8 +102,12 @@ void launch_init_tables(ge* dtab, fe* two_i, int nmax, hipStream_t s);
 void launch_terms(const RegionList& rl, const SlotDev* slots, const ge* G, const ge* H, const ge* g, const ge* h,
                   const ge* dtab, const fe* two_i, hipStream_t s);
 
-// Generic canonical-tree MSM: out[seg] for S segments of m points each.
-void launch_msm_points(ge* pts, const fe* scal, const ge* P, size_t m, const ge* dtab, hipStream_t s);
+// Generic canonical-tree MSM.  perm [m] / bins [MSM_BINS] (nullable): workspace of the
+// counting sort that groups items of equal chain length into the same waves (m >= MSM_SORT_MIN).
+constexpr size_t MSM_SORT_MIN = 4096;
+constexpr int MSM_BINS = 513;
+void launch_msm_points(ge* pts, const fe* scal, const ge* P, size_t m, uint32_t* perm, unsigned* bins,
+                       const ge* dtab, hipStream_t s);
 void launch_tree(ge* out, const ge* in, int S, size_t m, hipStream_t s);
 
 
@@ -162,5 +166,5 @@ void launch_ip_batch(fe* out, const fe* a, const fe* b, size_t n, size_t nvec, h
 void launch_invert(fe* r, const fe* a, size_t count, hipStream_t s);
 void launch_tree_full(ge* result, const ge* in, size_t n, ge* part0, ge* part1, hipStream_t s);
 void launch_msm_full(ge* result, const fe* scal, const ge* P, size_t n, ge* ptsbuf, ge* part0, ge* part1,
-                     const ge* dtab, hipStream_t s);
+                     uint32_t* perm, unsigned* bins, const ge* dtab, hipStream_t s);
 }  // namespace bp
