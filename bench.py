@@ -182,9 +182,9 @@ def msm_leg(args, dev, world, rank, T):
     import torch.distributed as dist
     from cudabulletproof_amd import shard, synth
     nm = 1 << args.msm_log2
-    sc, pts = synth.msm_inputs(nm)
     lo, hi = shard.msm_shard_bounds(nm, world, rank)
-    scd, ptd = T(sc[lo:hi]), T(pts[lo:hi])
+    sc, pts = synth.msm_config3(lo, hi, dev)   # SURVEY §8(d) config 3 inputs, this rank's rows
+    scd, ptd = T(sc), T(pts)
     del sc, pts
     shard.sharded_msm(scd, ptd, nm)
     torch.cuda.synchronize(dev)
@@ -203,10 +203,18 @@ def msm_leg(args, dev, world, rank, T):
         t = torch.tensor([mdt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         mdt = float(t.item())
+    digest = hashlib.sha256(res.cpu().numpy().tobytes()).hexdigest()[:16]
+    golden_ok = None   # tests/golden/msm_2p20.json: the CPU restatement's result for the 2^20 inputs
+    gpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden", "msm_2p20.json")
+    if os.path.exists(gpath):
+        with open(gpath) as f:
+            gold = json.load(f)
+        if gold["n"] == nm:
+            golden_ok = digest == gold["digest"]
     return {"metric": "MSM points/sec", "value": nm / mdt, "unit": "points/s", "points": nm,
             "ms_per_msm": mdt * 1e3, "n_gpus": world, "scaling": "strong" if world > 1 else None,
             "semantics": "canonical-tree per-point double-and-add (SURVEY A9); shards + all_gather + tree at N>1",
-            "result_sha256": hashlib.sha256(res.cpu().numpy().tobytes()).hexdigest()[:16]}
+            "result_sha256": digest, "matches_oracle_golden": golden_ok}
 
 
 def ipa_leg(args, dev):

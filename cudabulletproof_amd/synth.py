@@ -21,16 +21,20 @@ def _le_limbs(b32):
     return np.frombuffer(b32, dtype="<u8").astype(np.uint64)
 
 
-def base_points_xy(n, seed_byte):
-    """X, Y limbs of generate_deterministic_base_points (complete_bulletproof_test.cu:33-63)."""
+def base_points_xy(n, seed_byte, lo=0):
+    """X, Y limbs of generate_deterministic_base_points (complete_bulletproof_test.cu:33-63),
+    points lo .. lo+n-1."""
     seed = bytes([seed_byte]) + bytes(31)
-    pts = np.zeros((n, 16), np.uint64)
-    for i in range(n):
+    xs = bytearray()
+    ys = bytearray()
+    for i in range(lo, lo + n):
         x = hashlib.sha256(seed + int(i).to_bytes(4, "big")).digest()
-        y = hashlib.sha256(x).digest()
-        pts[i, 0:4] = _le_limbs(x)
-        pts[i, 4:8] = _le_limbs(y)
-        pts[i, 8] = 1
+        xs += x
+        ys += hashlib.sha256(x).digest()
+    pts = np.zeros((n, 16), np.uint64)
+    pts[:, 0:4] = np.frombuffer(bytes(xs), dtype="<u8").reshape(n, 4)
+    pts[:, 4:8] = np.frombuffer(bytes(ys), dtype="<u8").reshape(n, 4)
+    pts[:, 8] = 1
     return pts
 
 
@@ -97,6 +101,18 @@ def proofs(count, n, seed=1):
         V=_rand_pt(rng, (count,)), A=_rand_pt(rng, (count,)), S=_rand_pt(rng, (count,)),
         T1=_rand_pt(rng, (count,)), T2=_rand_pt(rng, (count,)), t=t, a=t[:, None, :].copy(), b=one,
         c=t.copy(), x=_rand_fe(rng, (count,)), L=_rand_pt(rng, (count, Lr)), R=_rand_pt(rng, (count, Lr)))
+
+
+def msm_config3(lo, hi, device):
+    """SURVEY §8(d) config 3 (BASELINE configs[2]), rows lo..hi-1 of the 2^20-point MSM input:
+    points = base points with seed {5} (T = X*Y on the GPU), scalars_i = SHA256("msm-s" || i_le32)
+    with byte 31 &= 0x7F.  tests/golden/msm_2p20.json holds the oracle's result for all 2^20."""
+    sc = bytearray()
+    for i in range(lo, hi):
+        sc += hashlib.sha256(b"msm-s" + int(i).to_bytes(4, "little")).digest()
+    s = np.frombuffer(bytes(sc), dtype="<u8").reshape(hi - lo, 4).copy()
+    s[:, 3] &= MASK63
+    return s, fill_T(base_points_xy(hi - lo, 5, lo), device)
 
 
 def msm_inputs(n, seed=5):

@@ -1,0 +1,97 @@
+"""Parity at BASELINE.json's full sizes (configs[2] and configs[4]), where the oracle cannot run
+the whole job inside a test:
+
+* configs[2]: the 2^20-point canonical-tree MSM on SURVEY §8(d)'s config-3 inputs against the
+  digest the CPU restatement produced (tests/golden/msm_2p20.json, make_msm_2p20.py), plus the
+  size-independent decomposition property (per-shard roots == the oracle's shard roots, and
+  the tree over them == the whole MSM).
+* configs[4]: a 2^16-proof batch = 1024 distinct 64-bit proofs tiled x64 (SURVEY §8(d) config 5:
+  the kernel must not dedupe) in ONE batched call: every tile returns exactly tile 0's verdicts,
+  P and check points, and a sample of tile 0 matches the oracle.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def d8(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()[:16]
+
+
+def _msm_inputs(oracle, n):
+    P = oracle.base_points(n, 5)
+    s = np.stack([np.frombuffer(hashlib.sha256(b"msm-s" + i.to_bytes(4, "little")).digest(), "<u8")
+                  for i in range(n)]).astype(np.uint64)
+    s[:, 3] &= np.uint64(0x7FFFFFFFFFFFFFFF)
+    return s, P
+
+
+def test_msm_2p20_matches_oracle_digest(bp, oracle):
+    import torch
+    with open(os.path.join(GOLDEN, "msm_2p20.json")) as f:
+        gold = json.load(f)
+    n = gold["n"]
+    s, P = _msm_inputs(oracle, n)
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    sd, Pd = T(s), T(P)
+    out = torch.zeros(16, dtype=torch.int64, device=dev)
+    bp.msm(out, sd, Pd)
+    torch.cuda.synchronize()
+    res = out.cpu().numpy().view(np.uint64)
+    assert d8(res) == gold["digest"]
+    assert [int(x) for x in res] == gold["result"]
+    # decomposition: each aligned 2^17 shard's MSM is the oracle's shard root, and the canonical
+    # tree over the roots (hipbp_point_tree) is the whole MSM again
+    m = 1 << gold["shard_log2"]
+    roots = torch.zeros(n // m, 16, dtype=torch.int64, device=dev)
+    for k in range(n // m):
+        bp.msm(roots[k], sd[k * m:(k + 1) * m], Pd[k * m:(k + 1) * m])
+    torch.cuda.synchronize()
+    assert np.array_equal(roots.cpu().numpy().view(np.uint64), np.array(gold["shard_roots"], np.uint64))
+    top = torch.zeros(16, dtype=torch.int64, device=dev)
+    bp.point_tree(top, roots)
+    torch.cuda.synchronize()
+    assert np.array_equal(top.cpu().numpy().view(np.uint64), res)
+
+
+def test_batch_2p16_tiled_verify(bp, oracle):
+    import torch
+    from cudabulletproof_amd import synth
+    n, distinct, tiles = 64, 1024, 64
+    base = synth.proofs(distinct, n, seed=4242)
+    base["c"][7] = base["c"][7] ^ np.uint64(1)        # a few failing proofs ride along
+    base["t"][11] = 0
+    arrays = {k: np.ascontiguousarray(np.concatenate([v] * tiles)) for k, v in base.items()}
+    B = distinct * tiles
+    G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+    g, h = oracle.gh()
+    dev = torch.device("cuda:0")
+    batch = bp.RangeProofBatch.from_numpy(n, arrays, dev)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    ok = torch.zeros(B, dtype=torch.uint8, device=dev)
+    P = torch.zeros(B, 16, dtype=torch.int64, device=dev)
+    chk = torch.zeros(B, 16, dtype=torch.int64, device=dev)
+    bp.batch_range_proof_verify(batch, T(G), T(H), T(g), T(h), ok, P, chk)
+    torch.cuda.synchronize()
+    ok = ok.cpu().numpy().astype(bool).reshape(tiles, distinct)
+    P = P.cpu().numpy().view(np.uint64).reshape(tiles, distinct, 16)
+    chk = chk.cpu().numpy().view(np.uint64).reshape(tiles, distinct, 16)
+    assert (ok == ok[0]).all() and (P == P[0]).all() and (chk == chk[0]).all()
+    assert not ok[0, 7]
+    for p in (0, 7, 11, 500, 1023):
+        head = np.concatenate([base[k][p] for k in ("V", "A", "S", "T1", "T2")] +
+                              [np.zeros(8, np.uint64), base["t"][p], base["c"][p], base["x"][p]])
+        okr, Pr, chkr, _, _ = oracle.cuda_range_proof_verify(head, base["V"][p], n, base["a"][p], base["b"][p],
+                                                             base["L"][p], base["R"][p], G, H, g, h)
+        assert ok[0, p] == okr, p
+        assert np.array_equal(P[0, p], Pr), p
+        if okr:
+            assert np.array_equal(chk[0, p], chkr), p

@@ -1,9 +1,12 @@
 """The CPU restatement (oracle/bp_oracle.c) against fixtures produced by the reference's own
 code (tests/golden/make_golden.py) and against the survey's golden digests."""
 import hashlib
+import os
 
 import numpy as np
 import pytest
+
+from conftest import GOLDEN
 
 
 def d8(a):
@@ -159,3 +162,13 @@ def test_prover_refuses_out_of_range(oracle):
     v = np.zeros(32, np.uint8)
     v[0], v[1] = 0xFF, 0xFF                                # 2^16 - 1: in range
     assert oracle.generate_range_proof(v, gamma, sLR, rnd4, n, G, H, g, h) is not None
+
+
+def test_msm_2p20_golden_consistent(oracle):
+    """tests/golden/msm_2p20.json: the canonical tree over its 8 shard roots is its result."""
+    import json
+    with open(os.path.join(GOLDEN, "msm_2p20.json")) as f:
+        gold = json.load(f)
+    roots = np.array(gold["shard_roots"], np.uint64)
+    assert roots.shape == (gold["n"] >> gold["shard_log2"], 16)
+    assert [int(x) for x in oracle.point_tree(roots)] == gold["result"]
