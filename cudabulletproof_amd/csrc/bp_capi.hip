@@ -295,8 +295,18 @@ struct Pipeline {
     // first): HIPBP_LANE_TREE_MAX (lane trees for n <= it), HIPBP_CHAINS_FIRST (per-proof chain
     // regions at the start of the grid instead of the end).
     bool lane_tree = false, chains_first = false;
+    // Lane sort (bp::launch_lane_sort): per-lane-scalar items in chain-length order, for batches
+    // of at least LANE_SORT_MIN proofs (HIPBP_LANE_SORT=0 turns it off, for A/B runs).
+    static constexpr size_t LANE_SORT_MIN = 64;
+    bool lane_sort = true;
+    int lane_sort_mask = 7;   // bit 0 stage 0, bit 1 rounds, bit 2 final terms, bit 3 shortest first
+    Buf sort_bins, sort_offs;
+    bp::LaneSortPlan plan{};
     hipError_t init(Engine* eng, hipStream_t st, size_t mb, int nn, int range) {
         e = eng; s = st; maxB = mb; n = nn; range_mode = range;
+        const char* ls = getenv("HIPBP_LANE_SORT");
+        lane_sort_mask = ls ? atoi(ls) : 7;
+        lane_sort = (lane_sort_mask & 7) != 0;
         const char* lt = getenv("HIPBP_LANE_TREE_MAX");
         lane_tree = n <= (lt ? atoi(lt) : bp::LANE_TREE_MAX);
         const char* cf = getenv("HIPBP_CHAINS_FIRST");
@@ -319,6 +329,58 @@ struct Pipeline {
         }
         if (slots_dev) (void)hipFree(slots_dev);
         if (host_dev) (void)hipHostFree(host_dev);
+        if (sort_bins.p) (void)hipFree(sort_bins.p);
+        if (sort_offs.p) (void)hipFree(sort_offs.p);
+    }
+    // The batch's per-lane item sets (stage 0's per-lane part, the rounds whose scalar runs are
+    // shorter than a wave, the final terms), their lane-order buffers and the sort plan.
+    hipError_t plan_sort(Slot& sl, int idx) {
+        plan = bp::LaneSortPlan{};
+        bp::SlotDev& d = sl.dev;
+        d.perm0 = nullptr;
+        for (auto& q : d.permr) q = nullptr;
+        d.perm_ft = nullptr;
+        const unsigned long long B = d.bv.B;
+        const int L = d.bv.L_len;
+        if (!lane_sort || B < LANE_SORT_MIN) return hipSuccess;
+        struct S { int kind, r; unsigned long long items; };
+        S sets[bp::LANE_SORT_SETS];
+        int cnt = 0;
+        const bp::Stage0Lanes z = bp::stage0_lanes(B, n, L, range_mode);
+        for (int c = 0; c < 4; c++)   // one set per class, contiguous in perm0 (stage0_item)
+            if (z.size[c] && (lane_sort_mask & 1)) sets[cnt++] = {bp::SS_STAGE0, c, z.size[c]};
+        for (int r = 1; r < L; r++)
+            if (bp::round_per_lane(n, r) && (lane_sort_mask & 2))
+                sets[cnt++] = {bp::SS_ROUND, r, B * 4 * (unsigned long long)(n >> (r + 1))};
+        if (lane_sort_mask & 4) sets[cnt++] = {bp::SS_FT, 0, B * 2};
+        if (!cnt) return hipSuccess;
+        plan.longest_first = (lane_sort_mask & 8) ? 0 : 1;
+        unsigned long long total = 0;
+        for (int k = 0; k < cnt; k++) total += sets[k].items;
+        if (total > 0xFFFFFFFFull) return hipSuccess;
+        hipError_t r;
+        if ((r = sl.b[20].need(total * sizeof(uint32_t))) != hipSuccess) return r;
+        const size_t nb = (size_t)bp::LANE_SORT_SETS * bp::MSM_BINS * sizeof(unsigned);
+        if (!sort_bins.p) {
+            if ((r = sort_bins.need(nb)) != hipSuccess) return r;
+            if ((r = hipMemsetAsync(sort_bins.p, 0, nb, s)) != hipSuccess) return r;
+            if ((r = sort_offs.need(nb)) != hipSuccess) return r;
+        }
+        uint32_t* base = sl.b[20].as<uint32_t>();
+        unsigned blk = 0;
+        for (int k = 0; k < cnt; k++) {
+            bp::LaneSortPlan::Set& st = plan.set[k];
+            st.kind = sets[k].kind; st.r = sets[k].r; st.items = sets[k].items; st.perm = base; st.block0 = blk;
+            if (st.kind == bp::SS_STAGE0 && !d.perm0) d.perm0 = base;
+            else if (st.kind == bp::SS_ROUND) d.permr[st.r] = base;
+            else d.perm_ft = base;
+            base += sets[k].items;
+            blk += (unsigned)((sets[k].items + bp::LANE_SORT_BLOCK - 1) / bp::LANE_SORT_BLOCK);
+        }
+        plan.count = cnt;
+        plan.blocks = blk;
+        plan.slot = slots_dev + idx;
+        return hipSuccess;
     }
     bool busy() const {
         for (auto& sl : slots) if (sl.active) return true;
@@ -369,6 +431,7 @@ struct Pipeline {
             nw.dev.poly_out = (bp::ge*)poly_out;
             nw.dev.range_mode = range_mode;
             nw.dev.lane_tree = lane_tree ? 1 : 0;
+            BP_RET_ON(plan_sort(nw, head));
             BP_RET_ON(hipEventSynchronize(nw.copied));   // staging slot free again
             host_dev[head] = nw.dev;
             BP_RET_ON(hipMemcpyAsync(slots_dev + head, host_dev + head, sizeof(bp::SlotDev), hipMemcpyHostToDevice, s));
@@ -408,9 +471,7 @@ struct Pipeline {
                     if (st == 0) add(tr, bp::RK_PREP, idx, 0, range_mode ? 2 * B : B, 64);
                 } else if (pass == 2) {
                     if (st == 1) {
-                        unsigned long long it = (range_mode ? B * 2 * n : 0) + (L > 0 ? B * 2 * n : 0) + B * 2 +
-                                                (range_mode == 2 ? B * 7 : 0);   // == stage0_items (device)
-                        add(tr, bp::RK_STAGE0, idx, 0, it, 64);
+                        add(tr, bp::RK_STAGE0, idx, 0, bp::stage0_lanes(B, n, L, range_mode).total, 64);
                     }
                     if (st >= 2 && st <= L) add(tr, bp::RK_ROUND, idx, st - 1, B * 4 * (n >> st), 64);
                     if (st == g.ft) add(tr, bp::RK_FINAL_TERMS, idx, 0, B * 2, 64);
@@ -423,6 +484,10 @@ struct Pipeline {
         bp::launch_terms(tr, slots_dev, G, H, g ? g : h, h, e->dtab, e->two_i, s);
         if (tm) tm->mark(bp::KT_TERMS, true, s);
         BP_RET_ON(hipGetLastError());
+        if (has && plan.count) {   // the new batch's scalars exist now (its RK_PREP ran): order its lanes
+            bp::launch_lane_sort(plan, sort_bins.as<unsigned>(), sort_offs.as<unsigned>(), s);
+            BP_RET_ON(hipGetLastError());
+        }
         for (auto& sl : slots) {
             if (!sl.active) continue;
             if (sl.stage == stages(sl.dev.bv.L_len).fin) sl.active = false;

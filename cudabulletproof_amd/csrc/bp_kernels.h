@@ -66,7 +66,71 @@ struct SlotDev {
     ge* poly_out;         // mode 2, nullable
     int range_mode;       // 0 inner product only, 1 cuda_range_proof_verify, 2 range_proof_verify
     int lane_tree;        // MSM trees reduced by final_task's lane (n <= lane-tree limit), else RK_TREE
+    // Lane orders of the per-lane-scalar item sets (nullable = index order), written by
+    // launch_lane_sort after the batch's challenge tick: the lanes of a wave take items of equal
+    // scalar-mult chain length.  perm0: stage-0 per-lane items; permr[r]: fold round r; perm_ft:
+    // the final terms.
+    uint32_t* perm0;
+    uint32_t* permr[17];
+    uint32_t* perm_ft;
 };
+
+// Stage-0 lane layout (host and device).  stage0_task's items by class — the <sG,G>/<sH,H>
+// terms, IPA fold round 0, t*h / c*Q, the 7 polynomial terms: each class is one call site of
+// the scalar multiplication, so a wave must not mix classes.  For n >= 64 the scalar-uniform
+// items come first (U lanes: the <sG,G> segments, one scalar per n items, then fold round 0, one
+// scalar per n-item half); then the per-lane classes, each in its own wave-aligned lane range
+// (sorted by chain length when SlotDev::perm0 is set): [<sH,H> (n < 64: all MSM terms)]
+// [fold round 0 (n < 64 only)] [t*h, c*Q] [poly terms].
+struct Stage0Lanes {
+    unsigned long long U;
+    unsigned long long off[4], size[4];   // lane offset / items of each per-lane class
+    unsigned long long total;             // region lanes
+    unsigned long long pl;                // per-lane items (perm0 length)
+};
+__host__ __device__ inline Stage0Lanes stage0_lanes(unsigned long long B, int n, int L, int range_mode) {
+    Stage0Lanes z;
+    const unsigned long long msm = range_mode ? B * 2 * n : 0, fold = L > 0 ? B * 2 * n : 0;
+    const bool uni = n >= 64;
+    z.U = uni ? msm / 2 + fold : 0;
+    z.size[0] = uni ? msm / 2 : msm;
+    z.size[1] = uni ? 0 : fold;
+    z.size[2] = B * 2;
+    z.size[3] = range_mode == 2 ? B * 7 : 0;
+    unsigned long long o = z.U, pl = 0;
+    for (int c = 0; c < 4; c++) {
+        z.off[c] = o;
+        o += (z.size[c] + 63) & ~63ull;
+        pl += z.size[c];
+    }
+    z.total = o;
+    z.pl = pl;
+    return z;
+}
+// Fold round r >= 1 runs per-lane scalars when a scalar's 2n' items are fewer than a wave.
+__host__ __device__ inline bool round_per_lane(int n, int r) { return (n >> r) < 64; }
+
+// Counting sort of one batch's per-lane item sets by chain length (see SlotDev::perm0).
+constexpr int MSM_BINS = 513;   // chain lengths 0..512
+
+enum SortSetKind { SS_STAGE0 = 0, SS_ROUND = 1, SS_FT = 2 };
+constexpr int LANE_SORT_SETS = 18;
+constexpr int LANE_SORT_BLOCK = 1024;
+struct LaneSortPlan {
+    int count;
+    int pad;
+    const SlotDev* slot;   // device copy of the batch's slot
+    struct Set {
+        int kind, r;
+        unsigned long long items;
+        uint32_t* perm;
+        unsigned block0;   // first block of this set in the hist / scatter grids
+        unsigned pad;
+    } set[LANE_SORT_SETS];
+    unsigned blocks;
+    int longest_first;
+};
+void launch_lane_sort(const LaneSortPlan& plan, unsigned* bins, unsigned* offs, hipStream_t s);
 
 // A tick's work list (one k_terms launch): region k covers items [begin_k, begin_{k+1}) of one
 // slot at one stage.  RK_TREE (block-level MSM tree; always first, 256-aligned), RK_PREP
@@ -105,7 +169,6 @@ void launch_terms(const RegionList& rl, const SlotDev* slots, const ge* G, const
 // Generic canonical-tree MSM.  perm [m] / bins [MSM_BINS] (nullable): workspace of the
 // counting sort that groups items of equal chain length into the same waves (m >= MSM_SORT_MIN).
 constexpr size_t MSM_SORT_MIN = 4096;
-constexpr int MSM_BINS = 513;
 void launch_msm_points(ge* pts, const fe* scal, const ge* P, size_t m, uint32_t* perm, unsigned* bins,
                        const ge* dtab, hipStream_t s);
 void launch_tree(ge* out, const ge* in, int S, size_t m, hipStream_t s);

@@ -311,19 +311,46 @@ __device__ __forceinline__ void fold_task(const BatchView& bv, const VerifyWs& w
     ws.fold[r & 1][p * (2 * n) + k] = ge_norm_host(t);
 }
 
-// Stage 0: every scalar multiplication that depends only on the proof (contiguous per kind,
-// so a wave's lanes mostly share a scalar):
+// Per-lane class c item j -> stage0_task's item index (perm0 holds, per class range, the
+// items of that class in chain-length order: perm0[pl_base(c) + j]).
+__device__ __forceinline__ size_t stage0_class_item(const SlotDev& sd, int c, size_t j) {
+    const size_t B = sd.bv.B;
+    const int n = sd.bv.n;
+    const size_t nA = sd.range_mode ? B * 2 * n : 0, nB = sd.bv.L_len > 0 ? B * 2 * n : 0;
+    if (c == 0) return n >= 64 ? (j / n) * 2 * n + n + j % n : j;
+    if (c == 1) return nA + j;
+    if (c == 2) return nA + nB + j;
+    return nA + nB + 2 * B + j;
+}
+
+// Stage-0 lane -> stage0_task item, or SIZE_MAX for a padding lane (stage0_lanes).
+__device__ __forceinline__ size_t stage0_item(const SlotDev& sd, size_t l) {
+    const size_t B = sd.bv.B;
+    const int n = sd.bv.n;
+    const Stage0Lanes z = stage0_lanes(B, n, sd.bv.L_len, sd.range_mode);
+    if (l < z.U) {
+        const size_t nG = sd.range_mode ? B * n : 0;
+        if (l < nG) return (l / n) * 2 * n + l % n;     // <sG,G> segment of proof l / n
+        return (sd.range_mode ? B * 2 * n : 0) + (l - nG);
+    }
+    int c = 0;
+    size_t base = 0;   // class c's offset in perm0
+#pragma unroll
+    for (int k = 1; k < 4; k++)
+        if (l >= z.off[k]) { c = k; base += z.size[k - 1]; }
+    const size_t j = l - z.off[c];
+    if (j >= z.size[c]) return SIZE_MAX;
+    return stage0_class_item(sd, c, sd.perm0 ? sd.perm0[base + j] : j);
+}
+
+// Stage 0: every scalar multiplication that depends only on the proof.  Item index space
+// (lanes reach it through stage0_item's class layout):
 //   [0, 2nB)      the two MSMs of calculate_inner_product_point (rp.cu:724, :728):
 //                 segment 2p = <sG, G>, 2p+1 = <sH, H>; Ndev (kernels.cu:26-42)
 //   [.., +2nB)    IPA fold round 0 terms
 //   [.., +2B)     t*h (rp.cu:778-781) and c*Q (crv:255, :268-269), host normalize
 //   [.., +7B)     mode 2: the polynomial identity's g^t, h^taux, V^z^2, g^delta, h^mu, T1^x, T2^x^2
 //                 (rp.cu:442-480), host normalize
-__device__ __forceinline__ size_t stage0_items(const SlotDev& sd) {
-    const size_t B = sd.bv.B;
-    return (sd.range_mode ? B * 2 * sd.bv.n : 0) + (sd.bv.L_len > 0 ? B * 2 * sd.bv.n : 0) + B * 2 +
-           (sd.range_mode == 2 ? B * 7 : 0);
-}
 
 __device__ __forceinline__ void stage0_task(const SlotDev& sd, size_t i, geq* qslot, const ge* __restrict__ G,
                                             const ge* __restrict__ H, const ge* __restrict__ g,
@@ -547,6 +574,115 @@ __device__ __forceinline__ void poly_task(const SlotDev& sd, size_t p) {
     }
 }
 
+// ------------------------------------------------------------------ lane sort (verify)
+// Chain length (sm_ops) of the scalar of item j of a per-lane set, read the way the item's
+// task reads it (stage0_task / fold_task / final_terms_task).  A lane with no work keys 0.
+__device__ __forceinline__ int lane_key(const SlotDev& sd, int kind, int r, size_t j) {
+    const BatchView& bv = sd.bv;
+    const VerifyWs& ws = sd.ws;
+    const size_t B = bv.B;
+    const int n = bv.n, Lr = bv.L_len;
+    fe s;
+    if (kind == SS_STAGE0) {
+        size_t i = stage0_class_item(sd, r, j);
+        const size_t nA = sd.range_mode ? B * 2 * n : 0, nB = Lr > 0 ? B * 2 * n : 0;
+        if (i < nA) {
+            size_t seg = i / n, p = seg >> 1;
+            s = (seg & 1) ? ws.sH[p * n + i % n] : ws.sG[p];
+        } else if (i - nA < nB) {
+            i -= nA;
+            size_t p = i / (2 * n);
+            int grp = (int)(i % (2 * n)) / (n >> 1);
+            s = grp < 2 ? ws.uinv[p * Lr] : ws.u[p * Lr];
+        } else if (i - nA - nB < 2 * B) {
+            i -= nA + nB;
+            bool isC = i & 1;
+            if (!isC && !sd.range_mode) return 0;
+            s = ws.sc[(i >> 1) * 4 + (isC ? 3 : 0)];
+        } else {
+            i -= nA + nB + 2 * B;
+            s = ws.psc[(i / 7) * 8 + i % 7];
+        }
+    } else if (kind == SS_ROUND) {
+        const int np = n >> (r + 1);
+        size_t p = j / (4 * np);
+        int grp = (int)(j % (4 * np)) / np;
+        s = grp < 2 ? ws.uinv[p * Lr + r] : ws.u[p * Lr + r];
+    } else {
+        s = ws.sc[(j >> 1) * 4 + ((j & 1) ? 2 : 1)];
+    }
+    return sm_ops(s);
+}
+
+__device__ __forceinline__ int lane_set_of(const LaneSortPlan& pl, unsigned b, LaneSortPlan::Set& st) {
+    int idx = 0;
+    st = pl.set[0];
+#pragma unroll
+    for (int k = 1; k < LANE_SORT_SETS; k++)
+        if (k < pl.count && b >= pl.set[k].block0) { st = pl.set[k]; idx = k; }
+    return idx;
+}
+
+__global__ __launch_bounds__(LANE_SORT_BLOCK) void k_lane_hist(LaneSortPlan pl, unsigned* bins) {
+    __shared__ unsigned h[OPS_BINS];
+    for (int k = threadIdx.x; k < OPS_BINS; k += LANE_SORT_BLOCK) h[k] = 0;
+    __syncthreads();
+    LaneSortPlan::Set st;
+    const int si = lane_set_of(pl, blockIdx.x, st);
+    const size_t j = (size_t)(blockIdx.x - st.block0) * LANE_SORT_BLOCK + threadIdx.x;
+    if (j < st.items) atomicAdd(&h[lane_key(*pl.slot, st.kind, st.r, j)], 1u);
+    __syncthreads();
+    for (int k = threadIdx.x; k < OPS_BINS; k += LANE_SORT_BLOCK)
+        if (h[k]) atomicAdd(&bins[si * OPS_BINS + k], h[k]);
+}
+
+// Per set (one block each): longest-first exclusive scan of its bins into offs; bins re-zeroed.
+__global__ __launch_bounds__(SCAN_T) void k_lane_scan(unsigned* bins, unsigned* offs, int longest_first) {
+    __shared__ unsigned a[SCAN_T];
+    const int t = threadIdx.x, k = longest_first ? OPS_BINS - 1 - t : t;
+    unsigned* bb = bins + (size_t)blockIdx.x * OPS_BINS;
+    const unsigned v = t < OPS_BINS ? bb[k] : 0u;
+    a[t] = v;
+    __syncthreads();
+    for (int off = 1; off < SCAN_T; off <<= 1) {
+        unsigned x = t >= off ? a[t - off] : 0u;
+        __syncthreads();
+        a[t] += x;
+        __syncthreads();
+    }
+    if (t < OPS_BINS) {
+        offs[(size_t)blockIdx.x * OPS_BINS + k] = a[t] - v;
+        bb[k] = 0;
+    }
+}
+
+__global__ __launch_bounds__(LANE_SORT_BLOCK) void k_lane_scatter(LaneSortPlan pl, unsigned* offs) {
+    __shared__ unsigned cnt[OPS_BINS], base[OPS_BINS];
+    for (int k = threadIdx.x; k < OPS_BINS; k += LANE_SORT_BLOCK) cnt[k] = 0;
+    __syncthreads();
+    LaneSortPlan::Set st;
+    const int si = lane_set_of(pl, blockIdx.x, st);
+    const size_t j = (size_t)(blockIdx.x - st.block0) * LANE_SORT_BLOCK + threadIdx.x;
+    int key = 0;
+    unsigned rank = 0;
+    if (j < st.items) {
+        key = lane_key(*pl.slot, st.kind, st.r, j);
+        rank = atomicAdd(&cnt[key], 1u);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < OPS_BINS; k += LANE_SORT_BLOCK)
+        if (cnt[k]) base[k] = atomicAdd(&offs[si * OPS_BINS + k], cnt[k]);
+    __syncthreads();
+    if (j < st.items) st.perm[base[key] + rank] = (uint32_t)j;
+}
+
+void launch_lane_sort(const LaneSortPlan& plan, unsigned* bins, unsigned* offs, hipStream_t s) {
+    if (!plan.count || !plan.blocks) return;
+    k_lane_hist<<<plan.blocks, LANE_SORT_BLOCK, 0, s>>>(plan, bins);
+    k_lane_scan<<<plan.count, SCAN_T, 0, s>>>(bins, offs, plan.longest_first);
+    k_lane_scatter<<<plan.blocks, LANE_SORT_BLOCK, 0, s>>>(plan, offs);
+}
+
 // One pipeline tick = ONE launch.  Every region is one in-flight batch at its own stage
 // (challenges / stage 0 / MSM trees / fold round r / final terms / final assembly), so a launch
 // carries a whole batch's worth of independent work however deep the batch-level dependency
@@ -591,13 +727,16 @@ __global__ __launch_bounds__(TPB, 4) void k_terms(RegionList rl, const SlotDev* 
         if (sd.range_mode && l < B) prep_range_task(sd.bv, sd.ws, two_i, l, sd.range_mode);
         else prep_ipa_task(sd.bv, sd.ws, sd.range_mode ? l - B : l);
     } else if (rg.kind == RK_STAGE0) {
-        stage0_task(sd, l, &qs[threadIdx.x], G, H, g, h, dtab);
+        const size_t it = stage0_item(sd, l);
+        if (it != SIZE_MAX) stage0_task(sd, it, &qs[threadIdx.x], G, H, g, h, dtab);
     } else if (rg.kind == RK_M3) {
         m3_task(sd, l, &qs[threadIdx.x], dtab);
     } else if (rg.kind == RK_ROUND) {
         const int np = sd.bv.n >> (rg.r + 1);
+        if (const uint32_t* pm = sd.permr[rg.r]) l = pm[l];
         fold_task(sd.bv, sd.ws, rg.r, l / (4 * np), (int)(l % (4 * np)), &qs[threadIdx.x], G, H, dtab);
     } else if (rg.kind == RK_FINAL_TERMS) {
+        if (sd.perm_ft) l = sd.perm_ft[l];
         final_terms_task(sd, l, &qs[threadIdx.x], G, H, dtab);
     } else if (rg.kind == RK_POLY) {
         poly_task(sd, l);

@@ -106,7 +106,7 @@ def proofs(count, n, seed=1):
 def msm_config3(lo, hi, device):
     """SURVEY §8(d) config 3 (BASELINE configs[2]), rows lo..hi-1 of the 2^20-point MSM input:
     points = base points with seed {5} (T = X*Y on the GPU), scalars_i = SHA256("msm-s" || i_le32)
-    with byte 31 &= 0x7F.  tests/golden/msm_2p20.json holds the oracle's result for all 2^20."""
+    with byte 31 &= 0x7F.  tests/golden/msm_2p20.json holds the expected result for all 2^20."""
     sc = bytearray()
     for i in range(lo, hi):
         sc += hashlib.sha256(b"msm-s" + int(i).to_bytes(4, "little")).digest()

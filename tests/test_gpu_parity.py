@@ -156,7 +156,9 @@ def test_batch_verify_matches_reference(bp, golden, n):
 
 
 @pytest.mark.parametrize("n,B,ab_len", [(64, 48, 1), (16, 40, 3), (4, 17, 2), (1, 9, 1), (256, 4, 1), (512, 3, 1),
-                                        (1024, 2, 2)])
+                                        (1024, 2, 2),
+                                        # B >= 64: lanes in chain-length order (the pipeline's lane sort)
+                                        (64, 72, 1), (16, 130, 2), (4, 64, 1)])
 def test_batch_verify_synthetic_vs_oracle(bp, oracle, n, B, ab_len):
     from cudabulletproof_amd import synth
     arrays = synth.proofs(B, n, seed=1000 + n)
@@ -273,12 +275,12 @@ def test_ipa4096_single_call_matches_reference(bp, golden, oracle):
         assert bp.cuda_inner_product_verify(proof, d["P"], G, H, Q) == bool(want)
 
 
-def test_ipa4096_batch_matches_reference(bp, golden, oracle):
+@pytest.mark.parametrize("B", [6, 66])   # 66: lanes in chain-length order (lane sort)
+def test_ipa4096_batch_matches_reference(bp, golden, oracle, B):
     """hipbp_batch_inner_product_verify over a batch of 4096-element IPAs: verdicts and the
     check point equal the reference's; rejected-at-<a,b> proofs leave no check point."""
     import torch
     d, n, G, H, Q = _ipa4096(golden, oracle)
-    B = 6
     dev = torch.device("cuda:0")
     zero_pt = np.zeros((B, 16), np.uint64)
     c = np.stack([d["c_fix"] if p % 3 else d["c_in"] for p in range(B)])
@@ -376,7 +378,8 @@ def test_std_verify_golden_proofs(bp, oracle, golden, n):
     _check_std_vs_oracle(oracle, n, arrays, heads, d["G"], d["H"], d["g"], d["h"], res)
 
 
-@pytest.mark.parametrize("n,B,ab_len", [(64, 20, 1), (16, 9, 2), (1, 5, 1), (2, 3, 1), (256, 2, 1)])
+@pytest.mark.parametrize("n,B,ab_len", [(64, 20, 1), (16, 9, 2), (1, 5, 1), (2, 3, 1), (256, 2, 1), (16, 70, 1),
+                                        (64, 64, 1)])
 def test_std_verify_synthetic_vs_oracle(bp, oracle, n, B, ab_len):
     from cudabulletproof_amd import synth
     arrays = synth.proofs(B, n, seed=500 + n)

@@ -23,3 +23,8 @@ extern "C" __global__ void p_ge_add_zone(ge* o, const ge* p, const geq* q) {
     qs[threadIdx.x] = q[threadIdx.x];
     o[threadIdx.x] = ge_add_qp<true>(p[threadIdx.x], &qs[threadIdx.x], true);
 }
+extern "C" __global__ void p_ge_add_sel_zone(ge* o, const ge* p, const geq* q, const int* u) {
+    __shared__ geq qs[256];
+    qs[threadIdx.x] = q[threadIdx.x];
+    o[threadIdx.x] = ge_add_sel<true, true>(p[threadIdx.x], &qs[threadIdx.x], u[threadIdx.x] != 0);
+}
