@@ -407,10 +407,12 @@ def main():
     ipa = None
     if not args.no_ipa and rank == 0:   # configs[3]: single-GPU
         ipa = ipa_leg(args, dev)
+        ipa["n_gpus"] = 1
 
     prove = None
     if not args.no_prove and rank == 0:
         prove = prove_leg(args, dev)
+        prove["n_gpus"] = 1
 
 
     if rank == 0:
@@ -429,6 +431,7 @@ def main():
         }
         print(json.dumps(line), flush=True)
     if world > 1:
+        dist.barrier()   # the other ranks wait out rank 0's single-GPU legs, then all leave together
         dist.destroy_process_group()
 
 

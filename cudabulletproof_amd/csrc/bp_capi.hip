@@ -130,7 +130,7 @@ struct Engine {
     Buf h2d[8], scratch[8];
     // prover workspaces (hipbp_batch_generate_range_proof), one per stream so batches on
     // different streams overlap (one batch's latency-bound stages under another's term launch)
-    struct ProverBufs { Buf b[17]; };
+    struct ProverBufs { Buf b[19]; };
     std::map<hipStream_t, ProverBufs*> provers;
     // pinned host staging for the single-proof entry points (a pageable source of an
     // async copy must outlive the copy; this one does, and the stream is synced after use)
@@ -724,12 +724,19 @@ int hipbp_batch_generate_range_proof(const hipbp_prove_input* in, const ge25519*
     Engine::ProverBufs*& pb = e->provers[s];
     if (!pb) pb = new Engine::ProverBufs();
     Buf* prv = pb->b;
-    for (int i = 0; i < 17; i++) BP_RET_ON(prv[i].need(sz[i]));
+    // terms0's heavy-list sort (HIPBP_PROVE_SORT=0 turns it off, for A/B runs)
+    static const bool psort = getenv("HIPBP_PROVE_SORT") ? atoi(getenv("HIPBP_PROVE_SORT")) != 0 : true;
+    const int nbuf = psort ? 19 : 17;
+    size_t sz2[19];
+    for (int i = 0; i < 19; i++) sz2[i] = i < 17 ? sz[i] : 0;
+    if (psort) { sz2[17] = cap * sizeof(uint32_t); sz2[18] = bp::MSM_BINS * sizeof(unsigned); }
+    for (int i = 0; i < nbuf; i++) BP_RET_ON(prv[i].need(sz2[i]));
     bp::ProveWs w{prv[0].as<bp::fe>(), prv[1].as<bp::ge>(), prv[2].as<bp::ge>(), prv[3].as<bp::ge>(),
                   prv[4].as<bp::fe>(), prv[5].as<bp::fe>(), prv[6].as<bp::ge>(), prv[7].as<bp::fe>(),
                   prv[8].as<bp::fe>(), prv[9].as<bp::fe>(), prv[10].as<bp::fe>(), prv[11].as<bp::ge>(),
                   prv[12].as<bp::fe>(), prv[13].as<uint8_t>(), prv[14].as<uint32_t>(), prv[15].as<unsigned>(), cap,
-                  prv[16].as<bp::ge>()};
+                  prv[16].as<bp::ge>(), psort ? prv[17].as<uint32_t>() : nullptr,
+                  psort ? prv[18].as<unsigned>() : nullptr};
     auto run = [&](int stage, int r) {
         bp::launch_prove(stage, r, pin, w, po, (const bp::ge*)G, (const bp::ge*)H, (const bp::ge*)g,
                          (const bp::ge*)h, e->dtab, e->two_i, s);

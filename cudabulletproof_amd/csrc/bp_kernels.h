@@ -172,6 +172,7 @@ constexpr size_t MSM_SORT_MIN = 4096;
 void launch_msm_points(ge* pts, const fe* scal, const ge* P, size_t m, uint32_t* perm, unsigned* bins,
                        const ge* dtab, hipStream_t s);
 void launch_tree(ge* out, const ge* in, int S, size_t m, hipStream_t s);
+void launch_ops_scan(unsigned* bins, int longest_first, hipStream_t s);   // bins -> start offsets
 
 
 
@@ -215,6 +216,8 @@ struct ProveWs {
     size_t cap;
     ge* ctab;     // [2n]      N(sm(tobytes(sub(0, 1)), H_i)) | N(sm(1, G_i)): the aR_i H_i term where
                   //           aL_i = 0 and the aL_i G_i term where aL_i = 1, once per batch
+    uint32_t* slist;  // [cap]  terms0's heavy list in chain-length order (nullable: list order)
+    unsigned* sbins;  // [MSM_BINS] its counting-sort bins
 };
 enum ProveStage { PS_PREP = 0, PS_TERMS0, PS_CHAIN0, PS_COMMIT, PS_TERMS1, PS_TX, PS_RTERMS, PS_RCHAIN, PS_ROUND,
                   PS_FINAL };

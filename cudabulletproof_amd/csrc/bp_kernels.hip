@@ -59,11 +59,6 @@ __global__ __launch_bounds__(TPB, 3) void k_msm_points(ge* pts, const fe* __rest
     pts[i] = ge_norm_dev(r);
 }
 
-// Length of ge25519_scalarmult's add chain past the leading zeros: the per-lane loop runs
-// (256 - clz) doublings + popcount adds, and a wave runs as long as its longest lane.
-__device__ __forceinline__ int sm_ops(const fe& s) {
-    return (256 - fe_clz256(s)) + __popcll(s.v[0]) + __popcll(s.v[1]) + __popcll(s.v[2]) + __popcll(s.v[3]);
-}
 constexpr int OPS_BINS = MSM_BINS;
 
 __global__ void k_ops_zero(unsigned* bins) {
@@ -121,6 +116,10 @@ __global__ __launch_bounds__(SCAN_T) void k_ops_scatter(uint32_t* perm, unsigned
         if (cnt[k]) base[k] = atomicAdd(&offs[k], cnt[k]);
     __syncthreads();
     if (i < n) perm[base[key] + rank] = (uint32_t)i;
+}
+
+void launch_ops_scan(unsigned* bins, int longest_first, hipStream_t s) {
+    k_ops_scan<<<1, SCAN_T, 0, s>>>(bins, longest_first);
 }
 
 void launch_msm_points(ge* pts, const fe* scal, const ge* P, size_t m, uint32_t* perm, unsigned* bins,

@@ -131,6 +131,46 @@ __global__ __launch_bounds__(TPB) void k_prove_prep(ProveIn in, ProveWs ws, cons
     });
 }
 
+// ---------------------------------------------------------------- terms0 lane sort
+// The heavy items are random 255-bit scalars (sL, sR, gamma): a wave runs as long as its
+// longest chain, so the heavy list is counting-sorted by chain length (sm_ops) into slist,
+// longest first (the same scheme as the MSM's k_ops_*).
+constexpr int SORT_T = 1024;
+__global__ __launch_bounds__(TPB) void k_prove_sort_hist(ProveIn in, ProveWs ws) {
+    __shared__ unsigned hb[MSM_BINS];
+    for (int k = threadIdx.x; k < MSM_BINS; k += TPB) hb[k] = 0;
+    __syncthreads();
+    const size_t i = gid(), per = 4 * (size_t)in.n + 4;
+    if (i < ws.cnt[0]) {
+        const uint32_t id = ws.list[i];
+        atomicAdd(&hb[sm_ops(terms0_scalar(in, ws, id / per, (int)(id % per)))], 1u);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < MSM_BINS; k += TPB)
+        if (hb[k]) atomicAdd(&ws.sbins[k], hb[k]);
+}
+
+__global__ __launch_bounds__(SORT_T) void k_prove_sort_scatter(ProveIn in, ProveWs ws) {
+    __shared__ unsigned cnt[MSM_BINS], base[MSM_BINS];
+    for (int k = threadIdx.x; k < MSM_BINS; k += SORT_T) cnt[k] = 0;
+    __syncthreads();
+    const size_t i = (size_t)blockIdx.x * SORT_T + threadIdx.x, per = 4 * (size_t)in.n + 4;
+    int key = 0;
+    unsigned rank = 0;
+    uint32_t id = 0;
+    const bool live = i < ws.cnt[0];
+    if (live) {
+        id = ws.list[i];
+        key = sm_ops(terms0_scalar(in, ws, id / per, (int)(id % per)));
+        rank = atomicAdd(&cnt[key], 1u);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < MSM_BINS; k += SORT_T)
+        if (cnt[k]) base[k] = atomicAdd(&ws.sbins[k], cnt[k]);
+    __syncthreads();
+    if (live) ws.slist[base[key] + rank] = id;
+}
+
 // ---------------------------------------------------------------- PS_TERMS0
 // item k of proof p (4n+4 items): k < 4n the MSM term ps[k] * (G|H)[k % n], host-normalized
 // (vectors.cu:204-206); then g^v, h^gamma (pedersen_commit, rp.cu:277-297: normalized) and the
@@ -146,7 +186,11 @@ __global__ __launch_bounds__(TPB, 3) void k_prove_terms0(ProveIn in, ProveWs ws,
     // queued items
     const size_t i = gid();
     uint32_t id = 0;
-    if (i >= 2 * (size_t)n && !next_item(ws, i - 2 * n, id)) return;
+    if (i >= 2 * (size_t)n) {
+        const size_t q = i - 2 * n;
+        if (ws.slist && q < ws.cnt[0]) id = ws.slist[q];
+        else if (!next_item(ws, q, id)) return;
+    }
     size_t p = id / per;
     int k = (int)(id % per);
     // operands are selected per lane and ONE scalar-mult follows: two call sites in one wave
@@ -462,6 +506,13 @@ void launch_prove(int stage, int r, const ProveIn& in, const ProveWs& ws, const 
             k_prove_prep<<<nblk(B), TPB, 0, s>>>(in, ws, dtab);
             break;
         case PS_TERMS0:
+            if (ws.slist) {   // heavy list -> chain-length order (the list length is on the device)
+                const size_t cap = ws.cap;
+                (void)hipMemsetAsync(ws.sbins, 0, MSM_BINS * sizeof(unsigned), s);
+                k_prove_sort_hist<<<nblk(cap), TPB, 0, s>>>(in, ws);
+                launch_ops_scan(ws.sbins, 1, s);
+                k_prove_sort_scatter<<<(unsigned)((cap + SORT_T - 1) / SORT_T), SORT_T, 0, s>>>(in, ws);
+            }
             k_prove_terms0<<<nblk(B * (4 * (size_t)n + 4) + 2 * n), TPB, 0, s>>>(in, ws, G, H, g, h, dtab);
             break;
         case PS_CHAIN0: k_prove_chain0<<<nblk(B * 4), TPB, 0, s>>>(in, ws); break;

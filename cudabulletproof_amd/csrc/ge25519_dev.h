@@ -95,6 +95,12 @@ BP_DEV int fe_clz256(const fe& s) {
 
 BP_DEV ge ld_ge(const ge* p) { return *p; }
 
+// Length of ge25519_scalarmult's add chain past the leading zeros: the per-lane loop runs
+// (256 - clz) doublings + popcount adds, and a wave runs as long as its longest lane.
+BP_DEV int sm_ops(const fe& s) {
+    return (256 - fe_clz256(s)) + __popcll(s.v[0]) + __popcll(s.v[1]) + __popcll(s.v[2]) + __popcll(s.v[3]);
+}
+
 // q-side operand access.  QLDS = true: this lane's LDS slot, read at the point of use (the
 // empty asm with a memory clobber stops the compiler from hoisting the loads and keeping all
 // of q in VGPRs, which would cost occupancy in the throughput kernels).  QLDS = false: a

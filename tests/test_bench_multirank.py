@@ -13,6 +13,10 @@ SMALL = ["--steps", "2", "--warmup", "1", "--batch", "128", "--msm-log2", "12", 
          "--no-prove"]
 
 
+# rank 0's single-GPU legs (IPA, prover) while the other rank waits at the closing barrier
+LEGS = ["--ipa-n", "256", "--ipa-batch", "8", "--ipa-steps", "2", "--prove-batch", "256", "--prove-steps", "1"]
+
+
 def _line(out):
     return json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
 
@@ -25,7 +29,7 @@ def test_bench_two_ranks_rehearsal_matches_one_rank():
     assert one.returncode == 0, one.stderr[-2000:]
     two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                           "--master-addr", "127.0.0.1", "--master-port", "29561", os.path.join(ROOT, "bench.py"),
-                          "--gpus", "2", "--rehearse"] + SMALL, capture_output=True, text=True, timeout=600, cwd=ROOT,
+                          "--gpus", "2", "--rehearse"] + SMALL[:-2] + LEGS, capture_output=True, text=True, timeout=600, cwd=ROOT,
                          env=env)
     assert two.returncode == 0, two.stderr[-2000:]
     l1, l2 = _line(one.stdout), _line(two.stdout)
@@ -33,3 +37,4 @@ def test_bench_two_ranks_rehearsal_matches_one_rank():
     assert l2["msm"]["scaling"] == "strong" and l2["scaling"] == "weak"
     assert l1["msm"]["result_sha256"] == l2["msm"]["result_sha256"]
     assert l2["config"]["passes_in_warmup_batch"] >= l1["config"]["passes_in_warmup_batch"]
+    assert l2["ipa"]["n_gpus"] == 1 and l2["prove"]["n_gpus"] == 1 and l2["prove"]["valid"] == 256
