@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--no-ipa", action="store_true")
     ap.add_argument("--prove-batch", type=int, default=65536, help="proofs per generate_range_proof batch")
     ap.add_argument("--prove-steps", type=int, default=4)
+    ap.add_argument("--prove-streams", type=int, default=2, help="HIP streams prover batches rotate over")
     ap.add_argument("--no-prove", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -266,20 +267,22 @@ def prove_leg(args, dev):
     # other batch's term launches (each stream has its own prover workspace in the engine)
     # (different priorities: HIP maps streams onto at most GPU_MAX_HW_QUEUES hardware queues and two
     # same-priority streams created after the verify legs' streams can share one, which serializes them)
-    streams = [torch.cuda.Stream(dev, priority=0), torch.cuda.Stream(dev, priority=-1)]
+    lo, hi = torch.cuda.Stream.priority_range()
+    ns = max(1, args.prove_streams)
+    streams = [torch.cuda.Stream(dev, priority=max(hi, lo - k)) for k in range(ns)]
     torch.cuda.synchronize(dev)
     run = lambda k: bp.batch_generate_range_proof(n, pi["v"], pi["gamma"], pi["sL"], pi["sR"], pi["rnd"], Gd, Hd,
-                                                  gd, hd, stream=streams[k % 2])
-    outs = [run(0), run(1)]
+                                                  gd, hd, stream=streams[k % ns])
+    outs = [run(k) for k in range(ns)]
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(args.prove_steps):
-        outs[k % 2] = run(k)
+        outs[k % ns] = run(k)
     torch.cuda.synchronize(dev)
     dt = (time.perf_counter() - t0) / args.prove_steps
-    same = all(torch.equal(outs[0][k], outs[1][k]) for k in ("A", "S", "T1", "L", "R"))
+    same = all(torch.equal(outs[0][k], outs[-1][k]) for k in ("A", "S", "T1", "L", "R"))
     return {"metric": f"{n}-bit range proofs generated/sec", "value": B / dt, "unit": "proofs/s", "batch": B,
-            "streams": 2, "ms_per_batch": dt * 1e3, "valid": int(outs[0]["valid"].sum().item()),
+            "streams": ns, "ms_per_batch": dt * 1e3, "valid": int(outs[0]["valid"].sum().item()),
             "deterministic_across_streams": same,
             "semantics": "generate_range_proof + inner_product_prove + fix_inner_product_proof (rp.cu:1159)"}
 
