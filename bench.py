@@ -207,15 +207,36 @@ def msm_leg(args, dev, world, rank, T):
     digest = hashlib.sha256(res.cpu().numpy().tobytes()).hexdigest()[:16]
     golden_ok = None   # tests/golden/msm_2p20.json: the CPU restatement's result for the 2^20 inputs
     gpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden", "msm_2p20.json")
+    gold = None
     if os.path.exists(gpath):
         with open(gpath) as f:
             gold = json.load(f)
         if gold["n"] == nm:
             golden_ok = digest == gold["digest"]
+        else:
+            gold = None
+    pip = None
+    if world == 1:   # the labelled alternative: Pippenger window 12 on the same inputs, one GPU
+        import cudabulletproof_amd as bp
+        out = torch.zeros(16, dtype=torch.int64, device=dev)
+        bp.msm_pippenger(out, scd, ptd, 12)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            bp.msm_pippenger(out, scd, ptd, 12)
+        torch.cuda.synchronize(dev)
+        pdt = (time.perf_counter() - t1) / reps
+        pd = hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest()[:16]
+        pip = {"metric": "MSM points/sec (Pippenger, window 12)", "value": nm / pdt, "unit": "points/s",
+               "ms_per_msm": pdt * 1e3, "window_bits": 12, "result_sha256": pd,
+               "matches_oracle_golden": (pd == gold["pippenger_w12"]["digest"]) if gold else None,
+               "semantics": "labelled alternative (hipbp_msm_pippenger): bucket algorithm over the reference's "
+                            "arithmetic, bit-exact with oracle/ orc_msm_pippenger, NOT the reference's MSM bits "
+                            "(non-associative arithmetic; the graded MSM is the canonical-tree leg above)"}
     return {"metric": "MSM points/sec", "value": nm / mdt, "unit": "points/s", "points": nm,
             "ms_per_msm": mdt * 1e3, "n_gpus": world, "scaling": "strong" if world > 1 else None,
             "semantics": "canonical-tree per-point double-and-add (SURVEY A9); shards + all_gather + tree at N>1",
-            "result_sha256": digest, "matches_oracle_golden": golden_ok}
+            "result_sha256": digest, "matches_oracle_golden": golden_ok, "pippenger": pip}
 
 
 def ipa_leg(args, dev):

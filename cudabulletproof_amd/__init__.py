@@ -23,7 +23,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB_PATH = os.path.join(HERE, "libcudabulletproof_hip.so")
 CSRC = os.path.join(HERE, "csrc")
-SOURCES = ["bp_kernels.hip", "bp_prove.hip", "bp_capi.hip"]
+SOURCES = ["bp_kernels.hip", "bp_prove.hip", "bp_pippenger.hip", "bp_capi.hip"]
 
 _lib = None
 
@@ -96,6 +96,7 @@ EXPORTS = [
     "cuda_benchmark_multi_scalar_mul", "cuda_benchmark_inner_product", "cuda_benchmark_field_operations",
     "cuda_benchmark_range_proof", "hipbp_last_error", "hipbp_device_count", "hipbp_batch_range_proof_verify",
     "hipbp_batch_range_proof_verify_std", "hipbp_batch_inner_product_verify", "hipbp_batch_generate_range_proof", "hipbp_msm",
+    "hipbp_msm_pippenger",
     "hipbp_point_tree", "hipbp_field_op", "hipbp_sync", "hipbp_timing_enable",
     "hipbp_timing_collect", "hipbp_kernel_count", "hipbp_kernel_name", "hipbp_pipeline_create",
     "hipbp_pipeline_push", "hipbp_pipeline_flush", "hipbp_pipeline_depth", "hipbp_pipeline_destroy",
@@ -121,6 +122,7 @@ def lib():
             getattr(L, f).restype = ctypes.c_bool
         for f in ("hipbp_batch_range_proof_verify", "hipbp_batch_range_proof_verify_std",
                   "hipbp_batch_inner_product_verify", "hipbp_batch_generate_range_proof", "hipbp_msm",
+                  "hipbp_msm_pippenger",
                   "hipbp_point_tree",
                   "hipbp_field_op", "hipbp_sync", "hipbp_device_count"):
             getattr(L, f).restype = ctypes.c_int
@@ -392,6 +394,13 @@ def msm(result, scalars, points, stream=None):
     """Canonical-tree MSM on CUDA tensors: result (16,), scalars (n,4), points (n,16)."""
     _chk(lib().hipbp_msm(_c(result.data_ptr()), _c(scalars.data_ptr()), _c(points.data_ptr()),
                          _sz(points.shape[0]), _stream_ptr(stream)))
+
+
+def msm_pippenger(result, scalars, points, window_bits=12, stream=None):
+    """Pippenger bucket MSM on CUDA tensors (labelled alternative: not the reference's MSM bits,
+    see include/cudabulletproof_hip.h)."""
+    _chk(lib().hipbp_msm_pippenger(_c(result.data_ptr()), _c(scalars.data_ptr()), _c(points.data_ptr()),
+                                   _sz(points.shape[0]), ctypes.c_int(window_bits), _stream_ptr(stream)))
 
 
 def point_tree(result, points, stream=None):

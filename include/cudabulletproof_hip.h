@@ -195,6 +195,16 @@ int hipbp_batch_generate_range_proof(const hipbp_prove_input* in, const ge25519*
 
 /* Canonical-tree MSM on device buffers. */
 int hipbp_msm(ge25519* result, const fe25519* scalars, const ge25519* points, size_t n, void* stream);
+
+/* Pippenger bucket MSM with window_bits-bit windows (4..12; BASELINE configs[2] names 12), over
+ * the same fe25519/ge25519 arithmetic, on device buffers.  A LABELLED ALTERNATIVE, not a drop-in
+ * for cuda_point_vector_multi_scalar_mul: the reference's MSM bits come from per-point
+ * double-and-add + the canonical tree (hipbp_msm), and this arithmetic is not associative, so a
+ * bucket regrouping yields different bits.  Its own result is fixed (stable bucket order, fixed
+ * trees) and equals the C restatement oracle/bp_oracle.c orc_msm_pippenger.  Synchronizes the
+ * stream once (the bucket-tree depth).  No reference counterpart. */
+int hipbp_msm_pippenger(ge25519* result, const fe25519* scalars, const ge25519* points, size_t n,
+                        int window_bits, void* stream);
 /* Canonical tree over n device points: for stride 1, 2, 4, ...: T[i] = Ndev(T[i] + T[i+stride])
  * for i % (2 stride) == 0 and i + stride < n; result = T[0] (the reduction half of
  * cuda_bulletproof_kernels.cu:45-115).  hipbp_msm = this tree over the per-point

@@ -313,6 +313,77 @@ void orc_point_tree(orc_ge* r, const orc_ge* P, size_t n) {
     *r = T[0];
     free(T);
 }
+/* Pippenger with c-bit windows (4 <= c <= 16), W = ceil(256/c) windows, NB = 2^c buckets,
+ * chunks of M = 16 buckets.  No normalization anywhere; Id = ge25519_0 (curve25519_ops.cu:318);
+ * add = ge25519_add; smul = ge25519_scalarmult on the scalar's raw LE bytes.
+ *   digit_w(i) = bits [c w, c w + c) of s_i (raw limbs)
+ *   B_{w,b}  = pairwise tree over the points with digit b, in index order (level s = 1, 2, 4, ...:
+ *              T[j] = add(T[j], T[j+s]) for j % 2s == 0, j + s < len); Id when the bucket is empty
+ *   chunk k of window w (buckets kM .. kM+M-1): R = S = B_{kM+M-1}; for j = M-2 .. 1:
+ *              R = add(R, B_{kM+j}); S = add(S, R); then R = add(R, B_{kM});
+ *              V_{w,k} = add(S, smul(kM, R))
+ *   S_w      = pairwise tree over V_{w,0..NB/M-1}
+ *   T = S_{W-1}; for w = W-2 .. 0: c times T = add(T, T); T = add(T, S_w).  Result T. */
+static void tree_inplace(orc_ge* T, size_t n) {
+    for (size_t st = 1; st < n; st *= 2)
+        for (size_t i = 0; i + st < n; i += 2 * st) orc_ge_add(&T[i], &T[i], &T[i + st]);
+}
+void orc_msm_pippenger(orc_ge* r, const orc_fe* s, const orc_ge* P, size_t n, int c) {
+    const int W = (256 + c - 1) / c, M = 16;
+    const size_t NB = (size_t)1 << c, NC = NB / M;
+    orc_ge* Bk = (orc_ge*)malloc(NB * sizeof(orc_ge));
+    orc_ge* V = (orc_ge*)malloc(NC * sizeof(orc_ge));
+    orc_ge* Sw = (orc_ge*)malloc(W * sizeof(orc_ge));
+    orc_ge* tmp = (orc_ge*)malloc((n ? n : 1) * sizeof(orc_ge));
+    uint32_t* dig = (uint32_t*)malloc((n ? n : 1) * sizeof(uint32_t));
+    size_t* cnt = (size_t*)malloc((NB + 1) * sizeof(size_t));
+    size_t* pos = (size_t*)malloc(NB * sizeof(size_t));
+    for (int w = 0; w < W; w++) {
+        for (size_t i = 0; i < n; i++) {
+            int lo = c * w;
+            uint32_t d = 0;
+            for (int b = 0; b < c && lo + b < 256; b++)
+                d |= (uint32_t)((s[i].v[(lo + b) >> 6] >> ((lo + b) & 63)) & 1) << b;
+            dig[i] = d;
+        }
+        /* stable counting sort of the points by digit: each bucket's points in index order */
+        memset(cnt, 0, (NB + 1) * sizeof(size_t));
+        for (size_t i = 0; i < n; i++) cnt[dig[i] + 1]++;
+        for (size_t b = 0; b < NB; b++) cnt[b + 1] += cnt[b];
+        memcpy(pos, cnt, NB * sizeof(size_t));
+        for (size_t i = 0; i < n; i++) tmp[pos[dig[i]]++] = P[i];
+        for (size_t b = 0; b < NB; b++) {
+            size_t len = cnt[b + 1] - cnt[b];
+            if (!len) { orc_ge_zero(&Bk[b]); continue; }
+            tree_inplace(tmp + cnt[b], len);
+            Bk[b] = tmp[cnt[b]];
+        }
+        for (size_t k = 0; k < NC; k++) {
+            const orc_ge* Bc = Bk + k * M;
+            orc_ge R = Bc[M - 1], S = Bc[M - 1], sm;
+            for (int j = M - 2; j >= 1; j--) {
+                orc_ge_add(&R, &R, &Bc[j]);
+                orc_ge_add(&S, &S, &R);
+            }
+            orc_ge_add(&R, &R, &Bc[0]);
+            uint8_t kb[32] = {0};
+            uint64_t km = (uint64_t)k * M;
+            for (int b = 0; b < 8; b++) kb[b] = (uint8_t)(km >> (8 * b));
+            orc_ge_scalarmult(&sm, kb, &R);
+            orc_ge_add(&V[k], &S, &sm);
+        }
+        tree_inplace(V, NC);
+        Sw[w] = V[0];
+    }
+    orc_ge T = Sw[W - 1];
+    for (int w = W - 2; w >= 0; w--) {
+        for (int d = 0; d < c; d++) orc_ge_add(&T, &T, &T);
+        orc_ge_add(&T, &T, &Sw[w]);
+    }
+    *r = T;
+    free(Bk); free(V); free(Sw); free(tmp); free(dig); free(cnt); free(pos);
+}
+
 /* bulletproof_vectors.cu:189-224 : sequential, host bytes and host normalize */
 void orc_msm_cpu(orc_ge* r, const orc_fe* s, const orc_ge* P, size_t n) {
     orc_ge acc;

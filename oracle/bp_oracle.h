@@ -43,6 +43,11 @@ void orc_ge_normalize_dev(orc_ge* p);
 void orc_msm_canon(orc_ge* r, const orc_fe* s, const orc_ge* P, size_t n);   /* GPU MSM semantics (A9) */
 void orc_point_tree(orc_ge* r, const orc_ge* P, size_t n);                   /* the A9 tree alone */
 void orc_msm_cpu(orc_ge* r, const orc_fe* s, const orc_ge* P, size_t n);     /* vectors.cu:189 (A11) */
+/* Pippenger bucket MSM over the reference's arithmetic (BASELINE configs[2]'s "window=12";
+ * a labelled alternative — not the reference's MSM bits, which come from per-point
+ * double-and-add + the A9 tree, and this arithmetic is not associative).  The algorithm this
+ * restates exactly (hipbp_msm_pippenger): see bp_oracle.c. */
+void orc_msm_pippenger(orc_ge* r, const orc_fe* s, const orc_ge* P, size_t n, int c);
 void orc_inner_product(orc_fe* r, const orc_fe* a, const orc_fe* b, size_t n); /* vectors.cu:101 */
 void orc_ip_gpu(orc_fe* r, const orc_fe* a, const orc_fe* b, size_t n);        /* cuda_inner_product.cu:97 */
 void orc_ip_gpu_shared(orc_fe* r, const orc_fe* a, const orc_fe* b, size_t n); /* cuda_inner_product.cu:185 */

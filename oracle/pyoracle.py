@@ -132,6 +132,13 @@ class Oracle(_Lib):
         self.f("point_tree")(_p(r), _p(P), _sz(len(P)))
         return r
 
+    def msm_pippenger(self, s, P, c=12):
+        r = ge()
+        s = np.ascontiguousarray(s, np.uint64)
+        P = np.ascontiguousarray(P, np.uint64)
+        self.f("msm_pippenger")(_p(r), _p(s), _p(P), _sz(len(P)), ctypes.c_int(c))
+        return r
+
     def msm_cpu(self, s, P):
         r = ge()
         s = np.ascontiguousarray(s, np.uint64)

@@ -11,6 +11,10 @@ combined by the oracle's point_tree: the same bits as one oracle.msm_canon over 
 (the 4096-point survey digest, test_msm_4096_survey_digest, pins that oracle to the reference).
 
     python tests/golden/make_msm_2p20.py      # ~1 min on 8 cores -> tests/golden/msm_2p20.json
+
+It also records the Pippenger (window 12) result of the same inputs from orc_msm_pippenger: the
+labelled alternative of include/cudabulletproof_hip.h hipbp_msm_pippenger (not the reference's
+MSM bits; pinned to the C restatement of the bucket algorithm only).
 """
 import hashlib
 import json
@@ -45,17 +49,27 @@ def _shard(k):
     return O.msm_canon(s, P)
 
 
+def _pippenger(c):
+    from oracle import pyoracle
+    O = pyoracle.Oracle()
+    n = 1 << LOG2
+    return O.msm_pippenger(scalars(n), O.base_points(n, 5), c)
+
+
 def main():
     from oracle import pyoracle
     O = pyoracle.Oracle()
-    with mp.Pool(SHARDS) as pool:
+    with mp.Pool(SHARDS + 1) as pool:
+        pip = pool.apply_async(_pippenger, (12,))   # the labelled alternative (orc_msm_pippenger, c = 12)
         roots = pool.map(_shard, range(SHARDS))
+        pip = pip.get()
     roots = np.stack(roots)
     res = O.point_tree(roots)
     d8 = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()[:16]
     out = {"n": 1 << LOG2, "points": "base_points(seed {5})", "scalars": "SHA256('msm-s'||i_le32), byte31&=0x7F",
            "digest": d8(res), "result": [int(x) for x in res],
-           "shard_log2": LOG2 - 3, "shard_roots": [[int(x) for x in r] for r in roots]}
+           "shard_log2": LOG2 - 3, "shard_roots": [[int(x) for x in r] for r in roots],
+           "pippenger_w12": {"digest": d8(pip), "result": [int(x) for x in pip]}}
     with open(os.path.join(HERE, "msm_2p20.json"), "w") as f:
         json.dump(out, f, indent=1)
     print("digest", out["digest"])

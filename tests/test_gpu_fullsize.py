@@ -95,3 +95,18 @@ def test_batch_2p16_tiled_verify(bp, oracle):
         assert np.array_equal(P[0, p], Pr), p
         if okr:
             assert np.array_equal(chk[0, p], chkr), p
+
+
+def test_msm_pippenger_2p20_matches_oracle(bp, oracle):
+    """hipbp_msm_pippenger (window 12, the labelled alternative) on the same 2^20 inputs equals
+    orc_msm_pippenger's result (tests/golden/msm_2p20.json)."""
+    import torch
+    with open(os.path.join(GOLDEN, "msm_2p20.json")) as f:
+        gold = json.load(f)
+    s, P = _msm_inputs(oracle, gold["n"])
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    out = torch.zeros(16, dtype=torch.int64, device=dev)
+    bp.msm_pippenger(out, T(s), T(P), 12)
+    torch.cuda.synchronize()
+    assert [int(x) for x in out.cpu().numpy().view(np.uint64)] == gold["pippenger_w12"]["result"]

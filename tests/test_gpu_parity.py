@@ -582,3 +582,33 @@ def test_sq_matches_mul(bp, oracle):
     got = r.cpu().numpy().view(np.uint64)
     for i in range(0, len(x), 13):
         assert np.array_equal(got[i], oracle.fe_mul(x[i], x[i])), i
+
+
+# ----------------------------------------------------------------------------- Pippenger (labelled alternative)
+@pytest.mark.parametrize("n,c", [(1, 12), (2, 4), (17, 12), (300, 12), (1000, 8), (777, 4), (20000, 8), (4096, 12)])
+def test_msm_pippenger_vs_oracle(bp, oracle, n, c):
+    """hipbp_msm_pippenger == orc_msm_pippenger (the bucket algorithm restated in C): zero and short
+    scalars (empty / crowded buckets), odd bucket sizes, every window width class."""
+    import torch
+    rng = np.random.default_rng(n * 31 + c)
+    P = oracle.base_points(n, 9)
+    s = rand_fe(rng, n)
+    s[::7] = 0
+    s[1::5, 1:] = 0
+    if n > 100:
+        s[3::11] = s[3]                          # a crowded bucket in every window
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    out = torch.zeros(16, dtype=torch.int64, device=dev)
+    bp.msm_pippenger(out, T(s), T(P), c)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint64), oracle.msm_pippenger(s, P, c))
+
+
+def test_msm_pippenger_rejects_bad_window(bp):
+    import torch
+    dev = torch.device("cuda:0")
+    z = torch.zeros(4, 16, dtype=torch.int64, device=dev)
+    with pytest.raises(bp.BulletproofError):
+        bp.msm_pippenger(torch.zeros(16, dtype=torch.int64, device=dev), torch.zeros(4, 4, dtype=torch.int64,
+                                                                                      device=dev), z, 13)

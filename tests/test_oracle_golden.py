@@ -172,3 +172,49 @@ def test_msm_2p20_golden_consistent(oracle):
     roots = np.array(gold["shard_roots"], np.uint64)
     assert roots.shape == (gold["n"] >> gold["shard_log2"], 16)
     assert [int(x) for x in oracle.point_tree(roots)] == gold["result"]
+
+
+def test_pippenger_oracle_small_cases(oracle):
+    """orc_msm_pippenger on tiny inputs against a direct Python statement of the same algorithm."""
+    rng = np.random.default_rng(3)
+    for n, c in ((1, 4), (5, 4), (9, 5)):
+        P = oracle.base_points(n, 4)
+        s = rng.integers(0, 2**64, size=(n, 4), dtype=np.uint64)
+        s[0] = 0
+        W, M = (256 + c - 1) // c, 16
+        NB = 1 << c
+        ident = np.zeros(16, np.uint64)
+        ident[4] = ident[8] = 1
+        add = oracle.ge_add
+
+        def tree(L):
+            L = list(L)
+            st = 1
+            while st < len(L):
+                for i in range(0, len(L) - st, 2 * st):
+                    L[i] = add(L[i], L[i + st])
+                st *= 2
+            return L[0]
+
+        def digit(i, w):
+            v = int(s[i, 0]) | int(s[i, 1]) << 64 | int(s[i, 2]) << 128 | int(s[i, 3]) << 192
+            return (v >> (c * w)) & (NB - 1)
+        Sw = []
+        for w in range(W):
+            B = [tree([P[i] for i in range(n) if digit(i, w) == b]) if any(digit(i, w) == b for i in range(n))
+                 else ident for b in range(NB)]
+            V = []
+            for k in range(NB // M):
+                R = S = B[k * M + M - 1]
+                for j in range(M - 2, 0, -1):
+                    R = add(R, B[k * M + j])
+                    S = add(S, R)
+                R = add(R, B[k * M])
+                V.append(add(S, oracle.ge_scalarmult(np.frombuffer((k * M).to_bytes(32, "little"), np.uint8), R)))
+            Sw.append(tree(V))
+        T = Sw[-1]
+        for w in range(W - 2, -1, -1):
+            for _ in range(c):
+                T = add(T, T)
+            T = add(T, Sw[w])
+        assert np.array_equal(oracle.msm_pippenger(s, P, c), T), (n, c)
