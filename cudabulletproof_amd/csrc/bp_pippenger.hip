@@ -9,9 +9,9 @@
 //   in index order;  chunk k of M = 16 buckets: running sums R, S, then V = S + (kM) R;
 //   S_w = pairwise tree over the chunks;  T = Horner over the windows (c doublings + add).
 //
-// GPU mapping.  (1) one (key = w<<c | digit, value = i) pair per window and point, stable radix
-// sort (hipCUB) -> each bucket's points contiguous in index order; bucket bounds from the sorted
-// keys (no atomics).  (2) the bucket trees level by level over ALL buckets at once: a level's
+// GPU mapping.  (1) one (key = w<<c | digit, value = i) pair per window and point, generated
+// window-major, stable radix sort (hipCUB) on the digit bits -> each bucket's points contiguous in
+// index order; bucket bounds from the sorted keys (no atomics).  (2) the bucket trees level by level over ALL buckets at once: a level's
 // lane takes one adjacent pair of one bucket's current list (lists compacted and padded to even
 // length after every level, offsets by an exclusive scan), so every lane of every wave adds —
 // ~W n point additions at the VALU roof instead of one lane walking a bucket.  (3) one lane per
@@ -39,10 +39,10 @@ __global__ __launch_bounds__(PTPB) void k_pip_keys(const fe* __restrict__ s, siz
     const size_t i = g % n;
     const int lo = c * w;
     // bits [lo, lo + c) of the 256-bit scalar (a window may straddle two limbs or end past bit 255)
-    const fe sc = s[i];
+    const uint64_t* sc = s[i].v;   // only the limb(s) the window touches
     const int li = lo >> 6, sh = lo & 63;
-    uint64_t v = sc.v[li] >> sh;
-    if (sh && li < 3) v |= sc.v[li + 1] << (64 - sh);
+    uint64_t v = sc[li] >> sh;
+    if (sh && li < 3) v |= sc[li + 1] << (64 - sh);
     const uint32_t d = (uint32_t)(v & ((1ull << c) - 1));
     keys[g] = ((uint32_t)w << c) | d;
     vals[g] = (uint32_t)i;
@@ -58,13 +58,18 @@ __global__ __launch_bounds__(PTPB) void k_pip_bounds(const uint32_t* __restrict_
     if (p == N - 1 || keys[p + 1] != k) len[k] = (uint32_t)(p + 1);   // end, made a length below
 }
 
+// Bucket lists are processed two tree levels per launch ("steps"): a step's lane takes one
+// aligned group of 4 consecutive elements of one bucket's current list and reduces it exactly as
+// levels s and 2s of the pairwise tree do (x0+x1, x2+x3, then their sum; a short last group
+// carries), so lists are padded to a multiple of 4.  bid[pos] = the bucket of element pos (every
+// group head is a real element, so no search is needed).
 __global__ __launch_bounds__(PTPB) void k_pip_len0(const uint32_t* __restrict__ start, uint32_t* len, uint32_t* pad,
                                                   size_t nb, unsigned* maxlen) {
     const size_t b = (size_t)blockIdx.x * PTPB + threadIdx.x;
     if (b >= nb) return;
     const uint32_t L = len[b] ? len[b] - start[b] : 0;
     len[b] = L;
-    pad[b] = L + (L & 1);
+    pad[b] = (L + 3) & ~3u;
     if (L) atomicMax(maxlen, L);
 }
 
@@ -72,78 +77,52 @@ __global__ __launch_bounds__(PTPB) void k_pip_nextlen(const uint32_t* __restrict
                                                      size_t nb) {
     const size_t b = (size_t)blockIdx.x * PTPB + threadIdx.x;
     if (b >= nb) return;
-    const uint32_t L = (len[b] + 1) >> 1;
+    const uint32_t L = (len[b] + 3) >> 2;
     len2[b] = L;
-    pad2[b] = L + (L & 1);
+    pad2[b] = (L + 3) & ~3u;
 }
 
-// largest b with off[b] <= pos (zero-length buckets share the next bucket's offset, so this is
-// the bucket whose padded region holds pos)
-__device__ __forceinline__ size_t bucket_of(const uint32_t* __restrict__ off, size_t nb, uint32_t pos) {
-    size_t lo = 0, hi = nb;   // invariant: off[lo] <= pos, answer in [lo, hi)
-    while (hi - lo > 1) {
-        size_t mid = (lo + hi) >> 1;
-        if (off[mid] <= pos) lo = mid;
-        else hi = mid;
-    }
-    return lo;
+__global__ __launch_bounds__(PTPB) void k_pip_bid0(const uint32_t* __restrict__ keys, size_t N,
+                                                  const uint32_t* __restrict__ start, const uint32_t* __restrict__ off,
+                                                  uint32_t* bid) {
+    const size_t p = (size_t)blockIdx.x * PTPB + threadIdx.x;
+    if (p >= N) return;
+    const uint32_t b = keys[p];
+    bid[off[b] + (p - start[b])] = b;
 }
 
-// One tree level over every bucket: lane k takes positions (2k, 2k+1) of the current padded
-// layout; pairs add, an odd bucket's last element is carried.  Level 0 reads the points through
-// the sorted indices.
-__global__ __launch_bounds__(PTPB) void k_pip_level(int first, const ge* __restrict__ P,
-                                                   const uint32_t* __restrict__ vals,
-                                                   const uint32_t* __restrict__ start, const ge* __restrict__ Qin,
-                                                   const uint32_t* __restrict__ off, const uint32_t* __restrict__ len,
-                                                   const uint32_t* __restrict__ pad,
-                                                   const uint32_t* __restrict__ off2, ge* Qout, size_t nb,
-                                                   size_t lanes) {
+__global__ __launch_bounds__(PTPB) void k_pip_step(int first, const ge* __restrict__ P,
+                                                  const uint32_t* __restrict__ vals,
+                                                  const uint32_t* __restrict__ start, const ge* __restrict__ Qin,
+                                                  const uint32_t* __restrict__ bid, const uint32_t* __restrict__ off,
+                                                  const uint32_t* __restrict__ len, const uint32_t* __restrict__ pad,
+                                                  const uint32_t* __restrict__ off2, ge* Qout, uint32_t* bid2,
+                                                  size_t nb, size_t lanes) {
     const size_t k = (size_t)blockIdx.x * PTPB + threadIdx.x;
     if (k >= lanes) return;
     const uint32_t total = off[nb - 1] + pad[nb - 1];
-    const uint32_t pos = (uint32_t)(2 * k);
+    const uint32_t pos = (uint32_t)(4 * k);
     if (pos >= total) return;
-    const size_t b = bucket_of(off, nb, pos);
+    const uint32_t b = bid[pos];
     const uint32_t j = pos - off[b], L = len[b];
-    if (j >= L) return;   // padding
-    ge x0, out;
-    if (first) x0 = P[vals[start[b] + j]];
-    else x0 = Qin[off[b] + j];
-    if (j + 1 < L) {
-        ge x1;
-        if (first) x1 = P[vals[start[b] + j + 1]];
-        else x1 = Qin[off[b] + j + 1];
-        out = ge_add(x0, x1);
-    } else {
-        out = x0;
+    const uint32_t r = L - j < 4 ? L - j : 4;
+    const size_t base = first ? (size_t)start[b] + j : (size_t)off[b] + j;
+    auto load = [&](uint32_t t) -> ge { return first ? P[vals[base + t]] : Qin[base + t]; };
+    ge y0 = load(0);
+    if (r > 1) y0 = ge_add(y0, load(1));
+    if (r > 2) {
+        ge y1 = load(2);
+        if (r > 3) y1 = ge_add(y1, load(3));
+        y0 = ge_add(y0, y1);
     }
-    Qout[off2[b] + j / 2] = out;
+    const uint32_t o = off2[b] + j / 4;
+    Qout[o] = y0;
+    bid2[o] = b;
 }
 
 __device__ __forceinline__ ge bucket_sum(const ge* __restrict__ Q, const uint32_t* __restrict__ off,
                                          const uint32_t* __restrict__ cnt, size_t b) {
     return cnt[b] ? Q[off[b]] : ge_zero();
-}
-
-// chunk k of window w: buckets kM .. kM+M-1 -> V = S + (kM) R (orc_msm_pippenger)
-__global__ __launch_bounds__(PTPB) void k_pip_chunks(const ge* __restrict__ Q, const uint32_t* __restrict__ off,
-                                                    const uint32_t* __restrict__ cnt, int c, int W, ge* V,
-                                                    const ge* __restrict__ dtab) {
-    __shared__ geq qs[PTPB];
-    const size_t NB = (size_t)1 << c, NC = NB / PM;
-    const size_t g = (size_t)blockIdx.x * PTPB + threadIdx.x;
-    if (g >= (size_t)W * NC) return;
-    const size_t w = g / NC, k = g % NC, b0 = w * NB + k * PM;
-    ge R = bucket_sum(Q, off, cnt, b0 + PM - 1), S = R;
-    for (int j = PM - 2; j >= 1; j--) {
-        R = ge_add(R, bucket_sum(Q, off, cnt, b0 + j));
-        S = ge_add(S, R);
-    }
-    R = ge_add(R, bucket_sum(Q, off, cnt, b0));
-    fe km = fe_set((uint64_t)k * PM);
-    ge sm = scalarmult<true>(km, R, &qs[threadIdx.x], dtab);
-    V[g] = ge_add(S, sm);
 }
 
 // one block per window: pairwise tree over its NC <= PTPB chunk values, in LDS
@@ -159,14 +138,88 @@ __global__ __launch_bounds__(PTPB) void k_pip_window(const ge* __restrict__ V, i
     if (t == 0) Sw[blockIdx.x] = sh[0];
 }
 
-__global__ void k_pip_horner(const ge* __restrict__ Sw, int W, int c, ge* out) {
-    if (threadIdx.x != 0) return;
+// ---- latency-bound chains: one point operation per lane QUAD.  ge25519_add / the doubling are
+// three dependent product stages — {A, B, T1 T2, Z1 Z2} (squares for a doubling), then C = (T1 T2) k,
+// then {E F, G H, F G, E H} — and the four products of a stage are independent, so the quad's
+// lanes form one each (operands selected per lane) and swap results over DPP: 3 product
+// latencies per operation instead of 9 on one lane.  Every value is the very product ge_add /
+// ge_dbl forms, so the bits are theirs.
+template <int SRC>
+__device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, SRC * 0x55, 0xF, 0xF, true);
+}
+template <int SRC>
+__device__ __forceinline__ fe fe_quad_bcast(const fe& a) {
+    fe r;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        uint32_t lo = quad_bcast<SRC>((uint32_t)a.v[i]), hi = quad_bcast<SRC>((uint32_t)(a.v[i] >> 32));
+        r.v[i] = (uint64_t)lo | ((uint64_t)hi << 32);
+    }
+    return r;
+}
+__device__ __forceinline__ fe fe_sel4(int q, const fe& a, const fe& b, const fe& c, const fe& d) {
+    fe r;
+#pragma unroll
+    for (int i = 0; i < 4; i++) r.v[i] = q == 0 ? a.v[i] : q == 1 ? b.v[i] : q == 2 ? c.v[i] : d.v[i];
+    return r;
+}
+// DBL: add(p, p) (q ignored); else add(p, q).  p, q replicated over the quad; result replicated.
+template <bool DBL>
+__device__ __forceinline__ ge ge_op_quad(const ge& p, const ge& q) {
+    const int qd = threadIdx.x & 3;
+    const fe ymx = fe_sub(p.Y, p.X), ypx = fe_add(p.Y, p.X);
+    fe r1;
+    if (DBL) {
+        r1 = fe_sq(fe_sel4(qd, ymx, ypx, p.T, p.Z));
+    } else {
+        const fe qymx = fe_sub(q.Y, q.X), qypx = fe_add(q.Y, q.X);
+        r1 = fe_mul(fe_sel4(qd, ymx, ypx, p.T, p.Z), fe_sel4(qd, qymx, qypx, q.T, q.Z));
+    }
+    const fe A = fe_quad_bcast<0>(r1), B = fe_quad_bcast<1>(r1), CT = fe_quad_bcast<2>(r1);
+    fe D = fe_quad_bcast<3>(r1);
+    const fe C = fe_mul(CT, k_const());
+    D = fe_add(D, D);
+    const fe E = fe_sub(B, A), F = fe_sub(D, C), G = fe_add(D, C), H = fe_add(B, A);
+    const fe r3 = fe_mul(fe_sel4(qd, E, G, F, E), fe_sel4(qd, F, H, G, H));
+    return ge{fe_quad_bcast<0>(r3), fe_quad_bcast<1>(r3), fe_quad_bcast<2>(r3), fe_quad_bcast<3>(r3)};
+}
+
+// T = S_{W-1}; for w = W-2 .. 0: c doublings, then + S_w.  One quad (the block's first wave runs
+// 16 identical quads; lane 0 stores).
+__global__ __launch_bounds__(64) void k_pip_horner(const ge* __restrict__ Sw, int W, int c, ge* out) {
     ge T = Sw[W - 1];
     for (int w = W - 2; w >= 0; w--) {
-        for (int d = 0; d < c; d++) T = ge_dbl(T);   // add(T, T): the same bits
-        T = ge_add(T, Sw[w]);
+        for (int d = 0; d < c; d++) T = ge_op_quad<true>(T, T);
+        T = ge_op_quad<false>(T, Sw[w]);
     }
-    *out = T;
+    if (threadIdx.x == 0) *out = T;
+}
+
+// chunk k of window w (one lane quad): buckets kM .. kM+M-1 -> V = S + (kM) R (orc_msm_pippenger);
+// (kM) R is ge25519_scalarmult's double-and-add on the scalar's raw bits, leading zeros from dtab.
+__global__ __launch_bounds__(PTPB) void k_pip_chunks(const ge* __restrict__ Q, const uint32_t* __restrict__ off,
+                                                    const uint32_t* __restrict__ cnt, int c, int W, ge* V,
+                                                    const ge* __restrict__ dtab) {
+    const size_t NB = (size_t)1 << c, NC = NB / PM;
+    const size_t g = ((size_t)blockIdx.x * PTPB + threadIdx.x) >> 2;
+    if (g >= (size_t)W * NC) return;   // whole quads leave together
+    const size_t w = g / NC, k = g % NC, b0 = w * NB + k * PM;
+    ge R = bucket_sum(Q, off, cnt, b0 + PM - 1), S = R;
+    for (int j = PM - 2; j >= 1; j--) {
+        R = ge_op_quad<false>(R, bucket_sum(Q, off, cnt, b0 + j));
+        S = ge_op_quad<false>(S, R);
+    }
+    R = ge_op_quad<false>(R, bucket_sum(Q, off, cnt, b0));
+    const uint64_t km = (uint64_t)k * PM;
+    ge r = dtab[km ? 192 + __clzll(km) : 256];
+    if (km)
+        for (int i = 63 - __clzll(km); i >= 0; i--) {
+            r = ge_op_quad<true>(r, r);
+            if ((km >> i) & 1) r = ge_op_quad<false>(r, R);
+        }
+    r = ge_op_quad<false>(S, r);
+    if ((threadIdx.x & 3) == 0) V[g] = r;
 }
 
 struct DBuf {
@@ -182,7 +235,7 @@ struct DBuf {
     template <typename T> T* as() const { return (T*)p; }
 };
 struct PipWs {
-    DBuf keys_in, vals_in, keys, vals, temp, start, len[2], pad[2], off[2], Q[2], V, Sw, maxlen;
+    DBuf keys_in, vals_in, keys, vals, temp, start, len[2], pad[2], off[2], bid[2], Q[2], V, Sw, maxlen;
     unsigned* host_max = nullptr;
 };
 std::map<hipStream_t, PipWs*> g_pip;   // per stream; callers hold the engine lock
@@ -202,16 +255,18 @@ hipError_t msm_pippenger(ge* result, const fe* scal, const ge* P, size_t n, int 
     PipWs& ws = *wsp;
     const int W = (256 + c - 1) / c;
     const size_t NB = (size_t)1 << c, nb = (size_t)W * NB, N = (size_t)W * n, NC = NB / PM;
-    int kbits = c;
-    while ((1 << (kbits - c)) < W) kbits++;
+    // keys are generated window-major, so a STABLE sort on the c digit bits alone leaves each
+    // (window, digit) bucket contiguous and in index order (buckets ordered digit-major)
+    const int kbits = c;
     PIP_RET(ws.keys_in.need(N * 4)); PIP_RET(ws.vals_in.need(N * 4));
     PIP_RET(ws.keys.need(N * 4)); PIP_RET(ws.vals.need(N * 4));
     PIP_RET(ws.start.need(nb * 4));
     for (int i = 0; i < 2; i++) {
         PIP_RET(ws.len[i].need(nb * 4)); PIP_RET(ws.pad[i].need(nb * 4)); PIP_RET(ws.off[i].need(nb * 4));
     }
-    // level outputs: at most (N + nb) / 2 points after level 0, halving (plus padding) after
-    const size_t qcap = (N + nb) / 2 + nb;
+    // step 0 reads <= N + 3 nb padded positions and writes a quarter of them (+ padding)
+    const size_t tot0 = N + 3 * nb, qcap = tot0 / 4 + 4 * nb;
+    PIP_RET(ws.bid[0].need(tot0 * 4)); PIP_RET(ws.bid[1].need(qcap * 4));
     PIP_RET(ws.Q[0].need(qcap * sizeof(ge))); PIP_RET(ws.Q[1].need(qcap * sizeof(ge)));
     PIP_RET(ws.V.need((size_t)W * NC * sizeof(ge))); PIP_RET(ws.Sw.need((size_t)W * sizeof(ge)));
     PIP_RET(ws.maxlen.need(sizeof(unsigned)));
@@ -233,28 +288,31 @@ hipError_t msm_pippenger(ge* result, const fe* scal, const ge* P, size_t n, int 
                                           nb, ws.maxlen.as<unsigned>());
     PIP_RET(hipcub::DeviceScan::ExclusiveSum(ws.temp.p, tb_scan, ws.pad[0].as<uint32_t>(), ws.off[0].as<uint32_t>(),
                                              (int)nb, s));
+    k_pip_bid0<<<nb_of(N), PTPB, 0, s>>>(ws.keys.as<uint32_t>(), N, ws.start.as<uint32_t>(), ws.off[0].as<uint32_t>(),
+                                         ws.bid[0].as<uint32_t>());
     PIP_RET(hipMemcpyAsync(ws.host_max, ws.maxlen.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
     PIP_RET(hipStreamSynchronize(s));
     int levels = 1;
     while (((size_t)1 << levels) < *ws.host_max) levels++;
-    // level l: layout (off, len, pad)[l & 1] -> (.., ..)[(l + 1) & 1], data Q[(l + 1) & 1] (l >= 1 reads Q[l & 1])
-    size_t lanes = (N + nb + 1) / 2;
-    for (int l = 0; l < levels; l++) {
-        const int a = l & 1, b = a ^ 1;
+    const int steps = (levels + 1) / 2;
+    // step t: layout (off, len, pad, bid)[t & 1] -> [(t + 1) & 1], data -> Q[(t + 1) & 1]
+    size_t lanes = (tot0 + 3) / 4;
+    for (int t = 0; t < steps; t++) {
+        const int a = t & 1, b = a ^ 1;
         k_pip_nextlen<<<nb_of(nb), PTPB, 0, s>>>(ws.len[a].as<uint32_t>(), ws.len[b].as<uint32_t>(),
                                                   ws.pad[b].as<uint32_t>(), nb);
         PIP_RET(hipcub::DeviceScan::ExclusiveSum(ws.temp.p, tb_scan, ws.pad[b].as<uint32_t>(),
                                                  ws.off[b].as<uint32_t>(), (int)nb, s));
-        k_pip_level<<<nb_of(lanes), PTPB, 0, s>>>(l == 0, P, ws.vals.as<uint32_t>(), ws.start.as<uint32_t>(),
-                                                   ws.Q[a].as<ge>(), ws.off[a].as<uint32_t>(),
-                                                   ws.len[a].as<uint32_t>(), ws.pad[a].as<uint32_t>(),
-                                                   ws.off[b].as<uint32_t>(), ws.Q[b].as<ge>(), nb, lanes);
-        lanes = lanes / 2 + nb;
+        k_pip_step<<<nb_of(lanes), PTPB, 0, s>>>(t == 0, P, ws.vals.as<uint32_t>(), ws.start.as<uint32_t>(),
+                                                  ws.Q[a].as<ge>(), ws.bid[a].as<uint32_t>(), ws.off[a].as<uint32_t>(),
+                                                  ws.len[a].as<uint32_t>(), ws.pad[a].as<uint32_t>(),
+                                                  ws.off[b].as<uint32_t>(), ws.Q[b].as<ge>(), ws.bid[b].as<uint32_t>(),
+                                                  nb, lanes);
+        lanes = lanes / 4 + nb;
     }
-    // after the last level every non-empty bucket holds its sum at off[levels & 1][b]
-    const int fin = levels & 1;
-    // a bucket is empty iff its level-0 length was 0 == its final length is 0
-    k_pip_chunks<<<nb_of((size_t)W * NC), PTPB, 0, s>>>(ws.Q[fin].as<ge>(), ws.off[fin].as<uint32_t>(),
+    // after the last step every non-empty bucket holds its sum at off[steps & 1][b]
+    const int fin = steps & 1;
+    k_pip_chunks<<<nb_of(4 * (size_t)W * NC), PTPB, 0, s>>>(ws.Q[fin].as<ge>(), ws.off[fin].as<uint32_t>(),
                                                          ws.len[fin].as<uint32_t>(), c, W, ws.V.as<ge>(), dtab);
     k_pip_window<<<W, PTPB, 0, s>>>(ws.V.as<ge>(), (int)NC, ws.Sw.as<ge>());
     k_pip_horner<<<1, 64, 0, s>>>(ws.Sw.as<ge>(), W, c, result);
