@@ -12,6 +12,9 @@
 namespace bp {
 
 constexpr int TPB = 256;   // threads per block for lane-per-item kernels
+#ifndef BP_TERMS_OCC
+#define BP_TERMS_OCC 4   // k_terms blocks per CU the register budget is sized for
+#endif
 
 
 __device__ __forceinline__ size_t gid() { return (size_t)blockIdx.x * blockDim.x + threadIdx.x; }
@@ -690,7 +693,7 @@ void launch_lane_sort(const LaneSortPlan& plan, unsigned* bins, unsigned* offs, 
 // The RK_TREE region (if any) comes first and spans whole blocks: each block folds TPB/n
 // segments of the batch's 2B MSMs with the canonical tree of k_tree, barriers block-uniform;
 // its LDS is the q-operand array (no scalar multiplication runs in those blocks).
-__global__ __launch_bounds__(TPB, 4) void k_terms(RegionList rl, const SlotDev* __restrict__ slots,
+__global__ __launch_bounds__(TPB, BP_TERMS_OCC) void k_terms(RegionList rl, const SlotDev* __restrict__ slots,
                                                const ge* __restrict__ G, const ge* __restrict__ H,
                                                const ge* __restrict__ g, const ge* __restrict__ h,
                                                const ge* __restrict__ dtab, const fe* __restrict__ two_i) {
