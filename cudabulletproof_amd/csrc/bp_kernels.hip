@@ -789,6 +789,23 @@ void launch_field_op(int op, fe* r, const fe* a, const fe* b, size_t count, hipS
 }
 
 
+// The halving tree's levels with stride <= 32 (their pairs (t, t+st) lie inside wave 0), in
+// registers: lane t takes lane t+st's value over a wave shuffle and adds it when t < st and
+// t + st < lim — exactly the LDS tree's pairs, order and guard.
+__device__ __forceinline__ fe fe_wave_tail(fe v, int tid, unsigned st, size_t lim) {
+    for (; st > 0; st >>= 1) {
+        fe o;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            uint32_t lo = (uint32_t)__shfl_down((int)(uint32_t)v.v[i], st, 64);
+            uint32_t hi = (uint32_t)__shfl_down((int)(uint32_t)(v.v[i] >> 32), st, 64);
+            o.v[i] = (uint64_t)lo | ((uint64_t)hi << 32);
+        }
+        if (tid < (int)st && (size_t)(tid + st) < lim) v = fe_add(v, o);
+    }
+    return v;
+}
+
 // ------------------------------------------------------------------ field inner products
 // cuda_inner_product.cu:154-183 field_vector_inner_product_shared_kernel, one block of
 // nthreads = min(n, 512): products, then halving tree from nthreads/2 with tid+stride < n.
@@ -798,19 +815,26 @@ __global__ __launch_bounds__(512) void k_ip_shared(fe* out, const fe* __restrict
     int tid = threadIdx.x;
     sh[tid] = fe_mul(a[tid], b[tid]);
     __syncthreads();
-    for (unsigned st = blockDim.x / 2; st > 0; st >>= 1) {
+    unsigned st = blockDim.x / 2;
+    for (; st > 32; st >>= 1) {
         if (tid < (int)st && (size_t)(tid + st) < n) sh[tid] = fe_add(sh[tid], sh[tid + st]);
         __syncthreads();
     }
-    if (tid == 0) *out = sh[0];
+    if (tid < 64) {
+        fe v = sh[tid];
+        v = fe_wave_tail(v, tid, st, n);
+        if (tid == 0) *out = v;
+    }
 }
 
 // cuda_inner_product.cu:33-61 field_vector_inner_product_kernel: grid-stride fold from 0,
-// then block tree 128..1 over all 256 slots.  With `warp_tail`, the tree stops at 32 and the
-// 16..1 halving of warp_reduce_field_element (:219-257) finishes it (batch_inner_product_kernel
-// :260-299).  blockIdx.y selects the vector (stride n) for the batched form.
+// then block tree 128..1 over all 256 slots.  With `warp_tail` the reference stops the block tree
+// at 32 and warp_reduce_field_element (:219-257) does 16..1 (batch_inner_product_kernel :260-299):
+// the same strides, so both run the wave-shuffle tail below 64.  blockIdx.y selects the vector
+// (stride n) for the batched form.
 __global__ __launch_bounds__(TPB) void k_ip_grid(fe* out, const fe* __restrict__ a, const fe* __restrict__ b,
                                                  size_t n, size_t grid_threads, int warp_tail) {
+    (void)warp_tail;
     __shared__ fe sh[TPB];
     int tid = threadIdx.x;
     size_t vec = blockIdx.y;
@@ -820,18 +844,16 @@ __global__ __launch_bounds__(TPB) void k_ip_grid(fe* out, const fe* __restrict__
     for (size_t idx = (size_t)blockIdx.x * TPB + tid; idx < n; idx += grid_threads) acc = fe_add(acc, fe_mul(a[idx], b[idx]));
     sh[tid] = acc;
     __syncthreads();
-    int stop = warp_tail ? 32 : 1;
-    for (int st = TPB / 2; st >= stop; st >>= 1) {
-        if (tid < st) sh[tid] = fe_add(sh[tid], sh[tid + st]);
+    unsigned st = TPB / 2;
+    for (; st > 32; st >>= 1) {
+        if (tid < (int)st) sh[tid] = fe_add(sh[tid], sh[tid + st]);
         __syncthreads();
     }
-    if (warp_tail) {
-        for (int st = 16; st >= 1; st >>= 1) {
-            if (tid < st) sh[tid] = fe_add(sh[tid], sh[tid + st]);
-            __syncthreads();
-        }
+    if (tid < 64) {
+        fe v = sh[tid];
+        v = fe_wave_tail(v, tid, st, TPB);
+        if (tid == 0) out[vec * gridDim.x + blockIdx.x] = v;
     }
-    if (tid == 0) out[vec * gridDim.x + blockIdx.x] = sh[0];
 }
 
 // cuda_inner_product.cu:69-92 fe25519_reduce_kernel: 256 slots, partials beyond 256 unread.
@@ -840,11 +862,16 @@ __global__ __launch_bounds__(TPB) void k_ip_reduce(fe* out, const fe* __restrict
     int tid = threadIdx.x;
     sh[tid] = (size_t)tid < np ? part[tid] : fe_set(0);
     __syncthreads();
-    for (int st = TPB / 2; st > 0; st >>= 1) {
-        if (tid < st && (size_t)(tid + st) < np) sh[tid] = fe_add(sh[tid], sh[tid + st]);
+    unsigned st = TPB / 2;
+    for (; st > 32; st >>= 1) {
+        if (tid < (int)st && (size_t)(tid + st) < np) sh[tid] = fe_add(sh[tid], sh[tid + st]);
         __syncthreads();
     }
-    if (tid == 0) *out = sh[0];
+    if (tid < 64) {
+        fe v = sh[tid];
+        v = fe_wave_tail(v, tid, st, np);
+        if (tid == 0) *out = v;
+    }
 }
 
 void launch_ip_shared(fe* out, const fe* a, const fe* b, size_t n, hipStream_t s) {
