@@ -96,7 +96,7 @@ EXPORTS = [
     "cuda_benchmark_multi_scalar_mul", "cuda_benchmark_inner_product", "cuda_benchmark_field_operations",
     "cuda_benchmark_range_proof", "hipbp_last_error", "hipbp_device_count", "hipbp_batch_range_proof_verify",
     "hipbp_batch_range_proof_verify_std", "hipbp_batch_inner_product_verify", "hipbp_batch_generate_range_proof", "hipbp_msm",
-    "hipbp_msm_pippenger",
+    "hipbp_msm_pippenger", "hipbp_msm_batch",
     "hipbp_point_tree", "hipbp_field_op", "hipbp_sync", "hipbp_timing_enable",
     "hipbp_timing_collect", "hipbp_kernel_count", "hipbp_kernel_name", "hipbp_pipeline_create",
     "hipbp_pipeline_push", "hipbp_pipeline_flush", "hipbp_pipeline_depth", "hipbp_pipeline_destroy",
@@ -122,7 +122,7 @@ def lib():
             getattr(L, f).restype = ctypes.c_bool
         for f in ("hipbp_batch_range_proof_verify", "hipbp_batch_range_proof_verify_std",
                   "hipbp_batch_inner_product_verify", "hipbp_batch_generate_range_proof", "hipbp_msm",
-                  "hipbp_msm_pippenger",
+                  "hipbp_msm_pippenger", "hipbp_msm_batch",
                   "hipbp_point_tree",
                   "hipbp_field_op", "hipbp_sync", "hipbp_device_count"):
             getattr(L, f).restype = ctypes.c_int
@@ -394,6 +394,17 @@ def msm(result, scalars, points, stream=None):
     """Canonical-tree MSM on CUDA tensors: result (16,), scalars (n,4), points (n,16)."""
     _chk(lib().hipbp_msm(_c(result.data_ptr()), _c(scalars.data_ptr()), _c(points.data_ptr()),
                          _sz(points.shape[0]), _stream_ptr(stream)))
+
+
+def msm_batch(results, scalars, points, stream=None):
+    """count canonical-tree MSMs over the same points: results (count,16), scalars (count*n,4) or
+    (count,n,4), points (n,16); CUDA tensors."""
+    n = points.shape[0]
+    count = results.shape[0]
+    if scalars.numel() != count * n * 4:
+        raise BulletproofError("msm_batch: scalars must hold count * n rows")
+    _chk(lib().hipbp_msm_batch(_c(results.data_ptr()), _c(scalars.data_ptr()), _c(points.data_ptr()), _sz(n),
+                               _sz(count), _stream_ptr(stream)))
 
 
 def msm_pippenger(result, scalars, points, window_bits=12, stream=None):

@@ -691,6 +691,28 @@ int hipbp_msm(ge25519* result, const fe25519* scalars, const ge25519* points, si
     return HIPBP_OK;
 }
 
+int hipbp_msm_batch(ge25519* results, const fe25519* scalars, const ge25519* points, size_t n, size_t count,
+                    void* stream) {
+    hipError_t err;
+    Engine* e = engine_or_null(&err);
+    BP_RET_ON(err);
+    if (n == 0 || count == 0) return HIPBP_OK;
+    if (!results || !scalars || !points) { g_err = "null argument"; return HIPBP_ERR_ARG; }
+    if (count > 0x7FFFFFFFull || n * count > 0xFFFFFFFFull) { g_err = "msm_batch: too many items"; return HIPBP_ERR_ARG; }
+    std::lock_guard<std::mutex> lk(e->mu);
+    const size_t tot = n * count, nb = count * ((n + 255) / 256);
+    BP_RET_ON(e->scratch[0].need(tot * sizeof(bp::ge)));
+    BP_RET_ON(e->scratch[1].need(nb * sizeof(bp::ge)));
+    BP_RET_ON(e->scratch[2].need(nb * sizeof(bp::ge)));
+    BP_RET_ON(e->scratch[6].need(tot * sizeof(uint32_t)));
+    BP_RET_ON(e->scratch[7].need(bp::MSM_BINS * sizeof(unsigned)));
+    bp::launch_msm_full((bp::ge*)results, (const bp::fe*)scalars, (const bp::ge*)points, n, e->scratch[0].as<bp::ge>(),
+                        e->scratch[1].as<bp::ge>(), e->scratch[2].as<bp::ge>(), e->scratch[6].as<uint32_t>(),
+                        e->scratch[7].as<unsigned>(), e->dtab, pick(stream, *e), count);
+    BP_RET_ON(hipGetLastError());
+    return HIPBP_OK;
+}
+
 int hipbp_msm_pippenger(ge25519* result, const fe25519* scalars, const ge25519* points, size_t n, int window_bits,
                         void* stream) {
     hipError_t err;

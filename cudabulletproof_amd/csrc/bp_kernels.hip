@@ -50,15 +50,16 @@ void launch_init_tables(ge* dtab, fe* two_i, int nmax, hipStream_t s) {
 // (cuda_bulletproof_kernels.cu:26-42); the scalar bytes are the raw limbs (device tobytes).
 // `perm` (nullable) maps lane -> item: the lanes of a wave take items of equal length, so no
 // lane idles while the longest scalar of its wave finishes (below).
+// `pm`: the point of item i is P[i % pm] (a batch of MSMs over the same points; pm = total for one).
 __global__ __launch_bounds__(TPB, 3) void k_msm_points(ge* pts, const fe* __restrict__ scal,
-                                                    const ge* __restrict__ P, size_t total,
+                                                    const ge* __restrict__ P, size_t total, size_t pm,
                                                     const uint32_t* __restrict__ perm,
                                                     const ge* __restrict__ dtab) {
     __shared__ geq qs[TPB];
     size_t i = gid();
     if (i >= total) return;
     if (perm) i = perm[i];
-    ge r = scalarmult<true>(scal[i], P[i], &qs[threadIdx.x], dtab);
+    ge r = scalarmult<true>(scal[i], P[pm == total ? i : i % pm], &qs[threadIdx.x], dtab);
     pts[i] = ge_norm_dev(r);
 }
 
@@ -126,7 +127,8 @@ void launch_ops_scan(unsigned* bins, int longest_first, hipStream_t s) {
 }
 
 void launch_msm_points(ge* pts, const fe* scal, const ge* P, size_t m, uint32_t* perm, unsigned* bins,
-                       const ge* dtab, hipStream_t s) {
+                       const ge* dtab, hipStream_t s, size_t pm) {
+    if (!pm) pm = m;
     size_t blocks = (m + TPB - 1) / TPB;
     static const int sort_mode = getenv("HIPBP_MSM_SORT") ? atoi(getenv("HIPBP_MSM_SORT")) : 1;
     if (!sort_mode) perm = nullptr;
@@ -138,7 +140,7 @@ void launch_msm_points(ge* pts, const fe* scal, const ge* P, size_t m, uint32_t*
     } else {
         perm = nullptr;
     }
-    k_msm_points<<<blocks, TPB, 0, s>>>(pts, scal, P, m, perm, dtab);
+    k_msm_points<<<blocks, TPB, 0, s>>>(pts, scal, P, m, pm, perm, dtab);
 }
 
 // Canonical pairwise tree over S segments of m points: for stride 1,2,4,..:
@@ -908,14 +910,14 @@ void launch_invert(fe* r, const fe* a, size_t count, hipStream_t s) {
 
 // Generic canonical-tree MSM on device: ptsbuf holds n points, part0/part1 ping-pong.
 // Canonical tree over n points (levels 1, 2, 4, ...: one k_tree launch per 256x reduction).
-void launch_tree_full(ge* result, const ge* in, size_t n, ge* part0, ge* part1, hipStream_t s) {
+void launch_tree_full(ge* result, const ge* in, size_t n, ge* part0, ge* part1, hipStream_t s, int S) {
     size_t m = n;
     ge* bufs[2] = {part0, part1};
     int w = 0;
     while (true) {
         size_t nb = (m + TPB - 1) / TPB;
         ge* out = (nb == 1) ? result : bufs[w];
-        launch_tree(out, in, 1, m, s);
+        launch_tree(out, in, S, m, s);
         if (nb == 1) break;
         in = out;
         m = nb;
@@ -924,9 +926,11 @@ void launch_tree_full(ge* result, const ge* in, size_t n, ge* part0, ge* part1, 
 }
 
 void launch_msm_full(ge* result, const fe* scal, const ge* P, size_t n, ge* ptsbuf, ge* part0, ge* part1,
-                     uint32_t* perm, unsigned* bins, const ge* dtab, hipStream_t s) {
-    launch_msm_points(ptsbuf, scal, P, n, perm, bins, dtab, s);
-    launch_tree_full(result, ptsbuf, n, part0, part1, s);
+                     uint32_t* perm, unsigned* bins, const ge* dtab, hipStream_t s, size_t count) {
+    // count MSMs of n points each over the same points: one per-point launch over all count*n
+    // items (chain-length sorted together), then the canonical tree per segment
+    launch_msm_points(ptsbuf, scal, P, n * count, perm, bins, dtab, s, n);
+    launch_tree_full(result, ptsbuf, n, part0, part1, s, (int)count);
 }
 
 }  // namespace bp

@@ -196,6 +196,13 @@ int hipbp_batch_generate_range_proof(const hipbp_prove_input* in, const ge25519*
 /* Canonical-tree MSM on device buffers. */
 int hipbp_msm(ge25519* result, const fe25519* scalars, const ge25519* points, size_t n, void* stream);
 
+/* count independent canonical-tree MSMs of n points each over the SAME points (e.g. the IPA
+ * commitments P = MSM(a||b, G||H) of a batch of proofs): scalars
+ * [count*n] (MSM k = rows k*n .. k*n+n-1), points [n], results [count]; each result is bit-exact
+ * with hipbp_msm on its rows.  Device buffers. */
+int hipbp_msm_batch(ge25519* results, const fe25519* scalars, const ge25519* points, size_t n, size_t count,
+                    void* stream);
+
 /* Pippenger bucket MSM with window_bits-bit windows (4..12; BASELINE configs[2] names 12), over
  * the same fe25519/ge25519 arithmetic, on device buffers.  A LABELLED ALTERNATIVE, not a drop-in
  * for cuda_point_vector_multi_scalar_mul: the reference's MSM bits come from per-point

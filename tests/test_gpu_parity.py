@@ -612,3 +612,61 @@ def test_msm_pippenger_rejects_bad_window(bp):
     with pytest.raises(bp.BulletproofError):
         bp.msm_pippenger(torch.zeros(16, dtype=torch.int64, device=dev), torch.zeros(4, 4, dtype=torch.int64,
                                                                                       device=dev), z, 13)
+
+
+@pytest.mark.parametrize("kind", ["same", "zero", "one_bit"])
+def test_msm_pippenger_degenerate_scalars(bp, oracle, kind):
+    """Every point in one bucket per window (deep bucket trees, many empty buckets)."""
+    import torch
+    n, c = 3000, 8
+    P = oracle.base_points(n, 12)
+    s = np.zeros((n, 4), np.uint64)
+    if kind == "same":
+        s[:] = rand_fe(np.random.default_rng(5), 1)[0]
+    elif kind == "one_bit":
+        s[:, 2] = np.uint64(1) << np.uint64(17)
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    out = torch.zeros(16, dtype=torch.int64, device=dev)
+    bp.msm_pippenger(out, T(s), T(P), c)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint64), oracle.msm_pippenger(s, P, c))
+
+
+# ----------------------------------------------------------------------------- batched MSM
+@pytest.mark.parametrize("n,count", [(1, 3), (17, 5), (300, 4), (256, 2)])
+def test_msm_batch_matches_single(bp, oracle, n, count):
+    """hipbp_msm_batch: each of count MSMs over the same points == the oracle's canonical MSM."""
+    import torch
+    rng = np.random.default_rng(n + count)
+    P = oracle.base_points(n, 13)
+    s = rand_fe(rng, n * count)
+    s[::9] = 0
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    out = torch.zeros(count, 16, dtype=torch.int64, device=dev)
+    bp.msm_batch(out, T(s), T(P))
+    torch.cuda.synchronize()
+    out = out.cpu().numpy().view(np.uint64)
+    for k in range(count):
+        assert np.array_equal(out[k], oracle.msm_canon(s[k * n:(k + 1) * n], P)), k
+
+
+def test_msm_batch_ipa4096_commitment(bp, golden, oracle):
+    """configs[3]'s P = MSM(a||b, G||H) over 8192 points, for 3 proofs at once, equals the
+    reference's P recorded in ipa4096.npz."""
+    import os
+    import sys
+    import torch
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_golden import ipa_vectors
+    d, n, G, H, Q = _ipa4096(golden, oracle)
+    a, b = ipa_vectors(n)
+    sc = np.concatenate([a, b] * 3)
+    dev = torch.device("cuda:0")
+    T = lambda x: torch.from_numpy(np.ascontiguousarray(x, np.uint64).view(np.int64)).to(dev)
+    out = torch.zeros(3, 16, dtype=torch.int64, device=dev)
+    bp.msm_batch(out, T(sc), T(np.concatenate([G, H])))
+    torch.cuda.synchronize()
+    for k in range(3):
+        assert np.array_equal(out.cpu().numpy().view(np.uint64)[k], d["P"])
