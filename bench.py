@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-procs", type=int, default=16, help="processes for the parallel CPU baseline")
     ap.add_argument("--no-msm", action="store_true")
+    ap.add_argument("--proofs", choices=["prover", "synthetic"], default="prover",
+                    help="verify inputs: proofs made by the GPU prover from random 64-bit values (default) "
+                         "or proof-shaped random data")
     ap.add_argument("--rehearse", action="store_true",
                     help="exercise the N>1 path on one GPU (all ranks on cuda:0, gloo collectives); not a measurement")
     return ap.parse_args()
@@ -357,7 +360,16 @@ def main():
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)
     Gd, Hd, gd, hd = T(G), T(H), T(g), T(h)
     nb = 4
-    batches = [bp.RangeProofBatch.from_numpy(n, synth.proofs(B, n, seed=1 + 1000 * rank + i), dev) for i in range(nb)]
+    if args.proofs == "prover":   # real 64-bit range proofs from the GPU prover (bit-exact with the reference's)
+        batches = []
+        for i in range(nb):
+            pi = {k: T(v) for k, v in synth.prove_inputs(B, n, seed=1 + 1000 * rank + i).items()}
+            out = bp.batch_generate_range_proof(n, pi["v"], pi["gamma"], pi["sL"], pi["sR"], pi["rnd"], Gd, Hd, gd, hd)
+            torch.cuda.synchronize(dev)
+            batches.append(bp.RangeProofBatch(n, **{k: out[k] for k in bp.RangeProofBatch.FIELDS}))
+    else:
+        batches = [bp.RangeProofBatch.from_numpy(n, synth.proofs(B, n, seed=1 + 1000 * rank + i), dev)
+                   for i in range(nb)]
     ns = max(1, args.streams)
     streams = [torch.cuda.Stream(dev) for _ in range(ns)]
     oks = [torch.zeros(B, dtype=torch.uint8, device=dev) for _ in range(max(ns, nb))]
@@ -459,7 +471,10 @@ def main():
             "metric": "64-bit range-proof verifies/sec (batched)", "value": value, "unit": "verifies/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
-            "data": "synthetic (seeded proof-shaped inputs, a=[t], b=[1], c=t; generators per "
+            "data": ("synthetic: real 64-bit range proofs of random values made by the GPU prover "
+                     "(generate_range_proof semantics, seeded randomness); generators per "
+                     "complete_bulletproof_test.cu:33-109") if args.proofs == "prover" else
+                    "synthetic (seeded proof-shaped inputs, a=[t], b=[1], c=t; generators per "
                     "complete_bulletproof_test.cu:33-109)",
             "config": {"workload": f"batch {B} x {n}-bit range-proof verify per GPU (BASELINE configs[1])",
                        "batch_per_gpu": B, "n": n, "semantics": "cuda_range_proof_verify (crv:82)",
