@@ -16,7 +16,8 @@
 // length after every level, offsets by an exclusive scan), so every lane of every wave adds —
 // ~W n point additions at the VALU roof instead of one lane walking a bucket.  (3) one lane per
 // chunk (W 2^c / 16 lanes) for the running sums and the small scalar-mult, (4) one block per
-// window: the chunk tree in LDS, (5) one lane: the Horner chain (~256 doublings, latency-bound).
+// window: the chunk tree in LDS, (5) one lane quad: the Horner chain (~256 doublings,
+// latency-bound), on a side stream so its top-half part overlaps the bottom half's buckets.
 #include <hipcub/hipcub.hpp>
 
 #include <map>
@@ -31,13 +32,14 @@ namespace {
 constexpr int PTPB = 256;
 constexpr int PM = 16;   // buckets per chunk
 
-__global__ __launch_bounds__(PTPB) void k_pip_keys(const fe* __restrict__ s, size_t n, int c, int W,
+// windows w0 .. w0+W-1 (local index lw = w - w0 in the key)
+__global__ __launch_bounds__(PTPB) void k_pip_keys(const fe* __restrict__ s, size_t n, int c, int w0, int W,
                                                   uint32_t* keys, uint32_t* vals) {
     const size_t g = (size_t)blockIdx.x * PTPB + threadIdx.x;
     if (g >= (size_t)W * n) return;
     const int w = (int)(g / n);
     const size_t i = g % n;
-    const int lo = c * w;
+    const int lo = c * (w0 + w);
     // bits [lo, lo + c) of the 256-bit scalar (a window may straddle two limbs or end past bit 255)
     const uint64_t* sc = s[i].v;   // only the limb(s) the window touches
     const int li = lo >> 6, sh = lo & 63;
@@ -185,11 +187,20 @@ __device__ __forceinline__ ge ge_op_quad(const ge& p, const ge& q) {
     return ge{fe_quad_bcast<0>(r3), fe_quad_bcast<1>(r3), fe_quad_bcast<2>(r3), fe_quad_bcast<3>(r3)};
 }
 
-// T = S_{W-1}; for w = W-2 .. 0: c doublings, then + S_w.  One quad (the block's first wave runs
-// 16 identical quads; lane 0 stores).
-__global__ __launch_bounds__(64) void k_pip_horner(const ge* __restrict__ Sw, int W, int c, ge* out) {
-    ge T = Sw[W - 1];
-    for (int w = W - 2; w >= 0; w--) {
+// Horner over windows w_top .. w_end (descending): T = Tin ? *Tin : S_{w_top} (then from
+// w_top - 1); per window c doublings, then + S_w.  One quad (the block's wave runs 16 identical
+// quads; lane 0 stores).  Split at any window, two calls give the single chain's bits.
+__global__ __launch_bounds__(64) void k_pip_horner(const ge* __restrict__ Sw, int w_top, int w_end, int c,
+                                                  const ge* __restrict__ Tin, ge* out) {
+    ge T;
+    int w = w_top;
+    if (Tin) {
+        T = *Tin;
+    } else {
+        T = Sw[w_top];
+        w--;
+    }
+    for (; w >= w_end; w--) {
         for (int d = 0; d < c; d++) T = ge_op_quad<true>(T, T);
         T = ge_op_quad<false>(T, Sw[w]);
     }
@@ -235,8 +246,11 @@ struct DBuf {
     template <typename T> T* as() const { return (T*)p; }
 };
 struct PipWs {
-    DBuf keys_in, vals_in, keys, vals, temp, start, len[2], pad[2], off[2], bid[2], Q[2], V, Sw, maxlen;
+    DBuf keys_in, vals_in, keys, vals, temp, start, len[2], pad[2], off[2], bid[2], Q[2], V, Sw, Tmid, maxlen;
     unsigned* host_max = nullptr;
+    hipStream_t side = nullptr;           // the Horner chain's stream
+    hipEvent_t ev[4] = {};   // [1] top half's buckets done, [2] bottom half done, [3] chain done
+    int fin = 0;
 };
 std::map<hipStream_t, PipWs*> g_pip;   // per stream; callers hold the engine lock
 
@@ -245,16 +259,12 @@ inline unsigned nb_of(size_t items) { return (unsigned)((items + PTPB - 1) / PTP
 
 #define PIP_RET(x) do { hipError_t _e = (x); if (_e != hipSuccess) return _e; } while (0)
 
-hipError_t msm_pippenger(ge* result, const fe* scal, const ge* P, size_t n, int c, const ge* dtab, hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    PipWs*& wsp = g_pip[s];
-    if (!wsp) {
-        wsp = new PipWs();
-        PIP_RET(hipHostMalloc(&wsp->host_max, sizeof(unsigned)));
-    }
-    PipWs& ws = *wsp;
-    const int W = (256 + c - 1) / c;
+// Bucket sums of windows [w0, w1) on stream s (ws.fin: the ping-pong side holding them).
+static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, int c, int w0, int w1,
+                              hipStream_t s) {
+    const int W = w1 - w0;
     const size_t NB = (size_t)1 << c, nb = (size_t)W * NB, N = (size_t)W * n, NC = NB / PM;
+    (void)P;
     // keys are generated window-major, so a STABLE sort on the c digit bits alone leaves each
     // (window, digit) bucket contiguous and in index order (buckets ordered digit-major)
     const int kbits = c;
@@ -268,7 +278,7 @@ hipError_t msm_pippenger(ge* result, const fe* scal, const ge* P, size_t n, int 
     const size_t tot0 = N + 3 * nb, qcap = tot0 / 4 + 4 * nb;
     PIP_RET(ws.bid[0].need(tot0 * 4)); PIP_RET(ws.bid[1].need(qcap * 4));
     PIP_RET(ws.Q[0].need(qcap * sizeof(ge))); PIP_RET(ws.Q[1].need(qcap * sizeof(ge)));
-    PIP_RET(ws.V.need((size_t)W * NC * sizeof(ge))); PIP_RET(ws.Sw.need((size_t)W * sizeof(ge)));
+    PIP_RET(ws.V.need((size_t)W * NC * sizeof(ge)));
     PIP_RET(ws.maxlen.need(sizeof(unsigned)));
     size_t tb_sort = 0, tb_scan = 0;
     PIP_RET(hipcub::DeviceRadixSort::SortPairs(nullptr, tb_sort, ws.keys_in.as<uint32_t>(), ws.keys.as<uint32_t>(),
@@ -277,7 +287,7 @@ hipError_t msm_pippenger(ge* result, const fe* scal, const ge* P, size_t n, int 
                                              (int)nb, s));
     PIP_RET(ws.temp.need(tb_sort > tb_scan ? tb_sort : tb_scan));
 
-    k_pip_keys<<<nb_of(N), PTPB, 0, s>>>(scal, n, c, W, ws.keys_in.as<uint32_t>(), ws.vals_in.as<uint32_t>());
+    k_pip_keys<<<nb_of(N), PTPB, 0, s>>>(scal, n, c, w0, W, ws.keys_in.as<uint32_t>(), ws.vals_in.as<uint32_t>());
     PIP_RET(hipcub::DeviceRadixSort::SortPairs(ws.temp.p, tb_sort, ws.keys_in.as<uint32_t>(), ws.keys.as<uint32_t>(),
                                                ws.vals_in.as<uint32_t>(), ws.vals.as<uint32_t>(), (int)N, 0, kbits, s));
     PIP_RET(hipMemsetAsync(ws.start.p, 0, nb * 4, s));
@@ -291,7 +301,7 @@ hipError_t msm_pippenger(ge* result, const fe* scal, const ge* P, size_t n, int 
     k_pip_bid0<<<nb_of(N), PTPB, 0, s>>>(ws.keys.as<uint32_t>(), N, ws.start.as<uint32_t>(), ws.off[0].as<uint32_t>(),
                                          ws.bid[0].as<uint32_t>());
     PIP_RET(hipMemcpyAsync(ws.host_max, ws.maxlen.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
-    PIP_RET(hipStreamSynchronize(s));
+    PIP_RET(hipStreamSynchronize(s));   // the bucket-tree depth (only this stream: the side stream runs on)
     int levels = 1;
     while (((size_t)1 << levels) < *ws.host_max) levels++;
     const int steps = (levels + 1) / 2;
@@ -311,12 +321,64 @@ hipError_t msm_pippenger(ge* result, const fe* scal, const ge* P, size_t n, int 
         lanes = lanes / 4 + nb;
     }
     // after the last step every non-empty bucket holds its sum at off[steps & 1][b]
-    const int fin = steps & 1;
+    ws.fin = steps & 1;
+    return hipGetLastError();
+}
+
+// Chunks -> window sums of windows [w0, w1) into Sw[w0 .. w1-1], on stream s (latency-bound).
+static hipError_t pip_finish(PipWs& ws, int c, int w0, int w1, ge* Sw, const ge* dtab, hipStream_t s) {
+    const int W = w1 - w0, fin = ws.fin;
+    const size_t NC = ((size_t)1 << c) / PM;
     k_pip_chunks<<<nb_of(4 * (size_t)W * NC), PTPB, 0, s>>>(ws.Q[fin].as<ge>(), ws.off[fin].as<uint32_t>(),
                                                          ws.len[fin].as<uint32_t>(), c, W, ws.V.as<ge>(), dtab);
-    k_pip_window<<<W, PTPB, 0, s>>>(ws.V.as<ge>(), (int)NC, ws.Sw.as<ge>());
-    k_pip_horner<<<1, 64, 0, s>>>(ws.Sw.as<ge>(), W, c, result);
+    k_pip_window<<<W, PTPB, 0, s>>>(ws.V.as<ge>(), (int)NC, Sw + w0);
     return hipGetLastError();
+}
+
+// The windows run as two halves, top half first, each with its own workspace.  The caller's
+// stream carries the throughput work (sort + bucket trees of both halves, then the bottom half's
+// chunks); a side stream carries the latency-bound chains: the top half's chunks + window trees
+// + its part of the Horner chain (~126 dependent doublings) overlap the bottom half's bucket
+// trees, and only the bottom half's chunks and Horner part remain at the end.  Same values,
+// same bits.
+std::map<hipStream_t, PipWs*> g_pip_lo;
+hipError_t msm_pippenger(ge* result, const fe* scal, const ge* P, size_t n, int c, const ge* dtab, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    PipWs*& wsp = g_pip[s];
+    PipWs*& wlp = g_pip_lo[s];
+    if (!wsp) {
+        wsp = new PipWs();
+        wlp = new PipWs();
+        PIP_RET(hipHostMalloc(&wsp->host_max, sizeof(unsigned)));
+        PIP_RET(hipHostMalloc(&wlp->host_max, sizeof(unsigned)));
+        // a high-priority stream: HIP spreads streams over a few hardware queues, and one that
+        // shared the caller's queue would serialize the chains behind the bottom half again
+        int lo_pr = 0, hi_pr = 0;
+        PIP_RET(hipDeviceGetStreamPriorityRange(&lo_pr, &hi_pr));
+        PIP_RET(hipStreamCreateWithPriority(&wsp->side, hipStreamNonBlocking, hi_pr));
+        for (auto& e : wsp->ev) PIP_RET(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    PipWs& hi = *wsp;
+    PipWs& lo = *wlp;
+    const int W = (256 + c - 1) / c, wm = W / 2;
+    PIP_RET(hi.Sw.need((size_t)W * sizeof(ge)));
+    PIP_RET(hi.Tmid.need(sizeof(ge)));
+    ge* Sw = hi.Sw.as<ge>();
+    PIP_RET(pip_buckets(hi, scal, P, n, c, wm, W, s));
+    PIP_RET(hipEventRecord(hi.ev[1], s));
+    PIP_RET(hipStreamWaitEvent(hi.side, hi.ev[1], 0));
+    PIP_RET(pip_finish(hi, c, wm, W, Sw, dtab, hi.side));
+    k_pip_horner<<<1, 64, 0, hi.side>>>(Sw, W - 1, wm, c, nullptr, hi.Tmid.as<ge>());
+    PIP_RET(hipGetLastError());
+    PIP_RET(pip_buckets(lo, scal, P, n, c, 0, wm, s));
+    PIP_RET(pip_finish(lo, c, 0, wm, Sw, dtab, s));
+    PIP_RET(hipEventRecord(hi.ev[2], s));
+    PIP_RET(hipStreamWaitEvent(hi.side, hi.ev[2], 0));
+    k_pip_horner<<<1, 64, 0, hi.side>>>(Sw, wm - 1, 0, c, hi.Tmid.as<ge>(), result);
+    PIP_RET(hipGetLastError());
+    PIP_RET(hipEventRecord(hi.ev[3], hi.side));
+    PIP_RET(hipStreamWaitEvent(s, hi.ev[3], 0));          // the result is ready in the caller's stream order
+    return hipSuccess;
 }
 
 }  // namespace bp
