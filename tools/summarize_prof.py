@@ -20,6 +20,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name):
+    name = name.replace("(anonymous namespace)::", "")
     return name.split("(")[0].replace("bp::", "")
 
 
