@@ -670,3 +670,40 @@ def test_msm_batch_ipa4096_commitment(bp, golden, oracle):
     torch.cuda.synchronize()
     for k in range(3):
         assert np.array_equal(out.cpu().numpy().view(np.uint64)[k], d["P"])
+
+
+def test_pipeline_sorted_and_unsorted_batches_in_flight(bp, oracle):
+    """Lane-sorted (B >= 64) and index-order (B < 64) batches share ticks: every proof's verdict,
+    P and check point equal the oracle's, whatever batch order and tick they ride in."""
+    import torch
+    from cudabulletproof_amd import synth
+    n = 16
+    G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+    g, h = oracle.gh()
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    pipe = bp.VerifyPipeline(130, n, T(G), T(H), T(h))
+    outs = []
+    for i, B in enumerate((100, 5, 130, 64, 3)):
+        arrays = synth.proofs(B, n, seed=700 + i)
+        batch = bp.RangeProofBatch.from_numpy(n, arrays, dev)
+        ok = torch.zeros(B, dtype=torch.uint8, device=dev)
+        P = torch.zeros(B, 16, dtype=torch.int64, device=dev)
+        chk = torch.zeros(B, 16, dtype=torch.int64, device=dev)
+        pipe.push(batch, ok, P, chk)
+        outs.append((arrays, ok, P, chk, batch))
+    pipe.flush()
+    torch.cuda.synchronize()
+    for arrays, ok, P, chk, _ in outs:
+        B = len(arrays["t"])
+        ok, P, chk = ok.cpu().numpy().astype(bool), P.cpu().numpy().view(np.uint64), chk.cpu().numpy().view(np.uint64)
+        for p in range(0, B, 7):   # a sample of each batch
+            head = np.concatenate([arrays[k][p] for k in ("V", "A", "S", "T1", "T2")] +
+                                  [np.zeros(8, np.uint64), arrays["t"][p], arrays["c"][p], arrays["x"][p]])
+            okr, Pr, chkr, _, _ = oracle.cuda_range_proof_verify(head, arrays["V"][p], n, arrays["a"][p],
+                                                                 arrays["b"][p], arrays["L"][p], arrays["R"][p],
+                                                                 G, H, g, h)
+            assert ok[p] == okr and np.array_equal(P[p], Pr), (B, p)
+            if okr:
+                assert np.array_equal(chk[p], chkr), (B, p)
+    pipe.close()
