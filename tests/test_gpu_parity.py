@@ -158,7 +158,8 @@ def test_batch_verify_matches_reference(bp, golden, n):
 @pytest.mark.parametrize("n,B,ab_len", [(64, 48, 1), (16, 40, 3), (4, 17, 2), (1, 9, 1), (256, 4, 1), (512, 3, 1),
                                         (1024, 2, 2),
                                         # B >= 64: lanes in chain-length order (the pipeline's lane sort)
-                                        (64, 72, 1), (16, 130, 2), (4, 64, 1)])
+                                        (64, 72, 1), (16, 130, 2), (4, 64, 1), (1, 70, 1), (2, 65, 1),
+                                        (128, 64, 1)])
 def test_batch_verify_synthetic_vs_oracle(bp, oracle, n, B, ab_len):
     from cudabulletproof_amd import synth
     arrays = synth.proofs(B, n, seed=1000 + n)
