@@ -209,7 +209,9 @@ int hipbp_msm_batch(ge25519* results, const fe25519* scalars, const ge25519* poi
  * double-and-add + the canonical tree (hipbp_msm), and this arithmetic is not associative, so a
  * bucket regrouping yields different bits.  Its own result is fixed (stable bucket order, fixed
  * trees) and equals the C restatement oracle/bp_oracle.c orc_msm_pippenger.  Synchronizes the
- * stream once (the bucket-tree depth).  No reference counterpart. */
+ * stream twice (the bucket-tree depth of each half of the windows) and runs the Horner chain on
+ * an internal side stream that the caller's stream waits on before returning, so it cannot be
+ * captured into a graph.  No reference counterpart. */
 int hipbp_msm_pippenger(ge25519* result, const fe25519* scalars, const ge25519* points, size_t n,
                         int window_bits, void* stream);
 /* Canonical tree over n device points: for stride 1, 2, 4, ...: T[i] = Ndev(T[i] + T[i+stride])
