@@ -51,11 +51,15 @@ void launch_init_tables(ge* dtab, fe* two_i, int nmax, hipStream_t s) {
 // `perm` (nullable) maps lane -> item: the lanes of a wave take items of equal length, so no
 // lane idles while the longest scalar of its wave finishes (below).
 // `pm`: the point of item i is P[i % pm] (a batch of MSMs over the same points; pm = total for one).
-__global__ __launch_bounds__(TPB, 3) void k_msm_points(ge* pts, const fe* __restrict__ scal,
+#ifndef BP_MSM_TPB
+#define BP_MSM_TPB 256   // k_msm_points block size
+#endif
+constexpr int MSM_TPB = BP_MSM_TPB;
+__global__ __launch_bounds__(MSM_TPB, 768 / MSM_TPB) void k_msm_points(ge* pts, const fe* __restrict__ scal,
                                                     const ge* __restrict__ P, size_t total, size_t pm,
                                                     const uint32_t* __restrict__ perm,
                                                     const ge* __restrict__ dtab) {
-    __shared__ geq qs[TPB];
+    __shared__ geq qs[MSM_TPB];
     size_t i = gid();
     if (i >= total) return;
     if (perm) i = perm[i];
@@ -140,7 +144,7 @@ void launch_msm_points(ge* pts, const fe* scal, const ge* P, size_t m, uint32_t*
     } else {
         perm = nullptr;
     }
-    k_msm_points<<<blocks, TPB, 0, s>>>(pts, scal, P, m, pm, perm, dtab);
+    k_msm_points<<<(unsigned)((m + MSM_TPB - 1) / MSM_TPB), MSM_TPB, 0, s>>>(pts, scal, P, m, pm, perm, dtab);
 }
 
 // Canonical pairwise tree over S segments of m points: for stride 1,2,4,..:
