@@ -589,6 +589,7 @@ int hipbp_batch_range_proof_verify(const hipbp_proof_batch* batch, const ge25519
     hipError_t err;
     Engine* e = engine_or_null(&err);
     BP_RET_ON(err);
+    if (batch && batch->count == 0) return HIPBP_OK;   // nothing read or written: empty outputs may be null
     if (!G || !H || !h || !ok) { g_err = "null generator/output"; return HIPBP_ERR_ARG; }
     std::lock_guard<std::mutex> lk(e->mu);
     return run_verify(*e, batch, nullptr, G, H, h, ok, P_out, check_out, 1, pick(stream, *e));
@@ -600,6 +601,7 @@ int hipbp_batch_range_proof_verify_std(const hipbp_proof_batch* batch, const ge2
     hipError_t err;
     Engine* e = engine_or_null(&err);
     BP_RET_ON(err);
+    if (batch && batch->count == 0) return HIPBP_OK;   // nothing read or written: empty outputs may be null
     if (!G || !H || !g || !h || !ok) { g_err = "null generator/output"; return HIPBP_ERR_ARG; }
     std::lock_guard<std::mutex> lk(e->mu);
     return run_verify(*e, batch, nullptr, G, H, h, ok, P_out, check_out, 2, pick(stream, *e), g, flags_out,
@@ -612,6 +614,7 @@ int hipbp_batch_inner_product_verify(const hipbp_proof_batch* batch, const ge255
     hipError_t err;
     Engine* e = engine_or_null(&err);
     BP_RET_ON(err);
+    if (batch && batch->count == 0) return HIPBP_OK;   // nothing read or written: empty outputs may be null
     if (!P || !G || !H || !Q || !ok) { g_err = "null argument"; return HIPBP_ERR_ARG; }
     std::lock_guard<std::mutex> lk(e->mu);
     return run_verify(*e, batch, P, G, H, Q, ok, nullptr, check_out, 0, pick(stream, *e));

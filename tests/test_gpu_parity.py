@@ -708,3 +708,33 @@ def test_pipeline_sorted_and_unsorted_batches_in_flight(bp, oracle):
             if okr:
                 assert np.array_equal(chk[p], chkr), (B, p)
     pipe.close()
+
+
+# ----------------------------------------------------------------------------- empty inputs
+def test_empty_inputs_are_noops(bp):
+    """n = 0 / count = 0 through every entry point: no launch, no fault, outputs untouched
+    (the reference's n = 0 behaviour is an invalid 0-block launch; this is the defined form)."""
+    import ctypes
+    import torch
+    dev = torch.device("cuda:0")
+    out = np.full(16, 7, np.uint64)
+    z4, z16 = np.zeros((0, 4), np.uint64), np.zeros((0, 16), np.uint64)
+    sv, pv = bp.FieldVector(z4.ctypes.data, 0), bp.PointVector(z16.ctypes.data, 0)
+    bp.lib().cuda_point_vector_multi_scalar_mul(ctypes.c_void_p(out.ctypes.data), ctypes.byref(sv), ctypes.byref(pv))
+    assert (out == 7).all()
+    r = torch.full((16,), 7, dtype=torch.int64, device=dev)
+    e4 = torch.zeros(0, 4, dtype=torch.int64, device=dev)
+    e16 = torch.zeros(0, 16, dtype=torch.int64, device=dev)
+    bp.msm(r, e4, e16)
+    bp.msm_pippenger(r, e4, e16, 12)
+    bp.point_tree(r, e16)
+    bp.msm_batch(torch.zeros(0, 16, dtype=torch.int64, device=dev), e4, torch.zeros(3, 16, dtype=torch.int64, device=dev))
+    torch.cuda.synchronize()
+    assert (r.cpu() == 7).all()
+    from cudabulletproof_amd import synth
+    arrays = {k: v[:0] for k, v in synth.proofs(1, 16, seed=1).items()}
+    batch = bp.RangeProofBatch.from_numpy(16, arrays, dev)
+    G, H = torch.zeros(16, 16, dtype=torch.int64, device=dev), torch.zeros(16, 16, dtype=torch.int64, device=dev)
+    g = torch.zeros(16, dtype=torch.int64, device=dev)
+    bp.batch_range_proof_verify(batch, G, H, g, g, torch.zeros(0, dtype=torch.uint8, device=dev))
+    torch.cuda.synchronize()
