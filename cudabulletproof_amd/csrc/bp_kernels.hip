@@ -304,19 +304,29 @@ __device__ __forceinline__ ge folded_point(const VerifyWs& ws, int n, int r, siz
     return ge_norm_host(ge_add(f[3 * npp + m], f[npp + m]));
 }
 
-__device__ __forceinline__ void fold_task(const BatchView& bv, const VerifyWs& ws, int r, size_t p, int k,
-                                          geq* qslot, const ge* __restrict__ G, const ge* __restrict__ H,
-                                          const ge* __restrict__ dtab) {
+// One scalar multiplication of a tick: its scalar, its point, where the result goes and which
+// normalize it gets.  Every task kind only FILLS a job; k_terms then runs the one scalarmult call
+// site for all of them, so the launch carries one copy of the scalar-mult loops instead of one per
+// task kind (each copy is tens of KB of straight-line code: several copies live in one launch
+// thrash the instruction cache of CUs running waves of different kinds).
+struct SmJob {
+    fe s;
+    ge P;
+    ge* dst;
+    int dev_norm;   // 1: device normalize (MSM terms, kernels.cu:26-42), 0: host normalize
+};
+
+__device__ __forceinline__ void fold_job(const BatchView& bv, const VerifyWs& ws, int r, size_t p, int k,
+                                         const ge* __restrict__ G, const ge* __restrict__ H, SmJob& jb) {
     const int n = bv.n, np = n >> (r + 1), Lr = bv.L_len;
     int grp = k / np, j = k % np;
     const bool isH = grp == 1 || grp == 3;
     const int m = (grp == 1 || grp == 2) ? j + np : j;
-    fe s = (grp < 2) ? ws.uinv[p * Lr + r] : ws.u[p * Lr + r];
-    ge P;   // through registers (an aggregate copy from a flat pointer goes via scratch)
-    if (r == 0) P = isH ? H[m] : G[m];
-    else P = folded_point(ws, n, r, p, isH, m);
-    ge t = scalarmult<true>(s, P, qslot, dtab);
-    ws.fold[r & 1][p * (2 * n) + k] = ge_norm_host(t);
+    jb.s = (grp < 2) ? ws.uinv[p * Lr + r] : ws.u[p * Lr + r];
+    if (r == 0) jb.P = isH ? H[m] : G[m];
+    else jb.P = folded_point(ws, n, r, p, isH, m);
+    jb.dst = ws.fold[r & 1] + p * (2 * n) + k;
+    jb.dev_norm = 0;
 }
 
 // Per-lane class c item j -> stage0_task's item index (perm0 holds, per class range, the
@@ -360,9 +370,9 @@ __device__ __forceinline__ size_t stage0_item(const SlotDev& sd, size_t l) {
 //   [.., +7B)     mode 2: the polynomial identity's g^t, h^taux, V^z^2, g^delta, h^mu, T1^x, T2^x^2
 //                 (rp.cu:442-480), host normalize
 
-__device__ __forceinline__ void stage0_task(const SlotDev& sd, size_t i, geq* qslot, const ge* __restrict__ G,
-                                            const ge* __restrict__ H, const ge* __restrict__ g,
-                                            const ge* __restrict__ h, const ge* __restrict__ dtab) {
+__device__ __forceinline__ bool stage0_job(const SlotDev& sd, size_t i, const ge* __restrict__ G,
+                                          const ge* __restrict__ H, const ge* __restrict__ g,
+                                          const ge* __restrict__ h, SmJob& jb) {
     const BatchView& bv = sd.bv;
     const VerifyWs& ws = sd.ws;
     const size_t B = bv.B;
@@ -374,62 +384,65 @@ __device__ __forceinline__ void stage0_task(const SlotDev& sd, size_t i, geq* qs
         int k = (int)(i % n);
         size_t p = seg >> 1;
         bool isH = seg & 1;
-        fe s = isH ? ws.sH[p * n + k] : ws.sG[p];
-        ge r = scalarmult<true>(s, isH ? H[k] : G[k], qslot, dtab);
-        ws.msm_pts[i] = ge_norm_dev(r);
-        return;
+        jb.s = isH ? ws.sH[p * n + k] : ws.sG[p];
+        jb.P = isH ? H[k] : G[k];
+        jb.dst = ws.msm_pts + i;
+        jb.dev_norm = 1;
+        return true;
     }
     i -= nA;
     if (i < nB) {
-        fold_task(bv, ws, 0, i / (2 * n), (int)(i % (2 * n)), qslot, G, H, dtab);
-        return;
+        fold_job(bv, ws, 0, i / (2 * n), (int)(i % (2 * n)), G, H, jb);
+        return true;
     }
     i -= nB;
     if (i < 2 * B) {
         size_t p = i >> 1;
         bool isC = i & 1;
-        if (!isC && !sd.range_mode) return;
-        fe s = isC ? ws.sc[p * 4 + 3] : ws.sc[p * 4 + 0];
-        ge r = scalarmult<true>(s, *h, qslot, dtab);
-        ws.terms[p * 4 + 2 + (isC ? 1 : 0)] = ge_norm_host(r);
-        return;
+        if (!isC && !sd.range_mode) return false;
+        jb.s = isC ? ws.sc[p * 4 + 3] : ws.sc[p * 4 + 0];
+        jb.P = *h;
+        jb.dst = ws.terms + p * 4 + 2 + (isC ? 1 : 0);
+        jb.dev_norm = 0;
+        return true;
     }
     i -= 2 * B;
     size_t p = i / 7;
     int k = (int)(i % 7);
-    ge P;
-    if (k == 0 || k == 3) P = *g;
-    else if (k == 1 || k == 4) P = *h;
-    else if (k == 2) P = bv.V[p];
-    else if (k == 5) P = bv.T1[p];
-    else P = bv.T2[p];
-    ge r = scalarmult<true>(ws.psc[p * 8 + k], P, qslot, dtab);
-    ws.pterm[p * 8 + k] = ge_norm_host(r);
+    if (k == 0 || k == 3) jb.P = *g;
+    else if (k == 1 || k == 4) jb.P = *h;
+    else if (k == 2) jb.P = bv.V[p];
+    else if (k == 5) jb.P = bv.T1[p];
+    else jb.P = bv.T2[p];
+    jb.s = ws.psc[p * 8 + k];
+    jb.dst = ws.pterm + p * 8 + k;
+    jb.dev_norm = 0;
+    return true;
 }
 
 // range_proof_verify method 3 (rp.cu:568-580): chal * left, chal * right, host normalize.
 // The scalar is the raw SHA-256 digest bytes.  Items: 2p -> left, 2p+1 -> right.
-__device__ __forceinline__ void m3_task(const SlotDev& sd, size_t i, geq* qslot, const ge* __restrict__ dtab) {
-    size_t p = i >> 1;
-    ge P = sd.ws.lr[i];
-    ge r = scalarmult<true>(sd.ws.chal[p], P, qslot, dtab);
-    sd.ws.m3[i] = ge_norm_host(r);
+__device__ __forceinline__ void m3_job(const SlotDev& sd, size_t i, SmJob& jb) {
+    jb.s = sd.ws.chal[i >> 1];
+    jb.P = sd.ws.lr[i];
+    jb.dst = sd.ws.m3 + i;
+    jb.dev_norm = 0;
 }
 
 // a0*G'_0 and b0*H'_0 (crv:262-266).  Items: 2p -> a0*G', 2p+1 -> b0*H'.
-__device__ __forceinline__ void final_terms_task(const SlotDev& sd, size_t i, geq* qslot, const ge* __restrict__ G,
-                                                 const ge* __restrict__ H, const ge* __restrict__ dtab) {
+__device__ __forceinline__ void final_terms_job(const SlotDev& sd, size_t i, const ge* __restrict__ G,
+                                                const ge* __restrict__ H, SmJob& jb) {
     const BatchView& bv = sd.bv;
     const VerifyWs& ws = sd.ws;
     size_t p = i >> 1;
     bool isH = i & 1;
     const int n = bv.n;
-    fe s = ws.sc[p * 4 + (isH ? 2 : 1)];
-    ge P;   // G'_0 / H'_0 after the last round (formed from its terms), the generators when there is none
-    if (bv.L_len > 0) P = folded_point(ws, n, bv.L_len, p, isH, 0);
-    else P = isH ? H[0] : G[0];
-    ge t = scalarmult<true>(s, P, qslot, dtab);
-    ws.fin[p * 2 + (isH ? 1 : 0)] = ge_norm_host(t);
+    jb.s = ws.sc[p * 4 + (isH ? 2 : 1)];
+    // G'_0 / H'_0 after the last round (formed from its terms), the generators when there is none
+    if (bv.L_len > 0) jb.P = folded_point(ws, n, bv.L_len, p, isH, 0);
+    else jb.P = isH ? H[0] : G[0];
+    jb.dst = ws.fin + p * 2 + (isH ? 1 : 0);
+    jb.dev_norm = 0;
 }
 
 // Region lookup with constant indices only (a run-time index into the by-value kernel
@@ -734,22 +747,31 @@ __global__ __launch_bounds__(TPB, BP_TERMS_OCC) void k_terms(RegionList rl, cons
         const size_t B = sd.bv.B;
         if (sd.range_mode && l < B) prep_range_task(sd.bv, sd.ws, two_i, l, sd.range_mode);
         else prep_ipa_task(sd.bv, sd.ws, sd.range_mode ? l - B : l);
-    } else if (rg.kind == RK_STAGE0) {
-        const size_t it = stage0_item(sd, l);
-        if (it != SIZE_MAX) stage0_task(sd, it, &qs[threadIdx.x], G, H, g, h, dtab);
-    } else if (rg.kind == RK_M3) {
-        m3_task(sd, l, &qs[threadIdx.x], dtab);
-    } else if (rg.kind == RK_ROUND) {
-        const int np = sd.bv.n >> (rg.r + 1);
-        if (const uint32_t* pm = sd.permr[rg.r]) l = pm[l];
-        fold_task(sd.bv, sd.ws, rg.r, l / (4 * np), (int)(l % (4 * np)), &qs[threadIdx.x], G, H, dtab);
-    } else if (rg.kind == RK_FINAL_TERMS) {
-        if (sd.perm_ft) l = sd.perm_ft[l];
-        final_terms_task(sd, l, &qs[threadIdx.x], G, H, dtab);
     } else if (rg.kind == RK_POLY) {
         poly_task(sd, l);
-    } else {
+    } else if (rg.kind == RK_FINAL) {
         final_task(sd, l);
+    } else {
+        // the scalar-multiplication kinds: fill the job, then the one call site
+        SmJob jb;
+        bool live = true;
+        if (rg.kind == RK_STAGE0) {
+            const size_t it = stage0_item(sd, l);
+            live = it != SIZE_MAX && stage0_job(sd, it, G, H, g, h, jb);
+        } else if (rg.kind == RK_M3) {
+            m3_job(sd, l, jb);
+        } else if (rg.kind == RK_ROUND) {
+            const int np = sd.bv.n >> (rg.r + 1);
+            if (const uint32_t* pm = sd.permr[rg.r]) l = pm[l];
+            fold_job(sd.bv, sd.ws, rg.r, l / (4 * np), (int)(l % (4 * np)), G, H, jb);
+        } else {   // RK_FINAL_TERMS
+            if (sd.perm_ft) l = sd.perm_ft[l];
+            final_terms_job(sd, l, G, H, jb);
+        }
+        if (live) {
+            ge t = scalarmult<true>(jb.s, jb.P, &qs[threadIdx.x], dtab);
+            *jb.dst = jb.dev_norm ? ge_norm_dev(t) : ge_norm_host(t);
+        }
     }
 }
 
