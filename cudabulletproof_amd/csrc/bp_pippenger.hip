@@ -360,7 +360,10 @@ hipError_t msm_pippenger(ge* result, const fe* scal, const ge* P, size_t n, int 
     }
     PipWs& hi = *wsp;
     PipWs& lo = *wlp;
-    const int W = (256 + c - 1) / c, wm = W / 2;
+#ifndef BP_PIP_SPLIT8
+#define BP_PIP_SPLIT8 3   // the bottom part's share of the windows, in eighths (3: measured best)
+#endif
+    const int W = (256 + c - 1) / c, wm = (W * BP_PIP_SPLIT8) / 8 > 0 ? (W * BP_PIP_SPLIT8) / 8 : 1;
     PIP_RET(hi.Sw.need((size_t)W * sizeof(ge)));
     PIP_RET(hi.Tmid.need(sizeof(ge)));
     ge* Sw = hi.Sw.as<ge>();
