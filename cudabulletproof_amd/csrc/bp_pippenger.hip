@@ -207,30 +207,56 @@ __global__ __launch_bounds__(64) void k_pip_horner(const ge* __restrict__ Sw, in
     if (threadIdx.x == 0) *out = T;
 }
 
-// chunk k of window w (one lane quad): buckets kM .. kM+M-1 -> V = S + (kM) R (orc_msm_pippenger);
-// (kM) R is ge25519_scalarmult's double-and-add on the scalar's raw bits, leading zeros from dtab.
+// A point moved across lane quads of one DPP row: CTRL 0x114 (row_shr:4, lane l takes l-4) or
+// 0x104 (row_shl:4, lane l takes l+4).
+template <int CTRL>
+__device__ __forceinline__ ge ge_row_move(const ge& a) {
+    auto mv = [](const fe& f) {
+        fe r;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)f.v[i], CTRL, 0xF, 0xF, true);
+            uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(f.v[i] >> 32), CTRL, 0xF, 0xF, true);
+            r.v[i] = (uint64_t)lo | ((uint64_t)hi << 32);
+        }
+        return r;
+    };
+    return ge{mv(a.X), mv(a.Y), mv(a.Z), mv(a.T)};
+}
+
+// chunk k of window w (one lane octet = two quads): buckets kM .. kM+M-1 -> V = S + (kM) R
+// (orc_msm_pippenger).  The running sums R = R + B_j, S = S + R are two chains: quad A walks R,
+// quad B walks S one step behind, fed each new R over DPP — both quads run the same point add in
+// lockstep on their own operands, 15 dependent adds instead of 29.  (kM) R is
+// ge25519_scalarmult's double-and-add on the scalar's raw bits, leading zeros from dtab.
 __global__ __launch_bounds__(PTPB) void k_pip_chunks(const ge* __restrict__ Q, const uint32_t* __restrict__ off,
                                                     const uint32_t* __restrict__ cnt, int c, int W, ge* V,
                                                     const ge* __restrict__ dtab) {
     const size_t NB = (size_t)1 << c, NC = NB / PM;
-    const size_t g = ((size_t)blockIdx.x * PTPB + threadIdx.x) >> 2;
-    if (g >= (size_t)W * NC) return;   // whole quads leave together
+    const size_t g = ((size_t)blockIdx.x * PTPB + threadIdx.x) >> 3;
+    if (g >= (size_t)W * NC) return;   // whole octets leave together
+    const bool qB = (threadIdx.x & 4) != 0;
     const size_t w = g / NC, k = g % NC, b0 = w * NB + k * PM;
-    ge R = bucket_sum(Q, off, cnt, b0 + PM - 1), S = R;
-    for (int j = PM - 2; j >= 1; j--) {
-        R = ge_op_quad<false>(R, bucket_sum(Q, off, cnt, b0 + j));
-        S = ge_op_quad<false>(S, R);
+    ge X = bucket_sum(Q, off, cnt, b0 + PM - 1);   // A: R = B_{M-1}; B: S = B_{M-1}
+    ge Rin = X;
+    for (int j = PM - 2; j >= 0; j--) {
+        // A: R_j = R_{j+1} + B_j (j = 0: the final R + B_0);  B: S = S + R_{j+1} (from j = M-3 on)
+        const ge y = qB ? Rin : bucket_sum(Q, off, cnt, b0 + j);
+        const ge res = ge_op_quad<false>(X, y);
+        if (!qB || j < PM - 2) X = res;
+        Rin = ge_row_move<0x114>(X);   // quad B takes quad A's new R
     }
-    R = ge_op_quad<false>(R, bucket_sum(Q, off, cnt, b0));
+    // A holds R, B holds S
     const uint64_t km = (uint64_t)k * PM;
     ge r = dtab[km ? 192 + __clzll(km) : 256];
     if (km)
         for (int i = 63 - __clzll(km); i >= 0; i--) {
             r = ge_op_quad<true>(r, r);
-            if ((km >> i) & 1) r = ge_op_quad<false>(r, R);
+            if ((km >> i) & 1) r = ge_op_quad<false>(r, X);
         }
+    const ge S = ge_row_move<0x104>(X);   // quad A takes quad B's S
     r = ge_op_quad<false>(S, r);
-    if ((threadIdx.x & 3) == 0) V[g] = r;
+    if ((threadIdx.x & 7) == 0) V[g] = r;
 }
 
 struct DBuf {
@@ -329,7 +355,7 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
 static hipError_t pip_finish(PipWs& ws, int c, int w0, int w1, ge* Sw, const ge* dtab, hipStream_t s) {
     const int W = w1 - w0, fin = ws.fin;
     const size_t NC = ((size_t)1 << c) / PM;
-    k_pip_chunks<<<nb_of(4 * (size_t)W * NC), PTPB, 0, s>>>(ws.Q[fin].as<ge>(), ws.off[fin].as<uint32_t>(),
+    k_pip_chunks<<<nb_of(8 * (size_t)W * NC), PTPB, 0, s>>>(ws.Q[fin].as<ge>(), ws.off[fin].as<uint32_t>(),
                                                          ws.len[fin].as<uint32_t>(), c, W, ws.V.as<ge>(), dtab);
     k_pip_window<<<W, PTPB, 0, s>>>(ws.V.as<ge>(), (int)NC, Sw + w0);
     return hipGetLastError();
