@@ -41,11 +41,23 @@ def build(force=False, verbose=False):
         t = os.path.getmtime(LIB_PATH)
         if all(os.path.getmtime(d) <= t for d in deps):
             return LIB_PATH
-    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
-           "-o", LIB_PATH + ".tmp"] + srcs
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.check_call(cmd)
+    import tempfile
+    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result"]
+    with tempfile.TemporaryDirectory() as tmp:   # one hipcc per source, in parallel, then link
+        objs = [os.path.join(tmp, os.path.basename(s) + ".o") for s in srcs]
+        procs = []
+        for s, o in zip(srcs, objs):
+            cmd = ["hipcc"] + flags + ["-c", s, "-o", o]
+            if verbose:
+                print(" ".join(cmd))
+            procs.append((cmd, subprocess.Popen(cmd)))
+        for cmd, p in procs:
+            if p.wait() != 0:
+                raise subprocess.CalledProcessError(p.returncode, cmd)
+        cmd = ["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB_PATH + ".tmp"] + objs
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.check_call(cmd)
     os.replace(LIB_PATH + ".tmp", LIB_PATH)
     return LIB_PATH
 

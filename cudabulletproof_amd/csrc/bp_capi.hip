@@ -126,8 +126,19 @@ struct Engine {
     bp::ge* dtab = nullptr;
     bp::fe* two_i = nullptr;
     int two_cap = 0;
-    // single-call staging
+    // single-call staging (Part 1: the engine's own stream, synchronous calls)
     Buf h2d[8], scratch[8];
+    // MSM / point-tree workspaces, one set per stream: the Part-2 calls run asynchronously on
+    // the caller's stream, so two MSMs on two streams (or an async MSM and a Part-1 call on the
+    // engine stream) must never share buffers.  [0] per-point terms, [1..2] block roots,
+    // [3..4] tree ping-pong, [5] lane order, [6] sort bins.
+    struct MsmBufs { Buf b[7]; };
+    std::map<hipStream_t, MsmBufs*> msm_ws;
+    Buf* msm_bufs(hipStream_t s) {
+        MsmBufs*& m = msm_ws[s];
+        if (!m) m = new MsmBufs();
+        return m->b;
+    }
     // prover workspaces (hipbp_batch_generate_range_proof), one per stream so batches on
     // different streams overlap (one batch's latency-bound stages under another's term launch)
     struct ProverBufs { Buf b[19]; };
@@ -403,10 +414,13 @@ struct Pipeline {
             size_t sz2[6] = {B * 8 * 32, B * 8 * 128, B * 2 * 128, B * 32, B * 2 * 128, B};
             for (int i = 0; i < 6; i++)
                 if ((r = sl.b[14 + i].need(sz2[i])) != hipSuccess) return r;
+            if ((r = sl.b[21].need(B * 3 * 128)) != hipSuccess) return r;
             w.psc = sl.b[14].as<bp::fe>(); w.pterm = sl.b[15].as<bp::ge>(); w.lr = sl.b[16].as<bp::ge>();
             w.chal = sl.b[17].as<bp::fe>(); w.m3 = sl.b[18].as<bp::ge>(); w.rflags = sl.b[19].as<uint8_t>();
+            w.pbase = sl.b[21].as<bp::ge>();
         } else {
             w.psc = nullptr; w.pterm = nullptr; w.lr = nullptr; w.chal = nullptr; w.m3 = nullptr; w.rflags = nullptr;
+            w.pbase = nullptr;
         }
         return hipSuccess;
     }
@@ -505,6 +519,22 @@ struct Pipeline {
     }
 };
 
+// `count` canonical-tree MSMs of n points each on stream s, in s's own workspace.
+hipError_t msm_run(Engine& e, bp::ge* results, const bp::fe* scalars, const bp::ge* points, size_t n, size_t count,
+                   hipStream_t s) {
+    const size_t tot = n * count, nb = count * ((n + 255) / 256);
+    Buf* w = e.msm_bufs(s);
+    hipError_t err;
+    if ((err = w[0].need(tot * sizeof(bp::ge))) != hipSuccess) return err;
+    if ((err = w[1].need(nb * sizeof(bp::ge))) != hipSuccess) return err;
+    if ((err = w[2].need(nb * sizeof(bp::ge))) != hipSuccess) return err;
+    if ((err = w[5].need(tot * sizeof(uint32_t))) != hipSuccess) return err;
+    if ((err = w[6].need(bp::MSM_BINS * sizeof(unsigned))) != hipSuccess) return err;
+    bp::launch_msm_full(results, scalars, points, n, w[0].as<bp::ge>(), w[1].as<bp::ge>(), w[2].as<bp::ge>(),
+                        w[5].as<uint32_t>(), w[6].as<unsigned>(), e.dtab, s, count);
+    return hipGetLastError();
+}
+
 // One-shot verify of a whole batch on `s` (push + drain of a cached pipeline).
 int run_verify(Engine& e, const hipbp_proof_batch* batch, const ge25519* P_in, const ge25519* G, const ge25519* H,
                const ge25519* h, uint8_t* ok, ge25519* P_out, ge25519* chk_out, int range_mode, hipStream_t s,
@@ -513,10 +543,19 @@ int run_verify(Engine& e, const hipbp_proof_batch* batch, const ge25519* P_in, c
     if (rc != HIPBP_OK || batch->count == 0) return rc;
     if (range_mode) BP_RET_ON(e.ensure_two((int)batch->n));
     auto key = std::make_tuple(s, (int)batch->n, range_mode);
-    Pipeline*& pl = e.pipes[key];
-    if (!pl) {
+    Pipeline* pl = nullptr;
+    auto it = e.pipes.find(key);
+    if (it != e.pipes.end()) {
+        pl = it->second;
+    } else {   // cached only once fully initialised (a failed init is released, never reused)
         pl = new Pipeline();
-        BP_RET_ON(pl->init(&e, s, batch->count, (int)batch->n, range_mode));
+        hipError_t ierr = pl->init(&e, s, batch->count, (int)batch->n, range_mode);
+        if (ierr != hipSuccess) {
+            pl->release();
+            delete pl;
+            BP_RET_ON(ierr);
+        }
+        e.pipes[key] = pl;
     }
     pl->G = (const bp::ge*)G;
     pl->H = (const bp::ge*)H;
@@ -681,15 +720,8 @@ int hipbp_msm(ge25519* result, const fe25519* scalars, const ge25519* points, si
     if (n == 0) return HIPBP_OK;
     if (!result || !scalars || !points) { g_err = "null argument"; return HIPBP_ERR_ARG; }
     std::lock_guard<std::mutex> lk(e->mu);
-    size_t nb = (n + 255) / 256;
-    BP_RET_ON(e->scratch[0].need(n * sizeof(bp::ge)));
-    BP_RET_ON(e->scratch[1].need(nb * sizeof(bp::ge)));
-    BP_RET_ON(e->scratch[2].need(nb * sizeof(bp::ge)));
-    BP_RET_ON(e->scratch[6].need(n * sizeof(uint32_t)));
-    BP_RET_ON(e->scratch[7].need(bp::MSM_BINS * sizeof(unsigned)));
-    bp::launch_msm_full((bp::ge*)result, (const bp::fe*)scalars, (const bp::ge*)points, n, e->scratch[0].as<bp::ge>(),
-                        e->scratch[1].as<bp::ge>(), e->scratch[2].as<bp::ge>(), e->scratch[6].as<uint32_t>(),
-                        e->scratch[7].as<unsigned>(), e->dtab, pick(stream, *e));
+    hipStream_t s = pick(stream, *e);
+    BP_RET_ON(msm_run(*e, (bp::ge*)result, (const bp::fe*)scalars, (const bp::ge*)points, n, 1, s));
     BP_RET_ON(hipGetLastError());
     return HIPBP_OK;
 }
@@ -703,15 +735,8 @@ int hipbp_msm_batch(ge25519* results, const fe25519* scalars, const ge25519* poi
     if (!results || !scalars || !points) { g_err = "null argument"; return HIPBP_ERR_ARG; }
     if (count > 0x7FFFFFFFull || n * count > 0xFFFFFFFFull) { g_err = "msm_batch: too many items"; return HIPBP_ERR_ARG; }
     std::lock_guard<std::mutex> lk(e->mu);
-    const size_t tot = n * count, nb = count * ((n + 255) / 256);
-    BP_RET_ON(e->scratch[0].need(tot * sizeof(bp::ge)));
-    BP_RET_ON(e->scratch[1].need(nb * sizeof(bp::ge)));
-    BP_RET_ON(e->scratch[2].need(nb * sizeof(bp::ge)));
-    BP_RET_ON(e->scratch[6].need(tot * sizeof(uint32_t)));
-    BP_RET_ON(e->scratch[7].need(bp::MSM_BINS * sizeof(unsigned)));
-    bp::launch_msm_full((bp::ge*)results, (const bp::fe*)scalars, (const bp::ge*)points, n, e->scratch[0].as<bp::ge>(),
-                        e->scratch[1].as<bp::ge>(), e->scratch[2].as<bp::ge>(), e->scratch[6].as<uint32_t>(),
-                        e->scratch[7].as<unsigned>(), e->dtab, pick(stream, *e), count);
+    hipStream_t s = pick(stream, *e);
+    BP_RET_ON(msm_run(*e, (bp::ge*)results, (const bp::fe*)scalars, (const bp::ge*)points, n, count, s));
     BP_RET_ON(hipGetLastError());
     return HIPBP_OK;
 }
@@ -805,10 +830,11 @@ int hipbp_point_tree(ge25519* result, const ge25519* points, size_t n, void* str
     if (!result || !points) { g_err = "null argument"; return HIPBP_ERR_ARG; }
     std::lock_guard<std::mutex> lk(e->mu);
     size_t nb = (n + 255) / 256;
-    BP_RET_ON(e->scratch[4].need(nb * sizeof(bp::ge)));
-    BP_RET_ON(e->scratch[5].need(nb * sizeof(bp::ge)));
-    bp::launch_tree_full((bp::ge*)result, (const bp::ge*)points, n, e->scratch[4].as<bp::ge>(),
-                         e->scratch[5].as<bp::ge>(), pick(stream, *e));
+    hipStream_t s = pick(stream, *e);
+    Buf* w = e->msm_bufs(s);
+    BP_RET_ON(w[3].need(nb * sizeof(bp::ge)));
+    BP_RET_ON(w[4].need(nb * sizeof(bp::ge)));
+    bp::launch_tree_full((bp::ge*)result, (const bp::ge*)points, n, w[3].as<bp::ge>(), w[4].as<bp::ge>(), s);
     BP_RET_ON(hipGetLastError());
     return HIPBP_OK;
 }
@@ -845,16 +871,7 @@ void cuda_point_vector_multi_scalar_mul(ge25519* result, const FieldVector* scal
     BP_EXIT_ON(e.h2d[2].need(sizeof(ge25519)));
     BP_EXIT_ON(hipMemcpyAsync(e.h2d[0].p, scalars->elements, n * sizeof(fe25519), hipMemcpyHostToDevice, e.stream));
     BP_EXIT_ON(hipMemcpyAsync(e.h2d[1].p, points->elements, n * sizeof(ge25519), hipMemcpyHostToDevice, e.stream));
-    size_t nb = (n + 255) / 256;
-    BP_EXIT_ON(e.scratch[0].need(n * sizeof(bp::ge)));
-    BP_EXIT_ON(e.scratch[1].need(nb * sizeof(bp::ge)));
-    BP_EXIT_ON(e.scratch[2].need(nb * sizeof(bp::ge)));
-    BP_EXIT_ON(e.scratch[6].need(n * sizeof(uint32_t)));
-    BP_EXIT_ON(e.scratch[7].need(bp::MSM_BINS * sizeof(unsigned)));
-    bp::launch_msm_full(e.h2d[2].as<bp::ge>(), e.h2d[0].as<bp::fe>(), e.h2d[1].as<bp::ge>(), n,
-                        e.scratch[0].as<bp::ge>(), e.scratch[1].as<bp::ge>(), e.scratch[2].as<bp::ge>(),
-                        e.scratch[6].as<uint32_t>(), e.scratch[7].as<unsigned>(), e.dtab, e.stream);
-    BP_EXIT_ON(hipGetLastError());
+    BP_EXIT_ON(msm_run(e, e.h2d[2].as<bp::ge>(), e.h2d[0].as<bp::fe>(), e.h2d[1].as<bp::ge>(), n, 1, e.stream));
     BP_EXIT_ON(hipMemcpyAsync(result, e.h2d[2].p, sizeof(ge25519), hipMemcpyDeviceToHost, e.stream));
     BP_EXIT_ON(hipStreamSynchronize(e.stream));
 }

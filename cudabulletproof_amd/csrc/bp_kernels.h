@@ -53,6 +53,8 @@ struct VerifyWs {
     fe* chal;      // [B]      SHA-256 of the sides' bytes (method 3 scalar, raw bytes)
     ge* m3;        // [B*2]    chal * left, chal * right
     uint8_t* rflags;   // [B]  bit0 V match, bit1 range check, bit2 methods 1|2
+    ge* pbase;     // [B*3]    V, T1, T2 copied by the prep task: stage 0 runs a tick after the push and
+               //          must not read the caller's batch (consumed by its own push)
 };
 
 // One batch in flight in the verify pipeline (device-resident copy, read by the tick kernels).

@@ -212,6 +212,9 @@ __device__ __forceinline__ void prep_std_task(const BatchView& bv, const VerifyW
     const ge& Vp = bv.Vp ? bv.Vp[p] : bv.V[p];
     bool vmatch = fe_eq(fe_canon(bv.V[p].X), fe_canon(Vp.X)) & fe_eq(fe_canon(bv.V[p].Y), fe_canon(Vp.Y));
     ws.rflags[p] = (uint8_t)((vmatch ? 1 : 0) | (range_ok ? 2 : 0));
+    ws.pbase[p * 3 + 0] = bv.V[p];
+    ws.pbase[p * 3 + 1] = bv.T1[p];
+    ws.pbase[p * 3 + 2] = bv.T2[p];
     fe* ps = ws.psc + p * 8;
     ps[0] = fe_canon(t);
     ps[1] = fe_canon(bv.taux[p]);
@@ -411,9 +414,9 @@ __device__ __forceinline__ bool stage0_job(const SlotDev& sd, size_t i, const ge
     int k = (int)(i % 7);
     if (k == 0 || k == 3) jb.P = *g;
     else if (k == 1 || k == 4) jb.P = *h;
-    else if (k == 2) jb.P = bv.V[p];
-    else if (k == 5) jb.P = bv.T1[p];
-    else jb.P = bv.T2[p];
+    else if (k == 2) jb.P = ws.pbase[p * 3 + 0];
+    else if (k == 5) jb.P = ws.pbase[p * 3 + 1];
+    else jb.P = ws.pbase[p * 3 + 2];
     jb.s = ws.psc[p * 8 + k];
     jb.dst = ws.pterm + p * 8 + k;
     jb.dev_norm = 0;

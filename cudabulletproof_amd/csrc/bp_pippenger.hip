@@ -278,7 +278,13 @@ struct PipWs {
     hipEvent_t ev[4] = {};   // [1] top half's buckets done, [2] bottom half done, [3] chain done
     int fin = 0;
 };
-std::map<hipStream_t, PipWs*> g_pip;   // per stream; callers hold the engine lock
+// Workspaces per (device, stream): torch's default stream is handle 0 on every device, so the
+// stream alone does not identify a workspace.  Each pair holds the top and bottom part's
+// workspaces.  g_pip_mu guards the map (engines of different devices hold different locks);
+// a workspace itself is used only under its device's engine lock.
+struct PipPair { PipWs hi, lo; };
+std::map<std::pair<int, hipStream_t>, PipPair*> g_pip;
+std::mutex g_pip_mu;
 
 inline unsigned nb_of(size_t items) { return (unsigned)((items + PTPB - 1) / PTPB); }
 }  // namespace
@@ -367,25 +373,41 @@ static hipError_t pip_finish(PipWs& ws, int c, int w0, int w1, ge* Sw, const ge*
 // + its part of the Horner chain (~126 dependent doublings) overlap the bottom half's bucket
 // trees, and only the bottom half's chunks and Horner part remain at the end.  Same values,
 // same bits.
-std::map<hipStream_t, PipWs*> g_pip_lo;
+static hipError_t pip_pair(PipPair** out, hipStream_t s) {
+    int dev = 0;
+    PIP_RET(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(g_pip_mu);
+    auto key = std::make_pair(dev, s);
+    auto it = g_pip.find(key);
+    if (it != g_pip.end()) { *out = it->second; return hipSuccess; }
+    PipPair* pp = new PipPair();
+    auto fail = [&](hipError_t e) {   // a half-made pair is never cached
+        if (pp->hi.host_max) (void)hipHostFree(pp->hi.host_max);
+        if (pp->lo.host_max) (void)hipHostFree(pp->lo.host_max);
+        delete pp;
+        return e;
+    };
+    hipError_t e;
+    if ((e = hipHostMalloc(&pp->hi.host_max, sizeof(unsigned))) != hipSuccess) return fail(e);
+    if ((e = hipHostMalloc(&pp->lo.host_max, sizeof(unsigned))) != hipSuccess) return fail(e);
+    // a high-priority stream: HIP spreads streams over a few hardware queues, and one that
+    // shared the caller's queue would serialize the chains behind the bottom half again
+    int lo_pr = 0, hi_pr = 0;
+    if ((e = hipDeviceGetStreamPriorityRange(&lo_pr, &hi_pr)) != hipSuccess) return fail(e);
+    if ((e = hipStreamCreateWithPriority(&pp->hi.side, hipStreamNonBlocking, hi_pr)) != hipSuccess) return fail(e);
+    for (auto& ev : pp->hi.ev)
+        if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return fail(e);
+    g_pip[key] = pp;
+    *out = pp;
+    return hipSuccess;
+}
+
 hipError_t msm_pippenger(ge* result, const fe* scal, const ge* P, size_t n, int c, const ge* dtab, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    PipWs*& wsp = g_pip[s];
-    PipWs*& wlp = g_pip_lo[s];
-    if (!wsp) {
-        wsp = new PipWs();
-        wlp = new PipWs();
-        PIP_RET(hipHostMalloc(&wsp->host_max, sizeof(unsigned)));
-        PIP_RET(hipHostMalloc(&wlp->host_max, sizeof(unsigned)));
-        // a high-priority stream: HIP spreads streams over a few hardware queues, and one that
-        // shared the caller's queue would serialize the chains behind the bottom half again
-        int lo_pr = 0, hi_pr = 0;
-        PIP_RET(hipDeviceGetStreamPriorityRange(&lo_pr, &hi_pr));
-        PIP_RET(hipStreamCreateWithPriority(&wsp->side, hipStreamNonBlocking, hi_pr));
-        for (auto& e : wsp->ev) PIP_RET(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    }
-    PipWs& hi = *wsp;
-    PipWs& lo = *wlp;
+    PipPair* pp = nullptr;
+    PIP_RET(pip_pair(&pp, s));
+    PipWs& hi = pp->hi;
+    PipWs& lo = pp->lo;
 #ifndef BP_PIP_SPLIT8
 #define BP_PIP_SPLIT8 3   // the bottom part's share of the windows, in eighths (3: measured best)
 #endif

@@ -193,7 +193,9 @@ typedef struct {
 int hipbp_batch_generate_range_proof(const hipbp_prove_input* in, const ge25519* G, const ge25519* H,
                                      const ge25519* g, const ge25519* h, hipbp_proof_out* out, void* stream);
 
-/* Canonical-tree MSM on device buffers. */
+/* Canonical-tree MSM on device buffers.  Asynchronous on `stream`; the MSM, MSM-batch
+ * and point-tree calls keep one workspace per (device, stream), so calls on different streams may
+ * run concurrently. */
 int hipbp_msm(ge25519* result, const fe25519* scalars, const ge25519* points, size_t n, void* stream);
 
 /* count independent canonical-tree MSMs of n points each over the SAME points (e.g. the IPA
@@ -211,7 +213,7 @@ int hipbp_msm_batch(ge25519* results, const fe25519* scalars, const ge25519* poi
  * trees) and equals the C restatement oracle/bp_oracle.c orc_msm_pippenger.  Synchronizes the
  * stream twice (the bucket-tree depth of each half of the windows) and runs the Horner chain on
  * an internal side stream that the caller's stream waits on before returning, so it cannot be
- * captured into a graph.  No reference counterpart. */
+ * captured into a graph.  Workspaces are per (device, stream).  No reference counterpart. */
 int hipbp_msm_pippenger(ge25519* result, const fe25519* scalars, const ge25519* points, size_t n,
                         int window_bits, void* stream);
 /* Canonical tree over n device points: for stride 1, 2, 4, ...: T[i] = Ndev(T[i] + T[i+stride])

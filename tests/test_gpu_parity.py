@@ -738,3 +738,74 @@ def test_empty_inputs_are_noops(bp):
     g = torch.zeros(16, dtype=torch.int64, device=dev)
     bp.batch_range_proof_verify(batch, G, H, g, g, torch.zeros(0, dtype=torch.uint8, device=dev))
     torch.cuda.synchronize()
+
+
+# ----------------------------------------------------------------------------- concurrency / lifetimes
+def test_msm_on_two_streams_at_once(bp, oracle):
+    """hipbp_msm / hipbp_msm_batch / hipbp_point_tree on two torch streams with no sync between
+    them, plus a Part-1 MSM on the engine stream in the middle: each stream has its own
+    workspace, so every result equals the serial (oracle) one."""
+    import torch
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    rng = np.random.default_rng(77)
+    n1, n2, n3 = 3000, 1100, 300
+    P1, P2, P3 = oracle.base_points(n1, 21), oracle.base_points(n2, 22), oracle.base_points(n3, 23)
+    s1, s2, s3 = rand_fe(rng, n1), rand_fe(rng, 3 * n2), rand_fe(rng, n3)
+    d1, d2, dp1, dp2 = T(s1), T(s2), T(P1), T(P2)
+    torch.cuda.synchronize()
+    st_a, st_b = torch.cuda.Stream(), torch.cuda.Stream()
+    r1 = torch.zeros(16, dtype=torch.int64, device=dev)
+    r2 = torch.zeros(3, 16, dtype=torch.int64, device=dev)
+    rt = torch.zeros(16, dtype=torch.int64, device=dev)
+    for _ in range(2):
+        bp.msm(r1, d1, dp1, stream=st_a)
+        bp.msm_batch(r2, d2, dp2, stream=st_b)
+        r3 = bp.cuda_point_vector_multi_scalar_mul(s3, P3)   # engine stream, synchronous
+        bp.point_tree(rt, dp1, stream=st_b)
+    torch.cuda.synchronize()
+    assert np.array_equal(r1.cpu().numpy().view(np.uint64), oracle.msm_canon(s1, P1))
+    out2 = r2.cpu().numpy().view(np.uint64)
+    for k in range(3):
+        assert np.array_equal(out2[k], oracle.msm_canon(s2[k * n2:(k + 1) * n2], P2)), k
+    assert np.array_equal(r3, oracle.msm_canon(s3, P3))
+    rt_ref = torch.zeros(16, dtype=torch.int64, device=dev)
+    bp.point_tree(rt_ref, dp1)
+    torch.cuda.synchronize()
+    assert np.array_equal(rt.cpu().numpy(), rt_ref.cpu().numpy())
+
+
+def test_pipeline_mode2_batch_overwritten_after_push(bp, oracle):
+    """range_proof_verify pipeline (mode 2): stage 0 runs a tick after the push, yet a batch is
+    consumed by its own push — the caller refills the batch tensors right after each push and
+    every result still equals the oracle's on the original proofs."""
+    import torch
+    from cudabulletproof_amd import synth
+    n, B = 16, 12
+    G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+    g, h = oracle.gh()
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    pipe = bp.VerifyPipeline(B, n, T(G), T(H), T(h), range_mode=2, g=T(g))
+    rng = np.random.default_rng(5)
+    runs = []
+    for i in range(3):
+        arrays = synth.proofs(B, n, seed=900 + i)
+        arrays["taux"] = rand_fe(rng, B, top=False)
+        arrays["mu"] = rand_fe(rng, B, top=False)
+        batch = bp.RangeProofBatch.from_numpy(n, arrays, dev)
+        outs = (torch.zeros(B, dtype=torch.uint8, device=dev), torch.zeros(B, 16, dtype=torch.int64, device=dev),
+                torch.zeros(B, 16, dtype=torch.int64, device=dev), torch.zeros(B, dtype=torch.uint8, device=dev),
+                torch.zeros(B, 4, 16, dtype=torch.int64, device=dev))
+        pipe.push(batch, outs[0], outs[1], outs[2], flags_out=outs[3], poly_out=outs[4])
+        for k in bp.RangeProofBatch.FIELDS + ("taux", "mu"):   # same stream, after the push
+            getattr(batch, k).fill_(0x5A5A)
+        runs.append((arrays, outs))
+    pipe.flush()
+    torch.cuda.synchronize()
+    u = lambda t: t.cpu().numpy().view(np.uint64)
+    for arrays, (ok, P, chk, fl, poly) in runs:
+        heads = np.concatenate([arrays[k] for k in ("V", "A", "S", "T1", "T2", "taux", "mu", "t", "c", "x")], axis=1)
+        res = (ok.cpu().numpy().astype(bool), u(P), u(chk), fl.cpu().numpy(), u(poly))
+        _check_std_vs_oracle(oracle, n, arrays, heads, G, H, g, h, res)
+    pipe.close()
