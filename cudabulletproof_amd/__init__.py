@@ -491,6 +491,11 @@ class VerifyPipeline:
     def flush(self):
         _chk(lib().hipbp_pipeline_flush(_c(self.h)))
 
+    def prefix_tables(self, bits):
+        """hipbp_pipeline_prefix_tables: fixed-base prefix tables of the generators (same bits,
+        fewer point operations); bits = 0 frees them.  Synchronous; the pipeline must be idle."""
+        _chk(lib().hipbp_pipeline_prefix_tables(_c(self.h), ctypes.c_int(int(bits))))
+
     def close(self):
         if self.h:
             lib().hipbp_pipeline_destroy(_c(self.h))

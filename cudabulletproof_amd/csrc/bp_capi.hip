@@ -313,6 +313,9 @@ struct Pipeline {
     int lane_sort_mask = 7;   // bit 0 stage 0, bit 1 rounds, bit 2 final terms, bit 3 shortest first
     Buf sort_bins, sort_offs;
     bp::LaneSortPlan plan{};
+    // fixed-base prefix tables of G, H, h, g (hipbp_pipeline_prefix_tables; pbits = 0: none)
+    Buf ptab;
+    int pbits = 0;
     hipError_t init(Engine* eng, hipStream_t st, size_t mb, int nn, int range) {
         e = eng; s = st; maxB = mb; n = nn; range_mode = range;
         const char* ls = getenv("HIPBP_LANE_SORT");
@@ -342,6 +345,7 @@ struct Pipeline {
         if (host_dev) (void)hipHostFree(host_dev);
         if (sort_bins.p) (void)hipFree(sort_bins.p);
         if (sort_offs.p) (void)hipFree(sort_offs.p);
+        if (ptab.p) (void)hipFree(ptab.p);
     }
     // The batch's per-lane item sets (stage 0's per-lane part, the rounds whose scalar runs are
     // shorter than a wave, the final terms), their lane-order buffers and the sort plan.
@@ -445,6 +449,8 @@ struct Pipeline {
             nw.dev.poly_out = (bp::ge*)poly_out;
             nw.dev.range_mode = range_mode;
             nw.dev.lane_tree = lane_tree ? 1 : 0;
+            nw.dev.ptab = pbits ? ptab.as<bp::ge>() : nullptr;
+            nw.dev.pbits = pbits;
             BP_RET_ON(plan_sort(nw, head));
             BP_RET_ON(hipEventSynchronize(nw.copied));   // staging slot free again
             host_dev[head] = nw.dev;
@@ -702,6 +708,29 @@ int hipbp_pipeline_flush(void* handle) {
     if (!pl) { g_err = "null pipeline"; return HIPBP_ERR_ARG; }
     std::lock_guard<std::mutex> lk(pl->e->mu);
     return pl->flush();
+}
+
+int hipbp_pipeline_prefix_tables(void* handle, int bits) {
+    Pipeline* pl = (Pipeline*)handle;
+    if (!pl) { g_err = "null pipeline"; return HIPBP_ERR_ARG; }
+    if (bits < 0 || bits > bp::PREFIX_MAX_BITS) { g_err = "prefix bits must be 0..24"; return HIPBP_ERR_ARG; }
+    std::lock_guard<std::mutex> lk(pl->e->mu);
+    if (pl->busy()) { g_err = "prefix tables: pipeline has batches in flight (flush first)"; return HIPBP_ERR_ARG; }
+    BP_RET_ON(hipStreamSynchronize(pl->s));
+    pl->pbits = 0;
+    if (pl->ptab.p) {
+        BP_RET_ON(hipFree(pl->ptab.p));
+        pl->ptab.p = nullptr;
+        pl->ptab.cap = 0;
+    }
+    if (!bits) return HIPBP_OK;
+    const size_t bytes = ((size_t)(2 * pl->n + 2) << bits) * sizeof(bp::ge);
+    BP_RET_ON(pl->ptab.need(bytes));
+    bp::launch_prefix_tables(pl->ptab.as<bp::ge>(), pl->G, pl->H, pl->h, pl->g, pl->n, bits, pl->s);
+    BP_RET_ON(hipGetLastError());
+    BP_RET_ON(hipStreamSynchronize(pl->s));
+    pl->pbits = bits;
+    return HIPBP_OK;
 }
 
 int hipbp_pipeline_depth(void* handle) { return handle ? ((Pipeline*)handle)->D : 0; }

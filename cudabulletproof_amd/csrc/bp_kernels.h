@@ -75,6 +75,10 @@ struct SlotDev {
     uint32_t* perm0;
     uint32_t* permr[17];
     uint32_t* perm_ft;
+    // Fixed-base prefix tables of the pipeline's generators (nullable; ge25519_dev.h): base b's
+    // table is ptab[b << pbits ..], b = k for G_k, n + k for H_k, 2n for h (= Q), 2n + 1 for g.
+    const ge* ptab;
+    int pbits;
 };
 
 // Stage-0 lane layout (host and device).  stage0_task's items by class — the <sG,G>/<sH,H>
@@ -165,6 +169,9 @@ struct RegionList {
 enum KernelKind { KT_PREP = 0, KT_TERMS, KT_TREE, KT_COMBINE, KT_COUNT };
 
 void launch_init_tables(ge* dtab, fe* two_i, int nmax, hipStream_t s);
+// Prefix tables (SlotDev::ptab) of the bases G[0..n), H[0..n), h, g (g nullable: its rows are
+// left unwritten): tab[(2n + 2) << K].
+void launch_prefix_tables(ge* tab, const ge* G, const ge* H, const ge* h, const ge* g, int n, int K, hipStream_t s);
 void launch_terms(const RegionList& rl, const SlotDev* slots, const ge* G, const ge* H, const ge* g, const ge* h,
                   const ge* dtab, const fe* two_i, hipStream_t s);
 

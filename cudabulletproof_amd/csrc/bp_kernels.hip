@@ -45,6 +45,32 @@ void launch_init_tables(ge* dtab, fe* two_i, int nmax, hipStream_t s) {
     k_init_tables<<<1, 64, 0, s>>>(dtab, two_i, nmax);
 }
 
+// tab[b << K | p] = the first K steps of ge25519_scalarmult (curve25519_ops.cu:397-415) on base b
+// for a scalar whose top K bits are p, from the identity: one add(r, r) per bit and one add(r, P)
+// per set bit — the per-lane step of sm_lane_loop, so the same operations as the verify kernels.
+__global__ __launch_bounds__(TPB) void k_prefix_tables(ge* tab, const ge* __restrict__ G, const ge* __restrict__ H,
+                                                       const ge* __restrict__ h, const ge* __restrict__ g, int n,
+                                                       int K, size_t total) {
+    const size_t i = gid();
+    if (i >= total) return;
+    const size_t b = i >> K;
+    const uint32_t p = (uint32_t)(i & ((1ull << K) - 1));
+    const ge* P = b < (size_t)n ? &G[b] : b < 2 * (size_t)n ? &H[b - n] : b == 2 * (size_t)n ? h : g;
+    if (!P) return;
+    const geq q = ge_prep(*P);
+    ge r = ge_zero();
+    for (int j = K - 1; j >= 0; j--) {
+        r = ge_add_sel<false>(r, &q, false);
+        if ((p >> j) & 1) r = ge_add_sel<false>(r, &q, true);
+    }
+    tab[i] = r;
+}
+
+void launch_prefix_tables(ge* tab, const ge* G, const ge* H, const ge* h, const ge* g, int n, int K, hipStream_t s) {
+    const size_t total = (size_t)(2 * n + 2) << K;
+    k_prefix_tables<<<(unsigned)((total + TPB - 1) / TPB), TPB, 0, s>>>(tab, G, H, h, g, n, K, total);
+}
+
 // ------------------------------------------------------------------ MSM
 // pts[seg*m + i] = Ndev(scalarmult(rawbytes(scal[seg*m+i]), P[i])) — point_scalar_mul_kernel
 // (cuda_bulletproof_kernels.cu:26-42); the scalar bytes are the raw limbs (device tobytes).
@@ -317,6 +343,7 @@ struct SmJob {
     ge P;
     ge* dst;
     int dev_norm;   // 1: device normalize (MSM terms, kernels.cu:26-42), 0: host normalize
+    int base;       // the fixed base's prefix-table row (SlotDev::ptab), -1: none
 };
 
 __device__ __forceinline__ void fold_job(const BatchView& bv, const VerifyWs& ws, int r, size_t p, int k,
@@ -326,8 +353,12 @@ __device__ __forceinline__ void fold_job(const BatchView& bv, const VerifyWs& ws
     const bool isH = grp == 1 || grp == 3;
     const int m = (grp == 1 || grp == 2) ? j + np : j;
     jb.s = (grp < 2) ? ws.uinv[p * Lr + r] : ws.u[p * Lr + r];
-    if (r == 0) jb.P = isH ? H[m] : G[m];
-    else jb.P = folded_point(ws, n, r, p, isH, m);
+    if (r == 0) {
+        jb.P = isH ? H[m] : G[m];
+        jb.base = isH ? n + m : m;
+    } else {
+        jb.P = folded_point(ws, n, r, p, isH, m);
+    }
     jb.dst = ws.fold[r & 1] + p * (2 * n) + k;
     jb.dev_norm = 0;
 }
@@ -389,6 +420,7 @@ __device__ __forceinline__ bool stage0_job(const SlotDev& sd, size_t i, const ge
         bool isH = seg & 1;
         jb.s = isH ? ws.sH[p * n + k] : ws.sG[p];
         jb.P = isH ? H[k] : G[k];
+        jb.base = isH ? n + k : k;
         jb.dst = ws.msm_pts + i;
         jb.dev_norm = 1;
         return true;
@@ -405,6 +437,7 @@ __device__ __forceinline__ bool stage0_job(const SlotDev& sd, size_t i, const ge
         if (!isC && !sd.range_mode) return false;
         jb.s = isC ? ws.sc[p * 4 + 3] : ws.sc[p * 4 + 0];
         jb.P = *h;
+        jb.base = 2 * n;
         jb.dst = ws.terms + p * 4 + 2 + (isC ? 1 : 0);
         jb.dev_norm = 0;
         return true;
@@ -412,8 +445,8 @@ __device__ __forceinline__ bool stage0_job(const SlotDev& sd, size_t i, const ge
     i -= 2 * B;
     size_t p = i / 7;
     int k = (int)(i % 7);
-    if (k == 0 || k == 3) jb.P = *g;
-    else if (k == 1 || k == 4) jb.P = *h;
+    if (k == 0 || k == 3) { jb.P = *g; jb.base = 2 * n + 1; }
+    else if (k == 1 || k == 4) { jb.P = *h; jb.base = 2 * n; }
     else if (k == 2) jb.P = ws.pbase[p * 3 + 0];
     else if (k == 5) jb.P = ws.pbase[p * 3 + 1];
     else jb.P = ws.pbase[p * 3 + 2];
@@ -607,8 +640,10 @@ __device__ __forceinline__ int lane_key(const SlotDev& sd, int kind, int r, size
     const size_t B = bv.B;
     const int n = bv.n, Lr = bv.L_len;
     fe s;
+    int K = 0;   // the item's prefix-table width (its base is a generator)
     if (kind == SS_STAGE0) {
         size_t i = stage0_class_item(sd, r, j);
+        if (sd.ptab) K = sd.pbits;
         const size_t nA = sd.range_mode ? B * 2 * n : 0, nB = Lr > 0 ? B * 2 * n : 0;
         if (i < nA) {
             size_t seg = i / n, p = seg >> 1;
@@ -626,6 +661,8 @@ __device__ __forceinline__ int lane_key(const SlotDev& sd, int kind, int r, size
         } else {
             i -= nA + nB + 2 * B;
             s = ws.psc[(i / 7) * 8 + i % 7];
+            const int k = (int)(i % 7);
+            if (k == 2 || k == 5 || k == 6) K = 0;   // V, T1, T2: the proof's own points
         }
     } else if (kind == SS_ROUND) {
         const int np = n >> (r + 1);
@@ -635,7 +672,7 @@ __device__ __forceinline__ int lane_key(const SlotDev& sd, int kind, int r, size
     } else {
         s = ws.sc[(j >> 1) * 4 + ((j & 1) ? 2 : 1)];
     }
-    return sm_ops(s);
+    return sm_ops_prefix(s, K);
 }
 
 __device__ __forceinline__ int lane_set_of(const LaneSortPlan& pl, unsigned b, LaneSortPlan::Set& st) {
@@ -757,6 +794,7 @@ __global__ __launch_bounds__(TPB, BP_TERMS_OCC) void k_terms(RegionList rl, cons
     } else {
         // the scalar-multiplication kinds: fill the job, then the one call site
         SmJob jb;
+        jb.base = -1;
         bool live = true;
         if (rg.kind == RK_STAGE0) {
             const size_t it = stage0_item(sd, l);
@@ -772,7 +810,8 @@ __global__ __launch_bounds__(TPB, BP_TERMS_OCC) void k_terms(RegionList rl, cons
             final_terms_job(sd, l, G, H, jb);
         }
         if (live) {
-            ge t = scalarmult<true>(jb.s, jb.P, &qs[threadIdx.x], dtab);
+            const ge* pt = (sd.ptab && jb.base >= 0) ? sd.ptab + ((size_t)jb.base << sd.pbits) : nullptr;
+            ge t = scalarmult<true>(jb.s, jb.P, &qs[threadIdx.x], dtab, pt, pt ? sd.pbits : 0);
             *jb.dst = jb.dev_norm ? ge_norm_dev(t) : ge_norm_host(t);
         }
     }

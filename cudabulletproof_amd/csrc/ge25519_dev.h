@@ -95,10 +95,26 @@ BP_DEV int fe_clz256(const fe& s) {
 
 BP_DEV ge ld_ge(const ge* p) { return *p; }
 
+// Fixed-base prefix tables (optional, for points that are the same in every proof: the
+// generators G_i, H_i, g, h).  ptab[p], p < 2^K, is the state of ge25519_scalarmult on this base
+// after the top K bits of any scalar whose top K bits are p: the identity, then for each of
+// those bits one add(r, r) and, for a set bit, one add(r, P).  A scalar with fewer than K
+// leading zeros starts from ptab[top K bits] at bit 255 - K instead of from the identity at bit
+// 255: the remaining operations are the same ones in the same order, so the result has the same
+// bits.  (With K or more leading zeros the identity-doubling table dtab already covers them.)
+constexpr int PREFIX_MAX_BITS = 24;
+BP_DEV uint32_t prefix_index(const fe& s, int K) { return (uint32_t)(s.v[3] >> (64 - K)); }
+
 // Length of ge25519_scalarmult's add chain past the leading zeros: the per-lane loop runs
 // (256 - clz) doublings + popcount adds, and a wave runs as long as its longest lane.
 BP_DEV int sm_ops(const fe& s) {
     return (256 - fe_clz256(s)) + __popcll(s.v[0]) + __popcll(s.v[1]) + __popcll(s.v[2]) + __popcll(s.v[3]);
+}
+// The same with a K-bit prefix table for the base (K = 0: none).
+BP_DEV int sm_ops_prefix(const fe& s, int K) {
+    if (K <= 0 || fe_clz256(s) >= K) return sm_ops(s);
+    const uint64_t top = K == 64 ? 0 : (s.v[3] & (~0ull >> K));
+    return (256 - K) + __popcll(s.v[0]) + __popcll(s.v[1]) + __popcll(s.v[2]) + __popcll(top);
 }
 
 // q-side operand access.  QLDS = true: this lane's LDS slot, read at the point of use (the
@@ -205,7 +221,7 @@ BP_DEV uint32_t bs_next(BitStream& b) {
 // `s` holds the scalar's 256 bits (limb i = bytes 8i..8i+7, little-endian); `q` holds
 // ge_prep(P); `dtab` = the identity-doubling table (257 points).
 template <bool QLDS>
-BP_DEV ge sm_uniform(const fe& s_in, const geq* q, const ge* __restrict__ dtab) {
+BP_DEV ge sm_uniform(const fe& s_in, const geq* q, const ge* __restrict__ dtab, const ge* ptab, int K) {
     fe s;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
@@ -214,11 +230,14 @@ BP_DEV ge sm_uniform(const fe& s_in, const geq* q, const ge* __restrict__ dtab) 
         s.v[i] = (uint64_t)lo | ((uint64_t)hi << 32);
     }
     int lz = fe_clz256(s);
-    ge r = ld_ge(&dtab[lz]);
-    if (lz == 256) return r;
+    // the prefix start only when every lane has a table (the start bit must stay wave-uniform)
+    const bool pre = K > 0 && lz < K && __all(ptab != nullptr);
+    const int top = pre ? 255 - K : 255 - lz;
+    ge r = ld_ge(pre ? &ptab[prefix_index(s, K)] : &dtab[lz]);
+    if (top < 0) return r;
     const bool zone = __all(fe_is_one(qget<QLDS>(&q->Z)));
-    BitStream bs = bs_init(s, 255 - lz);
-    for (int i = 255 - lz; i >= 0; i--) {
+    BitStream bs = bs_init(s, top);
+    for (int i = top; i >= 0; i--) {
         r = ge_dbl(r);
         if (bs_next(bs)) r = ge_add_qp<QLDS>(r, q, zone);
     }
@@ -228,10 +247,11 @@ BP_DEV ge sm_uniform(const fe& s_in, const geq* q, const ge* __restrict__ dtab) 
 // Same function for a per-lane scalar: every iteration is one ge25519_add whose second
 // operand is either r itself (the doubling) or P, so no lane idles on the other's branch.
 template <bool QLDS, bool ZONE>
-BP_DEV ge sm_lane_loop(const fe& s, const geq* q, const ge* __restrict__ dtab) {
+BP_DEV ge sm_lane_loop(const fe& s, const geq* q, const ge* __restrict__ dtab, const ge* ptab, int K) {
     int lz = fe_clz256(s);
-    ge r = ld_ge(&dtab[lz]);
-    int i = 255 - lz;          // index of the pending bit
+    const bool pre = K > 0 && lz < K && ptab != nullptr;
+    ge r = ld_ge(pre ? &ptab[prefix_index(s, K)] : &dtab[lz]);
+    int i = pre ? 255 - K : 255 - lz;   // index of the pending bit
     BitStream bs = bs_init(s, i < 0 ? 0 : i);
     uint32_t bit = i >= 0 ? bs_next(bs) : 0;
     bool add_phase = false;    // false: next op doubles; true: next op adds P
@@ -249,15 +269,17 @@ BP_DEV ge sm_lane_loop(const fe& s, const geq* q, const ge* __restrict__ dtab) {
 }
 
 template <bool QLDS>
-BP_DEV ge sm_lane(const fe& s, const geq* q, const ge* __restrict__ dtab) {
-    if (__all(fe_is_one(qget<QLDS>(&q->Z)))) return sm_lane_loop<QLDS, true>(s, q, dtab);
-    return sm_lane_loop<QLDS, false>(s, q, dtab);
+BP_DEV ge sm_lane(const fe& s, const geq* q, const ge* __restrict__ dtab, const ge* ptab, int K) {
+    if (__all(fe_is_one(qget<QLDS>(&q->Z)))) return sm_lane_loop<QLDS, true>(s, q, dtab, ptab, K);
+    return sm_lane_loop<QLDS, false>(s, q, dtab, ptab, K);
 }
 
 // Wave-level dispatch: uniform scalar -> scalar-branch loop, else the per-lane loop.
 // QLDS: `slot` is this lane's LDS slot and receives ge_prep(P); otherwise q stays in VGPRs.
+// ptab / K: this lane's base's prefix table (nullable) and its width in bits (0: none).
 template <bool QLDS>
-BP_DEV ge scalarmult(const fe& s, const ge& P, geq* slot, const ge* __restrict__ dtab) {
+BP_DEV ge scalarmult(const fe& s, const ge& P, geq* slot, const ge* __restrict__ dtab, const ge* ptab = nullptr,
+                     int K = 0) {
     geq qreg;
     const geq* q;
     if (QLDS) {
@@ -280,8 +302,8 @@ BP_DEV ge scalarmult(const fe& s, const ge& P, geq* slot, const ge* __restrict__
         uint32_t lo = (uint32_t)s.v[i], hi = (uint32_t)(s.v[i] >> 32);
         same &= (lo == __builtin_amdgcn_readfirstlane(lo)) & (hi == __builtin_amdgcn_readfirstlane(hi));
     }
-    if (__all(same)) return sm_uniform<QLDS>(s, q, dtab);
-    return sm_lane<QLDS>(s, q, dtab);
+    if (__all(same)) return sm_uniform<QLDS>(s, q, dtab, ptab, K);
+    return sm_lane<QLDS>(s, q, dtab, ptab, K);
 }
 
 }  // namespace bp

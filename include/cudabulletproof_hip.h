@@ -165,6 +165,16 @@ int hipbp_pipeline_push(void* pipeline, const hipbp_proof_batch* batch /* NULL =
                         uint8_t* flags_out /* range_mode 2, nullable */, ge25519* poly_out /* idem */);
 int hipbp_pipeline_flush(void* pipeline);
 int hipbp_pipeline_depth(void* pipeline);
+/* Fixed-base prefix tables for the pipeline's generators (no reference counterpart; an
+ * additive speed-up with the same bits).  bits = K in 1..24 builds, for each of the 2n + 2
+ * bases G_i, H_i, h, g, the state of ge25519_scalarmult after every possible top-K-bit prefix
+ * of a scalar ((2n + 2) * 2^K * 128 bytes of device memory: 17.4 GB at n = 64, K = 20).  The
+ * scalar multiplications on those bases (the two MSMs, fold round 0, t*h, c*Q, the polynomial
+ * terms on g and h) then start at bit 255 - K from the table entry; the operations after it are
+ * unchanged, so every output has the same bits.  Built from the generator CONTENTS at this call
+ * (synchronous); the caller must not change G/H/g/h afterwards while tables are on.  bits = 0
+ * frees them.  The pipeline must be idle (flushed). */
+int hipbp_pipeline_prefix_tables(void* pipeline, int bits);
 void hipbp_pipeline_destroy(void* pipeline);
 
 /* ---- prover: generate_range_proof (bulletproof_range_proof.cu:1159) + inner_product_prove

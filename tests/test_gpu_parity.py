@@ -809,3 +809,77 @@ def test_pipeline_mode2_batch_overwritten_after_push(bp, oracle):
         res = (ok.cpu().numpy().astype(bool), u(P), u(chk), fl.cpu().numpy(), u(poly))
         _check_std_vs_oracle(oracle, n, arrays, heads, G, H, g, h, res)
     pipe.close()
+
+
+@pytest.mark.parametrize("n,B,mode,K", [(16, 70, 1, 8), (64, 66, 1, 12), (16, 9, 2, 5), (64, 64, 2, 10),
+                                        (4, 5, 1, 1), (16, 6, 0, 9)])
+def test_pipeline_prefix_tables_same_bits(bp, oracle, n, B, mode, K):
+    """hipbp_pipeline_prefix_tables: the generators' scalar multiplications start from a table
+    entry at bit 255 - K; every output (verdict, P, check point, mode-2 flags and polynomial
+    sides) is bit-identical to the table-free pipeline, and a sample equals the oracle."""
+    import torch
+    from cudabulletproof_amd import synth
+    G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+    g, h = oracle.gh()
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    arrays = synth.proofs(B, n, seed=40 + n + K)
+    rng = np.random.default_rng(K)
+    arrays["taux"] = rand_fe(rng, B, top=False)
+    arrays["mu"] = rand_fe(rng, B, top=False)
+    arrays["t"][0] = 0                              # zero scalar: the dtab path beside the table path
+    arrays["t"][1, 3] = np.uint64(1) << np.uint64(63 - K)   # exactly K leading zeros
+    arrays["t"][1, :3] = 0
+    arrays["a"][:, 0] = arrays["t"]
+    arrays["c"][:] = arrays["t"]
+    Pg = T(oracle.base_points(B, 9))                # mode 0: given P
+    outs = []
+    for bits in (0, K):
+        pipe = bp.VerifyPipeline(B, n, T(G), T(H), T(h), range_mode=mode, g=T(g) if mode == 2 else None)
+        if bits:
+            pipe.prefix_tables(bits)
+        batch = bp.RangeProofBatch.from_numpy(n, arrays, dev)
+        o = [torch.zeros(B, dtype=torch.uint8, device=dev), torch.zeros(B, 16, dtype=torch.int64, device=dev),
+             torch.zeros(B, 16, dtype=torch.int64, device=dev), torch.zeros(B, dtype=torch.uint8, device=dev),
+             torch.zeros(B, 4, 16, dtype=torch.int64, device=dev)]
+        if mode == 0:
+            pipe.push(batch, o[0], None, o[2], P_in=Pg)
+        elif mode == 1:
+            pipe.push(batch, o[0], o[1], o[2])
+        else:
+            pipe.push(batch, o[0], o[1], o[2], flags_out=o[3], poly_out=o[4])
+        pipe.flush()
+        torch.cuda.synchronize()
+        outs.append([x.cpu() for x in o])
+        pipe.close()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    if mode == 1:
+        ok, P = outs[1][0].numpy().astype(bool), outs[1][1].numpy().view(np.uint64)
+        for p in range(0, B, 5):
+            head = np.concatenate([arrays[k][p] for k in ("V", "A", "S", "T1", "T2")] +
+                                  [np.zeros(8, np.uint64), arrays["t"][p], arrays["c"][p], arrays["x"][p]])
+            okr, Pr, _, _, _ = oracle.cuda_range_proof_verify(head, arrays["V"][p], n, arrays["a"][p], arrays["b"][p],
+                                                              arrays["L"][p], arrays["R"][p], G, H, g, h)
+            assert ok[p] == okr and np.array_equal(P[p], Pr), p
+
+
+def test_prefix_tables_reject_busy_and_bad_bits(bp, oracle):
+    import torch
+    from cudabulletproof_amd import synth
+    n = 16
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+    _, h = oracle.gh()
+    pipe = bp.VerifyPipeline(4, n, T(G), T(H), T(h))
+    with pytest.raises(bp.BulletproofError):
+        pipe.prefix_tables(25)
+    batch = bp.RangeProofBatch.from_numpy(n, synth.proofs(4, n, seed=3), dev)
+    pipe.push(batch, torch.zeros(4, dtype=torch.uint8, device=dev))
+    with pytest.raises(bp.BulletproofError):
+        pipe.prefix_tables(4)
+    pipe.flush()
+    pipe.prefix_tables(4)
+    pipe.prefix_tables(0)
+    pipe.close()
