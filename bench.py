@@ -61,7 +61,7 @@ def parse():
     ap.add_argument("--proofs", choices=["prover", "synthetic"], default="prover",
                     help="verify inputs: proofs made by the GPU prover from random 64-bit values (default) "
                          "or proof-shaped random data")
-    ap.add_argument("--prefix-bits", type=int, default=20,
+    ap.add_argument("--prefix-bits", type=int, default=22,
                     help="fixed-base prefix tables of the generators (hipbp_pipeline_prefix_tables; "
                          "0 = off): one-time setup, same bits")
     ap.add_argument("--rehearse", action="store_true",
@@ -163,11 +163,14 @@ def cpu_model():
     return "unknown"
 
 
-def pmc(kernel, key):
-    """A per-launch PMC figure for `kernel` from the committed rocprofv3 summary, if present."""
+def pmc(kernel, key, config=None):
+    """A per-launch PMC figure for `kernel` from the committed rocprofv3 summary, if present and
+    (when `config` is given) collected on the same bench configuration."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(path))
+        if config is not None and d.get("config") != config:
+            return None
         return d.get(kernel, {}).get(key)
     except (OSError, ValueError):
         return None
@@ -347,6 +350,7 @@ def main():
         cpu = cpu_baseline(args.n, args.cpu_seconds, args.cpu_procs)
     if args.rehearse:   # N>1 code path on a 1-GPU box: every rank on cuda:0, gloo instead of RCCL
         local = 0
+        args.prefix_bits = min(args.prefix_bits, 16)   # every rank's tables share the one GPU
     if world > 1:
         torch.cuda.set_device(local)
         if args.rehearse:
@@ -444,20 +448,21 @@ def main():
     ab_batch = alg_bytes(dom, B, n, 1)
     per_launch = ab_batch * args.steps / launches if ab_batch else None
     achieved = (per_launch / (avg_ms * 1e-3)) / 1e9 if per_launch else None
+    pcfg = {"batch_per_gpu": B, "n": n, "prefix_bits": prefix["bits"] if prefix else 0}
     roofline = {
         "bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": pmc(dom, "bytes_per_launch"),
+        "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": pmc(dom, "bytes_per_launch", pcfg),
         "avg_launch_ms": avg_ms, "launches": launches,
         "kernel_ms_share": {k: round(v / sum(kern_ms.values()), 4) for k, v in kern_ms.items()},
         "binding": "VALU integer (not HBM, not MFMA): see DESIGN.md and valu_roofline",
         "scalar_mults_per_s": value * sm_per_verify(n),
     }
-    vi = pmc(dom, "valu_instr_per_launch")
+    vi = pmc(dom, "valu_instr_per_launch", pcfg)
     valu_roofline = {
         "kernel": dom, "unit": "wave64 VALU instr/s", "peak": VALU_PEAK_WINSTR,
         "instr_per_launch": vi, "achieved": vi / (avg_ms * 1e-3) if vi else None,
         "frac": vi / (avg_ms * 1e-3) / VALU_PEAK_WINSTR if vi else None,
-        "valu_busy_pct": pmc(dom, "valu_busy_pct"),
+        "valu_busy_pct": pmc(dom, "valu_busy_pct", pcfg), "pmc_config": pcfg,
         "source": "SQ_INSTS_VALU per steady-state launch (profiles/pmc_traffic.json) / live HIP-event launch time",
     }
 

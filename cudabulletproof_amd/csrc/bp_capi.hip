@@ -500,6 +500,7 @@ struct Pipeline {
             }
         }
         if (overflow) { g_err = "pipeline region list overflow (internal)"; return HIPBP_ERR_ARG; }
+        if (tr.total >= (1ull << 32)) { g_err = "pipeline tick exceeds 2^32 lanes (batch too large for n)"; return HIPBP_ERR_ARG; }
         if (tm) tm->mark(bp::KT_TERMS, false, s);
         bp::launch_terms(tr, slots_dev, G, H, g ? g : h, h, e->dtab, e->two_i, s);
         if (tm) tm->mark(bp::KT_TERMS, true, s);

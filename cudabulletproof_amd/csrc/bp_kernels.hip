@@ -346,52 +346,56 @@ struct SmJob {
     int base;       // the fixed base's prefix-table row (SlotDev::ptab), -1: none
 };
 
-__device__ __forceinline__ void fold_job(const BatchView& bv, const VerifyWs& ws, int r, size_t p, int k,
+// Lane and item indices of a tick are 32-bit (the host keeps a launch below 2^32 lanes) and n
+// is a power of two: index arithmetic is shifts and masks, no 64-bit division sequences.
+__device__ __forceinline__ int log2n(int n) { return __ffs(n) - 1; }
+
+__device__ __forceinline__ void fold_job(const BatchView& bv, const VerifyWs& ws, int r, uint32_t p, uint32_t k,
                                          const ge* __restrict__ G, const ge* __restrict__ H, SmJob& jb) {
-    const int n = bv.n, np = n >> (r + 1), Lr = bv.L_len;
-    int grp = k / np, j = k % np;
+    const int n = bv.n, lnp = log2n(n) - r - 1, np = 1 << lnp, Lr = bv.L_len;   // np = n >> (r + 1)
+    const int grp = (int)(k >> lnp), j = (int)(k & (np - 1));
     const bool isH = grp == 1 || grp == 3;
     const int m = (grp == 1 || grp == 2) ? j + np : j;
-    jb.s = (grp < 2) ? ws.uinv[p * Lr + r] : ws.u[p * Lr + r];
+    jb.s = (grp < 2) ? ws.uinv[(size_t)p * Lr + r] : ws.u[(size_t)p * Lr + r];
     if (r == 0) {
         jb.P = isH ? H[m] : G[m];
         jb.base = isH ? n + m : m;
     } else {
         jb.P = folded_point(ws, n, r, p, isH, m);
     }
-    jb.dst = ws.fold[r & 1] + p * (2 * n) + k;
+    jb.dst = ws.fold[r & 1] + (size_t)p * (2 * n) + k;
     jb.dev_norm = 0;
 }
 
 // Per-lane class c item j -> stage0_task's item index (perm0 holds, per class range, the
 // items of that class in chain-length order: perm0[pl_base(c) + j]).
-__device__ __forceinline__ size_t stage0_class_item(const SlotDev& sd, int c, size_t j) {
-    const size_t B = sd.bv.B;
-    const int n = sd.bv.n;
-    const size_t nA = sd.range_mode ? B * 2 * n : 0, nB = sd.bv.L_len > 0 ? B * 2 * n : 0;
-    if (c == 0) return n >= 64 ? (j / n) * 2 * n + n + j % n : j;
+__device__ __forceinline__ uint32_t stage0_class_item(const SlotDev& sd, int c, uint32_t j) {
+    const uint32_t B = (uint32_t)sd.bv.B;
+    const int n = sd.bv.n, ln = log2n(n);
+    const uint32_t nA = sd.range_mode ? B << (ln + 1) : 0, nB = sd.bv.L_len > 0 ? B << (ln + 1) : 0;
+    if (c == 0) return n >= 64 ? ((j >> ln) << (ln + 1)) + n + (j & (n - 1)) : j;
     if (c == 1) return nA + j;
     if (c == 2) return nA + nB + j;
     return nA + nB + 2 * B + j;
 }
 
 // Stage-0 lane -> stage0_task item, or SIZE_MAX for a padding lane (stage0_lanes).
-__device__ __forceinline__ size_t stage0_item(const SlotDev& sd, size_t l) {
-    const size_t B = sd.bv.B;
-    const int n = sd.bv.n;
+__device__ __forceinline__ uint32_t stage0_item(const SlotDev& sd, uint32_t l) {
+    const uint32_t B = (uint32_t)sd.bv.B;
+    const int n = sd.bv.n, ln = log2n(n);
     const Stage0Lanes z = stage0_lanes(B, n, sd.bv.L_len, sd.range_mode);
-    if (l < z.U) {
-        const size_t nG = sd.range_mode ? B * n : 0;
-        if (l < nG) return (l / n) * 2 * n + l % n;     // <sG,G> segment of proof l / n
-        return (sd.range_mode ? B * 2 * n : 0) + (l - nG);
+    if (l < (uint32_t)z.U) {
+        const uint32_t nG = sd.range_mode ? B << ln : 0;
+        if (l < nG) return ((l >> ln) << (ln + 1)) + (l & (n - 1));   // <sG,G> segment of proof l / n
+        return (sd.range_mode ? B << (ln + 1) : 0) + (l - nG);
     }
     int c = 0;
-    size_t base = 0;   // class c's offset in perm0
+    uint32_t base = 0;   // class c's offset in perm0
 #pragma unroll
     for (int k = 1; k < 4; k++)
-        if (l >= z.off[k]) { c = k; base += z.size[k - 1]; }
-    const size_t j = l - z.off[c];
-    if (j >= z.size[c]) return SIZE_MAX;
+        if (l >= (uint32_t)z.off[k]) { c = k; base += (uint32_t)z.size[k - 1]; }
+    const uint32_t j = l - (uint32_t)z.off[c];
+    if (j >= (uint32_t)z.size[c]) return UINT32_MAX;
     return stage0_class_item(sd, c, sd.perm0 ? sd.perm0[base + j] : j);
 }
 
@@ -404,21 +408,21 @@ __device__ __forceinline__ size_t stage0_item(const SlotDev& sd, size_t l) {
 //   [.., +7B)     mode 2: the polynomial identity's g^t, h^taux, V^z^2, g^delta, h^mu, T1^x, T2^x^2
 //                 (rp.cu:442-480), host normalize
 
-__device__ __forceinline__ bool stage0_job(const SlotDev& sd, size_t i, const ge* __restrict__ G,
+__device__ __forceinline__ bool stage0_job(const SlotDev& sd, uint32_t i, const ge* __restrict__ G,
                                           const ge* __restrict__ H, const ge* __restrict__ g,
                                           const ge* __restrict__ h, SmJob& jb) {
     const BatchView& bv = sd.bv;
     const VerifyWs& ws = sd.ws;
-    const size_t B = bv.B;
-    const int n = bv.n;
-    const size_t nA = sd.range_mode ? B * 2 * n : 0;
-    const size_t nB = bv.L_len > 0 ? B * 2 * n : 0;
+    const uint32_t B = (uint32_t)bv.B;
+    const int n = bv.n, ln = log2n(n);
+    const uint32_t nA = sd.range_mode ? B << (ln + 1) : 0;
+    const uint32_t nB = bv.L_len > 0 ? B << (ln + 1) : 0;
     if (i < nA) {
-        size_t seg = i / n;
-        int k = (int)(i % n);
-        size_t p = seg >> 1;
-        bool isH = seg & 1;
-        jb.s = isH ? ws.sH[p * n + k] : ws.sG[p];
+        const uint32_t seg = i >> ln;
+        const int k = (int)(i & (n - 1));
+        const uint32_t p = seg >> 1;
+        const bool isH = seg & 1;
+        jb.s = isH ? ws.sH[(size_t)p * n + k] : ws.sG[p];
         jb.P = isH ? H[k] : G[k];
         jb.base = isH ? n + k : k;
         jb.dst = ws.msm_pts + i;
@@ -427,38 +431,38 @@ __device__ __forceinline__ bool stage0_job(const SlotDev& sd, size_t i, const ge
     }
     i -= nA;
     if (i < nB) {
-        fold_job(bv, ws, 0, i / (2 * n), (int)(i % (2 * n)), G, H, jb);
+        fold_job(bv, ws, 0, i >> (ln + 1), i & (2 * n - 1), G, H, jb);
         return true;
     }
     i -= nB;
     if (i < 2 * B) {
-        size_t p = i >> 1;
-        bool isC = i & 1;
+        const uint32_t p = i >> 1;
+        const bool isC = i & 1;
         if (!isC && !sd.range_mode) return false;
-        jb.s = isC ? ws.sc[p * 4 + 3] : ws.sc[p * 4 + 0];
+        jb.s = isC ? ws.sc[(size_t)p * 4 + 3] : ws.sc[(size_t)p * 4 + 0];
         jb.P = *h;
         jb.base = 2 * n;
-        jb.dst = ws.terms + p * 4 + 2 + (isC ? 1 : 0);
+        jb.dst = ws.terms + (size_t)p * 4 + 2 + (isC ? 1 : 0);
         jb.dev_norm = 0;
         return true;
     }
     i -= 2 * B;
-    size_t p = i / 7;
-    int k = (int)(i % 7);
+    const uint32_t p = i / 7u;
+    const int k = (int)(i - 7u * p);
     if (k == 0 || k == 3) { jb.P = *g; jb.base = 2 * n + 1; }
     else if (k == 1 || k == 4) { jb.P = *h; jb.base = 2 * n; }
-    else if (k == 2) jb.P = ws.pbase[p * 3 + 0];
-    else if (k == 5) jb.P = ws.pbase[p * 3 + 1];
-    else jb.P = ws.pbase[p * 3 + 2];
-    jb.s = ws.psc[p * 8 + k];
-    jb.dst = ws.pterm + p * 8 + k;
+    else if (k == 2) jb.P = ws.pbase[(size_t)p * 3 + 0];
+    else if (k == 5) jb.P = ws.pbase[(size_t)p * 3 + 1];
+    else jb.P = ws.pbase[(size_t)p * 3 + 2];
+    jb.s = ws.psc[(size_t)p * 8 + k];
+    jb.dst = ws.pterm + (size_t)p * 8 + k;
     jb.dev_norm = 0;
     return true;
 }
 
 // range_proof_verify method 3 (rp.cu:568-580): chal * left, chal * right, host normalize.
 // The scalar is the raw SHA-256 digest bytes.  Items: 2p -> left, 2p+1 -> right.
-__device__ __forceinline__ void m3_job(const SlotDev& sd, size_t i, SmJob& jb) {
+__device__ __forceinline__ void m3_job(const SlotDev& sd, uint32_t i, SmJob& jb) {
     jb.s = sd.ws.chal[i >> 1];
     jb.P = sd.ws.lr[i];
     jb.dst = sd.ws.m3 + i;
@@ -466,18 +470,18 @@ __device__ __forceinline__ void m3_job(const SlotDev& sd, size_t i, SmJob& jb) {
 }
 
 // a0*G'_0 and b0*H'_0 (crv:262-266).  Items: 2p -> a0*G', 2p+1 -> b0*H'.
-__device__ __forceinline__ void final_terms_job(const SlotDev& sd, size_t i, const ge* __restrict__ G,
+__device__ __forceinline__ void final_terms_job(const SlotDev& sd, uint32_t i, const ge* __restrict__ G,
                                                 const ge* __restrict__ H, SmJob& jb) {
     const BatchView& bv = sd.bv;
     const VerifyWs& ws = sd.ws;
-    size_t p = i >> 1;
+    const uint32_t p = i >> 1;
     bool isH = i & 1;
     const int n = bv.n;
-    jb.s = ws.sc[p * 4 + (isH ? 2 : 1)];
+    jb.s = ws.sc[(size_t)p * 4 + (isH ? 2 : 1)];
     // G'_0 / H'_0 after the last round (formed from its terms), the generators when there is none
     if (bv.L_len > 0) jb.P = folded_point(ws, n, bv.L_len, p, isH, 0);
     else jb.P = isH ? H[0] : G[0];
-    jb.dst = ws.fin + p * 2 + (isH ? 1 : 0);
+    jb.dst = ws.fin + (size_t)p * 2 + (isH ? 1 : 0);
     jb.dev_norm = 0;
 }
 
@@ -642,7 +646,7 @@ __device__ __forceinline__ int lane_key(const SlotDev& sd, int kind, int r, size
     fe s;
     int K = 0;   // the item's prefix-table width (its base is a generator)
     if (kind == SS_STAGE0) {
-        size_t i = stage0_class_item(sd, r, j);
+        size_t i = stage0_class_item(sd, r, (uint32_t)j);
         if (sd.ptab) K = sd.pbits;
         const size_t nA = sd.range_mode ? B * 2 * n : 0, nB = Lr > 0 ? B * 2 * n : 0;
         if (i < nA) {
@@ -796,18 +800,19 @@ __global__ __launch_bounds__(TPB, BP_TERMS_OCC) void k_terms(RegionList rl, cons
         SmJob jb;
         jb.base = -1;
         bool live = true;
+        uint32_t li = (uint32_t)l;   // < 2^32: Pipeline::push keeps a tick below 2^32 lanes
         if (rg.kind == RK_STAGE0) {
-            const size_t it = stage0_item(sd, l);
-            live = it != SIZE_MAX && stage0_job(sd, it, G, H, g, h, jb);
+            const uint32_t it = stage0_item(sd, li);
+            live = it != UINT32_MAX && stage0_job(sd, it, G, H, g, h, jb);
         } else if (rg.kind == RK_M3) {
-            m3_job(sd, l, jb);
+            m3_job(sd, li, jb);
         } else if (rg.kind == RK_ROUND) {
-            const int np = sd.bv.n >> (rg.r + 1);
-            if (const uint32_t* pm = sd.permr[rg.r]) l = pm[l];
-            fold_job(sd.bv, sd.ws, rg.r, l / (4 * np), (int)(l % (4 * np)), G, H, jb);
+            const int l4 = log2n(sd.bv.n) - rg.r + 1;   // 4 n' = 2^l4 items per proof
+            if (const uint32_t* pm = sd.permr[rg.r]) li = pm[li];
+            fold_job(sd.bv, sd.ws, rg.r, li >> l4, li & ((1u << l4) - 1), G, H, jb);
         } else {   // RK_FINAL_TERMS
-            if (sd.perm_ft) l = sd.perm_ft[l];
-            final_terms_job(sd, l, G, H, jb);
+            if (sd.perm_ft) li = sd.perm_ft[li];
+            final_terms_job(sd, li, G, H, jb);
         }
         if (live) {
             const ge* pt = (sd.ptab && jb.base >= 0) ? sd.ptab + ((size_t)jb.base << sd.pbits) : nullptr;

@@ -9,8 +9,8 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SMALL = ["--steps", "2", "--warmup", "1", "--batch", "128", "--msm-log2", "12", "--no-cpu", "--no-ipa",
-         "--no-prove"]
+SMALL = ["--steps", "2", "--warmup", "1", "--batch", "128", "--msm-log2", "12", "--prefix-bits", "12", "--no-cpu",
+         "--no-ipa", "--no-prove"]
 
 
 # rank 0's single-GPU legs (IPA, prover) while the other rank waits at the closing barrier

@@ -175,7 +175,16 @@ def main():
               "of kernel time the CUs' vector ALUs are issuing; VALUUtilization = active lanes per VALU instruction."]
     os.makedirs(os.path.dirname(out_md), exist_ok=True)
     open(out_md, "w").write("\n".join(lines) + "\n")
-    json.dump({"tag": tag, **traffic}, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
+    # the bench configuration the counters belong to: bench.py uses them only for the same one
+    cfg = None
+    try:
+        bc = json.loads(open(os.path.join(base, "bench_valu.json")).read().strip().splitlines()[-1])["config"]
+        cfg = {"batch_per_gpu": bc["batch_per_gpu"], "n": bc["n"],
+               "prefix_bits": (bc.get("prefix_tables") or {}).get("bits", 0)}
+    except (OSError, ValueError, KeyError, IndexError):
+        pass
+    json.dump({"tag": tag, "config": cfg, **traffic}, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"),
+              indent=1)
     print("\n".join(lines))
 
 
