@@ -297,7 +297,7 @@ def ipa_leg(args, dev):
                          "(crv:130)", "pipeline_depth": pipe.depth}
 
 
-def prove_leg(args, dev):
+def prove_leg(args, dev, gens=None):
     """§8(f) rank 1: generate_range_proof (rp.cu:1159) batched on the GPU, n = args.n, synthetic
     values and random scalars; proofs/s over whole batches (inputs resident in HBM)."""
     import torch
@@ -317,7 +317,7 @@ def prove_leg(args, dev):
     streams = [torch.cuda.Stream(dev, priority=max(hi, lo - k)) for k in range(ns)]
     torch.cuda.synchronize(dev)
     run = lambda k: bp.batch_generate_range_proof(n, pi["v"], pi["gamma"], pi["sL"], pi["sR"], pi["rnd"], Gd, Hd,
-                                                  gd, hd, stream=streams[k % ns])
+                                                  gd, hd, stream=streams[k % ns], gens=gens)
     outs = [run(k) for k in range(ns)]
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -329,7 +329,8 @@ def prove_leg(args, dev):
     return {"metric": f"{n}-bit range proofs generated/sec", "value": B / dt, "unit": "proofs/s", "batch": B,
             "streams": ns, "ms_per_batch": dt * 1e3, "valid": int(outs[0]["valid"].sum().item()),
             "deterministic_across_streams": same,
-            "semantics": "generate_range_proof + inner_product_prove + fix_inner_product_proof (rp.cu:1159)"}
+            "semantics": "generate_range_proof + inner_product_prove + fix_inner_product_proof (rp.cu:1159)",
+            "prefix_bits": gens.bits if gens is not None else 0}
 
 
 def main():
@@ -366,12 +367,23 @@ def main():
     G, H, g, h = synth.generators(n, dev)
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)
     Gd, Hd, gd, hd = T(G), T(H), T(g), T(h)
+    # one generator set (snapshot + fixed-base prefix tables): the input prover, the verify pipeline
+    # and the prover leg share it; one-time setup per generator set, outside every timed region
+    prefix = None
+    gens = None
+    if args.prefix_bits:
+        torch.cuda.synchronize(dev)
+        tp = time.perf_counter()
+        gens = bp.Generators(n, Gd, Hd, gd, hd, prefix_bits=args.prefix_bits)
+        prefix = {"bits": args.prefix_bits, "bases": 2 * n + 2, "GB": gens.nbytes_tables() / 1e9,
+                  "build_s": time.perf_counter() - tp}
     nb = 4
     if args.proofs == "prover":   # real 64-bit range proofs from the GPU prover (bit-exact with the reference's)
         batches = []
         for i in range(nb):
             pi = {k: T(v) for k, v in synth.prove_inputs(B, n, seed=1 + 1000 * rank + i).items()}
-            out = bp.batch_generate_range_proof(n, pi["v"], pi["gamma"], pi["sL"], pi["sR"], pi["rnd"], Gd, Hd, gd, hd)
+            out = bp.batch_generate_range_proof(n, pi["v"], pi["gamma"], pi["sL"], pi["sR"], pi["rnd"], Gd, Hd, gd, hd,
+                                                gens=gens)
             torch.cuda.synchronize(dev)
             batches.append(bp.RangeProofBatch(n, **{k: out[k] for k in bp.RangeProofBatch.FIELDS}))
     else:
@@ -383,15 +395,10 @@ def main():
     stream = torch.cuda.current_stream(dev)
     torch.cuda.synchronize(dev)
     pipe = None
-    prefix = None
     if args.mode == "pipeline":
         pipe = bp.VerifyPipeline(B, n, Gd, Hd, hd, stream=streams[0])
-        if args.prefix_bits:   # one-time setup per generator set, outside the timed region
-            tp = time.perf_counter()
-            pipe.prefix_tables(args.prefix_bits)
-            prefix = {"bits": args.prefix_bits, "bases": 2 * n + 2,
-                      "GB": (2 * n + 2) * (1 << args.prefix_bits) * GE_B / 1e9,
-                      "build_s": time.perf_counter() - tp}
+        if gens is not None:
+            pipe.use_gens(gens)
 
         def step(k):   # one tick: stage s of the batch pushed s ticks earlier, for every s
             pipe.push(batches[k % nb], oks[k % nb])
@@ -477,7 +484,7 @@ def main():
 
     prove = None
     if not args.no_prove and rank == 0:
-        prove = prove_leg(args, dev)
+        prove = prove_leg(args, dev, gens)
         prove["n_gpus"] = 1
 
 

@@ -371,7 +371,36 @@ def batch_inner_product_verify(batch, P, G, H, Q, ok, check_out=None, stream=Non
         _c(check_out.data_ptr()) if check_out is not None else None, _stream_ptr(stream)))
 
 
-def batch_generate_range_proof(n, v, gamma, sL, sR, rnd, G, H, g, h, stream=None):
+class Generators:
+    """hipbp_gens_create: a device snapshot of the generators G (n,16), H (n,16), g, h (16,) and,
+    with prefix_bits > 0, their fixed-base prefix tables ((2n + 2) * 2^bits * 128 bytes).  Pass it
+    to batch_generate_range_proof(gens=...) and VerifyPipeline.use_gens(); results keep their bits."""
+
+    def __init__(self, n, G, H, g, h, prefix_bits=0, stream=None):
+        L = lib()
+        L.hipbp_gens_create.restype = ctypes.c_void_p
+        self.n, self.bits = int(n), int(prefix_bits)
+        self.h = L.hipbp_gens_create(_sz(n), _c(G.data_ptr()), _c(H.data_ptr()), _c(g.data_ptr()), _c(h.data_ptr()),
+                                     ctypes.c_int(self.bits), _stream_ptr(stream))
+        if not self.h:
+            raise BulletproofError(L.hipbp_last_error().decode())
+
+    def nbytes_tables(self):
+        return (2 * self.n + 2) * (1 << self.bits) * 128 if self.bits else 0
+
+    def close(self):
+        if self.h:
+            lib().hipbp_gens_destroy(_c(self.h))
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def batch_generate_range_proof(n, v, gamma, sL, sR, rnd, G, H, g, h, stream=None, gens=None):
     """generate_range_proof (bulletproof_range_proof.cu:1159) over a batch, on the GPU.
 
     v, gamma (B,4); sL, sR (B,n,4); rnd (B,4,4) = alpha, rho, tau1, tau2: int64 CUDA tensors of the
@@ -395,9 +424,13 @@ def batch_generate_range_proof(n, v, gamma, sL, sR, rnd, G, H, g, h, stream=None
     ic = ProveInputC(B, int(n), *[t.data_ptr() for t in ins])
     oc = ProofOutC(*[out[k].data_ptr() if out[k].numel() else None for k in
                      ("V", "A", "S", "T1", "T2", "taux", "mu", "t", "c", "x", "a", "b", "L", "R", "valid")])
-    _chk(lib().hipbp_batch_generate_range_proof(ctypes.byref(ic), _c(G.data_ptr()), _c(H.data_ptr()),
-                                                _c(g.data_ptr()), _c(h.data_ptr()), ctypes.byref(oc),
-                                                _stream_ptr(stream)))
+    if gens is not None:   # the set's generators and prefix tables (G, H, g, h are not read)
+        _chk(lib().hipbp_batch_generate_range_proof_gens(ctypes.byref(ic), _c(gens.h), ctypes.byref(oc),
+                                                         _stream_ptr(stream)))
+    else:
+        _chk(lib().hipbp_batch_generate_range_proof(ctypes.byref(ic), _c(G.data_ptr()), _c(H.data_ptr()),
+                                                    _c(g.data_ptr()), _c(h.data_ptr()), ctypes.byref(oc),
+                                                    _stream_ptr(stream)))
     out["_keep"] = ins
     return out
 
@@ -490,6 +523,11 @@ class VerifyPipeline:
 
     def flush(self):
         _chk(lib().hipbp_pipeline_flush(_c(self.h)))
+
+    def use_gens(self, gens):
+        """hipbp_pipeline_use_gens: generators and prefix tables from a Generators set."""
+        _chk(lib().hipbp_pipeline_use_gens(_c(self.h), _c(gens.h)))
+        self._gens = gens
 
     def prefix_tables(self, bits):
         """hipbp_pipeline_prefix_tables: fixed-base prefix tables of the generators (same bits,

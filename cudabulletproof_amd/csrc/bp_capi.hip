@@ -268,6 +268,24 @@ bp::BatchView view_of(const hipbp_proof_batch* b) {
 //   accept)
 // A round-r item forms its own input point G'/H' from two round r-1 terms (each folded point
 // has exactly one consumer), so no launch of its own is needed for the fold combinations.
+// A generator set (hipbp_gens_create): a device snapshot of G[n] | H[n] | h | g and, optionally,
+// their fixed-base prefix tables (bp::launch_prefix_tables, same base order).
+struct Gens {
+    int device = -1;
+    size_t n = 0;
+    Buf gen, tab;
+    int bits = 0;
+    const bp::ge* G() const { return gen.as<bp::ge>(); }
+    const bp::ge* H() const { return gen.as<bp::ge>() + n; }
+    const bp::ge* h() const { return gen.as<bp::ge>() + 2 * n; }
+    const bp::ge* g() const { return gen.as<bp::ge>() + 2 * n + 1; }
+    void release() {
+        if (gen.p) (void)hipFree(gen.p);
+        if (tab.p) (void)hipFree(tab.p);
+        gen.p = tab.p = nullptr;
+    }
+};
+
 struct Pipeline {
     Engine* e = nullptr;
     hipStream_t s = nullptr;
@@ -313,9 +331,12 @@ struct Pipeline {
     int lane_sort_mask = 7;   // bit 0 stage 0, bit 1 rounds, bit 2 final terms, bit 3 shortest first
     Buf sort_bins, sort_offs;
     bp::LaneSortPlan plan{};
-    // fixed-base prefix tables of G, H, h, g (hipbp_pipeline_prefix_tables; pbits = 0: none)
+    // fixed-base prefix tables of G, H, h, g (hipbp_pipeline_prefix_tables: ptab, owned; or a
+    // generator set's, hipbp_pipeline_use_gens: ext_tab, borrowed); pbits = 0: none
     Buf ptab;
+    const bp::ge* ext_tab = nullptr;
     int pbits = 0;
+    const bp::ge* tables() const { return ext_tab ? ext_tab : ptab.as<bp::ge>(); }
     hipError_t init(Engine* eng, hipStream_t st, size_t mb, int nn, int range) {
         e = eng; s = st; maxB = mb; n = nn; range_mode = range;
         const char* ls = getenv("HIPBP_LANE_SORT");
@@ -449,7 +470,7 @@ struct Pipeline {
             nw.dev.poly_out = (bp::ge*)poly_out;
             nw.dev.range_mode = range_mode;
             nw.dev.lane_tree = lane_tree ? 1 : 0;
-            nw.dev.ptab = pbits ? ptab.as<bp::ge>() : nullptr;
+            nw.dev.ptab = pbits ? tables() : nullptr;
             nw.dev.pbits = pbits;
             BP_RET_ON(plan_sort(nw, head));
             BP_RET_ON(hipEventSynchronize(nw.copied));   // staging slot free again
@@ -719,6 +740,7 @@ int hipbp_pipeline_prefix_tables(void* handle, int bits) {
     if (pl->busy()) { g_err = "prefix tables: pipeline has batches in flight (flush first)"; return HIPBP_ERR_ARG; }
     BP_RET_ON(hipStreamSynchronize(pl->s));
     pl->pbits = 0;
+    pl->ext_tab = nullptr;
     if (pl->ptab.p) {
         BP_RET_ON(hipFree(pl->ptab.p));
         pl->ptab.p = nullptr;
@@ -786,8 +808,8 @@ int hipbp_msm_pippenger(ge25519* result, const fe25519* scalars, const ge25519* 
     return HIPBP_OK;
 }
 
-int hipbp_batch_generate_range_proof(const hipbp_prove_input* in, const ge25519* G, const ge25519* H,
-                                     const ge25519* g, const ge25519* h, hipbp_proof_out* out, void* stream) {
+static int prove_run(const hipbp_prove_input* in, const ge25519* G, const ge25519* H, const ge25519* g,
+                     const ge25519* h, const bp::ge* ptab, int pbits, hipbp_proof_out* out, void* stream) {
     hipError_t err;
     Engine* e = engine_or_null(&err);
     BP_RET_ON(err);
@@ -831,7 +853,7 @@ int hipbp_batch_generate_range_proof(const hipbp_prove_input* in, const ge25519*
                   prv[8].as<bp::fe>(), prv[9].as<bp::fe>(), prv[10].as<bp::fe>(), prv[11].as<bp::ge>(),
                   prv[12].as<bp::fe>(), prv[13].as<uint8_t>(), prv[14].as<uint32_t>(), prv[15].as<unsigned>(), cap,
                   prv[16].as<bp::ge>(), psort ? prv[17].as<uint32_t>() : nullptr,
-                  psort ? prv[18].as<unsigned>() : nullptr};
+                  psort ? prv[18].as<unsigned>() : nullptr, ptab, ptab ? pbits : 0};
     auto run = [&](int stage, int r) {
         bp::launch_prove(stage, r, pin, w, po, (const bp::ge*)G, (const bp::ge*)H, (const bp::ge*)g,
                          (const bp::ge*)h, e->dtab, e->two_i, s);
@@ -849,6 +871,88 @@ int hipbp_batch_generate_range_proof(const hipbp_prove_input* in, const ge25519*
     }
     run(bp::PS_FINAL, 0);
     BP_RET_ON(hipGetLastError());
+    return HIPBP_OK;
+}
+
+int hipbp_batch_generate_range_proof(const hipbp_prove_input* in, const ge25519* G, const ge25519* H,
+                                     const ge25519* g, const ge25519* h, hipbp_proof_out* out, void* stream) {
+    return prove_run(in, G, H, g, h, nullptr, 0, out, stream);
+}
+
+void* hipbp_gens_create(size_t n, const ge25519* G, const ge25519* H, const ge25519* g, const ge25519* h,
+                        int prefix_bits, void* stream) {
+    hipError_t err;
+    Engine* e = engine_or_null(&err);
+    if (!e) { g_err = std::string("engine: ") + hipGetErrorString(err); return nullptr; }
+    if (!is_pow2(n) || n > MAX_N || !G || !H || !g || !h) { g_err = "gens: bad n or null generator"; return nullptr; }
+    if (prefix_bits < 0 || prefix_bits > bp::PREFIX_MAX_BITS) { g_err = "gens: prefix bits must be 0..24"; return nullptr; }
+    Gens* gs = new Gens();
+    gs->device = e->device;
+    gs->n = n;
+    hipStream_t s = pick(stream, *e);
+    const size_t GE = sizeof(ge25519);
+    auto fail = [&](hipError_t er, const char* what) -> void* {
+        g_err = std::string(what) + ": " + hipGetErrorString(er);
+        gs->release();
+        delete gs;
+        return nullptr;
+    };
+    if ((err = gs->gen.need((2 * n + 2) * GE)) != hipSuccess) return fail(err, "gens alloc");
+    uint8_t* d = gs->gen.as<uint8_t>();   // snapshot: G | H | h | g (the table base order)
+    if ((err = hipMemcpyAsync(d, G, n * GE, hipMemcpyDeviceToDevice, s)) != hipSuccess) return fail(err, "gens copy");
+    if ((err = hipMemcpyAsync(d + n * GE, H, n * GE, hipMemcpyDeviceToDevice, s)) != hipSuccess) return fail(err, "gens copy");
+    if ((err = hipMemcpyAsync(d + 2 * n * GE, h, GE, hipMemcpyDeviceToDevice, s)) != hipSuccess) return fail(err, "gens copy");
+    if ((err = hipMemcpyAsync(d + (2 * n + 1) * GE, g, GE, hipMemcpyDeviceToDevice, s)) != hipSuccess)
+        return fail(err, "gens copy");
+    if (prefix_bits) {
+        if ((err = gs->tab.need(((2 * n + 2) << prefix_bits) * GE)) != hipSuccess) return fail(err, "gens tables");
+        bp::launch_prefix_tables(gs->tab.as<bp::ge>(), gs->G(), gs->H(), gs->h(), gs->g(), (int)n, prefix_bits, s);
+        if ((err = hipGetLastError()) != hipSuccess) return fail(err, "gens tables");
+        gs->bits = prefix_bits;
+    }
+    if ((err = hipStreamSynchronize(s)) != hipSuccess) return fail(err, "gens sync");
+    return gs;
+}
+
+void hipbp_gens_destroy(void* gens) {
+    Gens* gs = (Gens*)gens;
+    if (!gs) return;
+    gs->release();
+    delete gs;
+}
+
+int hipbp_batch_generate_range_proof_gens(const hipbp_prove_input* in, void* gens, hipbp_proof_out* out,
+                                          void* stream) {
+    Gens* gs = (Gens*)gens;
+    if (!gs) { g_err = "null gens"; return HIPBP_ERR_ARG; }
+    if (!in || in->n != gs->n) { g_err = "prover: input n differs from the generator set's"; return HIPBP_ERR_ARG; }
+    int dev = -1;
+    BP_RET_ON(hipGetDevice(&dev));
+    if (dev != gs->device) { g_err = "gens: created on another device"; return HIPBP_ERR_ARG; }
+    return prove_run(in, (const ge25519*)gs->G(), (const ge25519*)gs->H(), (const ge25519*)gs->g(),
+                     (const ge25519*)gs->h(), gs->bits ? gs->tab.as<bp::ge>() : nullptr, gs->bits, out, stream);
+}
+
+int hipbp_pipeline_use_gens(void* handle, void* gens) {
+    Pipeline* pl = (Pipeline*)handle;
+    Gens* gs = (Gens*)gens;
+    if (!pl || !gs) { g_err = "null pipeline or gens"; return HIPBP_ERR_ARG; }
+    if ((int)gs->n != pl->n) { g_err = "pipeline n differs from the generator set's"; return HIPBP_ERR_ARG; }
+    if (gs->device != pl->e->device) { g_err = "gens: created on another device"; return HIPBP_ERR_ARG; }
+    std::lock_guard<std::mutex> lk(pl->e->mu);
+    if (pl->busy()) { g_err = "use_gens: pipeline has batches in flight (flush first)"; return HIPBP_ERR_ARG; }
+    BP_RET_ON(hipStreamSynchronize(pl->s));
+    if (pl->ptab.p) {   // its own tables (hipbp_pipeline_prefix_tables) give way to the set's
+        BP_RET_ON(hipFree(pl->ptab.p));
+        pl->ptab.p = nullptr;
+        pl->ptab.cap = 0;
+    }
+    pl->G = gs->G();
+    pl->H = gs->H();
+    pl->h = gs->h();
+    pl->g = gs->g();
+    pl->ext_tab = gs->bits ? gs->tab.as<bp::ge>() : nullptr;
+    pl->pbits = gs->bits;
     return HIPBP_OK;
 }
 

@@ -229,6 +229,10 @@ struct ProveWs {
                   //           aL_i = 0 and the aL_i G_i term where aL_i = 1, once per batch
     uint32_t* slist;  // [cap]  terms0's heavy list in chain-length order (nullable: list order)
     unsigned* sbins;  // [MSM_BINS] its counting-sort bins
+    // fixed-base prefix tables of G, H, h, g (nullable; the SlotDev::ptab layout): every prover
+    // scalar multiplication is on one of these bases (the IPA rounds use the original G, H, Q = h)
+    const ge* ptab;
+    int pbits;
 };
 enum ProveStage { PS_PREP = 0, PS_TERMS0, PS_CHAIN0, PS_COMMIT, PS_TERMS1, PS_TX, PS_RTERMS, PS_RCHAIN, PS_ROUND,
                   PS_FINAL };

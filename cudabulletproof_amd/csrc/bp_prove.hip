@@ -32,9 +32,15 @@ __device__ __forceinline__ size_t gid() { return (size_t)blockIdx.x * blockDim.x
 inline unsigned nblk(size_t items) { return (unsigned)((items + TPB - 1) / TPB); }
 }  // namespace
 
+// Base b's prefix-table row (ProveWs::ptab), or null without tables.
+__device__ __forceinline__ const ge* prow(const ProveWs& ws, int b) {
+    return ws.ptab ? ws.ptab + ((size_t)b << ws.pbits) : nullptr;
+}
+
 // ge25519_normalize(scalarmult(tobytes(s), P)) — the scalar is already in tobytes form.
-__device__ __forceinline__ ge sm_norm(const fe& s, const ge& P, geq* qslot, const ge* __restrict__ dtab) {
-    return ge_norm_host(scalarmult<true>(s, P, qslot, dtab));
+__device__ __forceinline__ ge sm_norm(const fe& s, const ge& P, geq* qslot, const ge* __restrict__ dtab,
+                                      const ge* pt, int K) {
+    return ge_norm_host(scalarmult<true>(s, P, qslot, dtab, pt, pt ? K : 0));
 }
 
 // sequential inner product, field_vector_inner_product (vectors.cu:101-114)
@@ -143,7 +149,7 @@ __global__ __launch_bounds__(TPB) void k_prove_sort_hist(ProveIn in, ProveWs ws)
     const size_t i = gid(), per = 4 * (size_t)in.n + 4;
     if (i < ws.cnt[0]) {
         const uint32_t id = ws.list[i];
-        atomicAdd(&hb[sm_ops(terms0_scalar(in, ws, id / per, (int)(id % per)))], 1u);
+        atomicAdd(&hb[sm_ops_prefix(terms0_scalar(in, ws, id / per, (int)(id % per)), ws.ptab ? ws.pbits : 0)], 1u);
     }
     __syncthreads();
     for (int k = threadIdx.x; k < MSM_BINS; k += TPB)
@@ -161,7 +167,7 @@ __global__ __launch_bounds__(SORT_T) void k_prove_sort_scatter(ProveIn in, Prove
     const bool live = i < ws.cnt[0];
     if (live) {
         id = ws.list[i];
-        key = sm_ops(terms0_scalar(in, ws, id / per, (int)(id % per)));
+        key = sm_ops_prefix(terms0_scalar(in, ws, id / per, (int)(id % per)), ws.ptab ? ws.pbits : 0);
         rank = atomicAdd(&cnt[key], 1u);
     }
     __syncthreads();
@@ -198,23 +204,28 @@ __global__ __launch_bounds__(TPB, 3) void k_prove_terms0(ProveIn in, ProveWs ws,
     fe s;
     ge P;
     bool norm = true;
+    int base;                                       // prefix-table row of P
     ge* dst = ws.pterm + id;
     if (i < 2 * (size_t)n) {
         const bool hs = i < (size_t)n;
         P = hs ? H[i] : G[i - n];
+        base = hs ? n + (int)i : (int)i - n;
         s = hs ? fe_canon(fe_sub(fe_set(0), fe_set(1))) : fe_set(1);   // k_prove_prep's aR (aL = 0), aL = 1
         dst = ws.ctab + i;
     } else if (k < 4 * n) {
         int blk = k / n, j = k % n;
         P = (blk & 1) ? H[j] : G[j];
+        base = (blk & 1) ? n + j : j;
         s = ws.ps[p * 4 * n + k];
     } else {
         k -= 4 * n;
         P = k == 0 ? *g : *h;
+        base = k == 0 ? 2 * n + 1 : 2 * n;
         s = terms0_scalar(in, ws, p, 4 * n + k);
         norm = k < 2;                               // alpha_bytes / rho_bytes: raw, not normalized
     }
-    ge r = scalarmult<true>(s, P, &qs[threadIdx.x], dtab);
+    const ge* pt = prow(ws, base);
+    ge r = scalarmult<true>(s, P, &qs[threadIdx.x], dtab, pt, pt ? ws.pbits : 0);
     *dst = norm ? ge_norm_host(r) : r;
 }
 
@@ -313,7 +324,8 @@ __global__ __launch_bounds__(TPB, 3) void k_prove_terms1(ProveIn in, ProveWs ws,
     __shared__ geq qs[TPB];
     size_t i = gid();
     if (i >= (size_t)in.B * 4) return;
-    ws.tt[i] = sm_norm(ws.tsc[i], (i & 1) ? *h : *g, &qs[threadIdx.x], dtab);
+    ws.tt[i] = sm_norm(ws.tsc[i], (i & 1) ? *h : *g, &qs[threadIdx.x], dtab, prow(ws, 2 * in.n + ((i & 1) ? 0 : 1)),
+                       ws.pbits);
 }
 
 // round-r scalars (inner_product_prove, vectors.cu:345-376): c_L = <a_L, b_R>, c_R = <a_R, b_L> and the
@@ -417,16 +429,20 @@ __global__ __launch_bounds__(TPB, 3) void k_prove_rterms(ProveIn in, ProveWs ws,
     int k = (int)(id % per);
     fe s;
     ge P;
+    int base;
     const bool msm = k < 4 * np;
     if (msm) {
         int blk = k / np, j = k % np;
         P = blk == 0 ? G[np + j] : blk == 1 ? H[j] : blk == 2 ? G[j] : H[np + j];
+        base = blk == 0 ? np + j : blk == 1 ? n + j : blk == 2 ? j : n + np + j;
         s = ws.iscal[p * 2 * n + k];
     } else {
         P = *Q;
+        base = 2 * n;   // Q = h
         s = ws.csc[p * 2 + (k - 4 * np)];
     }
-    ge r = scalarmult<true>(s, P, &qs[threadIdx.x], dtab);   // one call site (see k_prove_terms0)
+    const ge* pt = prow(ws, base);
+    ge r = scalarmult<true>(s, P, &qs[threadIdx.x], dtab, pt, pt ? ws.pbits : 0);   // one call site (k_prove_terms0)
     ws.iterm[p * (2 * (size_t)n + 2) + k] = msm ? ge_norm_host(r) : r;
 }
 

@@ -175,6 +175,16 @@ int hipbp_pipeline_depth(void* pipeline);
  * (synchronous); the caller must not change G/H/g/h afterwards while tables are on.  bits = 0
  * frees them.  The pipeline must be idle (flushed). */
 int hipbp_pipeline_prefix_tables(void* pipeline, int bits);
+/* Generator sets (no reference counterpart): a device snapshot of G[n], H[n], g, h (device
+ * buffers, copied at create; the caller may free them afterwards) plus, for prefix_bits in 1..24,
+ * their fixed-base prefix tables (as hipbp_pipeline_prefix_tables; 0 = none).  Synchronous.
+ * Returns NULL on error.  One set serves the prover and any number of verify pipelines. */
+void* hipbp_gens_create(size_t n, const ge25519* G, const ge25519* H, const ge25519* g, const ge25519* h,
+                        int prefix_bits, void* stream);
+void hipbp_gens_destroy(void* gens);
+/* The pipeline reads its generators and prefix tables from `gens` (same n; the pipeline must be
+ * idle; the set must outlive the pipeline's use of it).  Results keep their bits. */
+int hipbp_pipeline_use_gens(void* pipeline, void* gens);
 void hipbp_pipeline_destroy(void* pipeline);
 
 /* ---- prover: generate_range_proof (bulletproof_range_proof.cu:1159) + inner_product_prove
@@ -202,6 +212,10 @@ typedef struct {
 } hipbp_proof_out;
 int hipbp_batch_generate_range_proof(const hipbp_prove_input* in, const ge25519* G, const ge25519* H,
                                      const ge25519* g, const ge25519* h, hipbp_proof_out* out, void* stream);
+/* The same with a generator set's generators and prefix tables (every scalar multiplication of
+ * the prover is on G_i, H_i, g or h); same bits as hipbp_batch_generate_range_proof on them. */
+int hipbp_batch_generate_range_proof_gens(const hipbp_prove_input* in, void* gens, hipbp_proof_out* out,
+                                          void* stream);
 
 /* Canonical-tree MSM on device buffers.  Asynchronous on `stream`; the MSM, MSM-batch
  * and point-tree calls keep one workspace per (device, stream), so calls on different streams may

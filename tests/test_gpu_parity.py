@@ -883,3 +883,58 @@ def test_prefix_tables_reject_busy_and_bad_bits(bp, oracle):
     pipe.prefix_tables(4)
     pipe.prefix_tables(0)
     pipe.close()
+
+
+@pytest.mark.parametrize("n,B,K", [(16, 40, 9), (64, 70, 14), (4, 3, 2)])
+def test_gens_prover_and_pipeline_same_bits(bp, oracle, n, B, K):
+    """A generator set with prefix tables (hipbp_gens_create): the prover on it gives the same
+    proofs as without tables (and a sample equals the oracle's prover), and a verify pipeline on
+    the same set gives the same verdicts / P / check points as one on the plain generators."""
+    import torch
+    from cudabulletproof_amd import synth
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+    g, h = oracle.gh()
+    rng = np.random.default_rng(n + K)
+    values = [np.concatenate([rng.integers(0, 256, max(1, n // 8)).astype(np.uint8),
+                              np.zeros(32 - max(1, n // 8), np.uint8)]) for _ in range(B)]
+    if n % 8:
+        for v in values:
+            v[0] &= (1 << n) - 1
+    v, gam, sL, sR, rnd, rb = _prove_inputs([300 + p for p in range(B)], values, n)
+    Gd, Hd, gd, hd = T(G), T(H), T(g), T(h)
+    gens = bp.Generators(n, Gd, Hd, gd, hd, prefix_bits=K)
+    args = [T(x) for x in (v, gam, sL, sR, rnd)]
+    o0 = bp.batch_generate_range_proof(n, *args, Gd, Hd, gd, hd)
+    o1 = bp.batch_generate_range_proof(n, *args, None, None, None, None, gens=gens)
+    torch.cuda.synchronize()
+    for k in ("V", "A", "S", "T1", "T2", "taux", "mu", "t", "c", "x", "a", "b", "L", "R", "valid"):
+        assert torch.equal(o0[k], o1[k]), k
+    from oracle.pyoracle import head_fields
+    u = lambda t: t.cpu().numpy().view(np.uint64)
+    for p in (0, B - 1):
+        pr = oracle.generate_range_proof(values[p], *rb[p], n, G, H, g, h)
+        if pr is None:   # refused (validate_range_input's byte rule refuses most values at n < 8)
+            assert int(o1["valid"][p]) == 0, p
+            continue
+        hf = head_fields(pr["head"])
+        for k in ("V", "A", "S", "T1", "T2", "t", "x"):
+            assert np.array_equal(u(o1[k])[p], hf[k]), (p, k)
+        assert np.array_equal(u(o1["L"])[p], pr["L"]), p
+    batch = bp.RangeProofBatch(n, **{k: o1[k] for k in bp.RangeProofBatch.FIELDS})
+    res = []
+    for use in (False, True):
+        pipe = bp.VerifyPipeline(B, n, Gd, Hd, hd)
+        if use:
+            pipe.use_gens(gens)
+        o = [torch.zeros(B, dtype=torch.uint8, device=dev), torch.zeros(B, 16, dtype=torch.int64, device=dev),
+             torch.zeros(B, 16, dtype=torch.int64, device=dev)]
+        pipe.push(batch, *o)
+        pipe.flush()
+        torch.cuda.synchronize()
+        res.append([x.cpu() for x in o])
+        pipe.close()
+    for a, b2 in zip(*res):
+        assert torch.equal(a, b2)
+    gens.close()
