@@ -45,6 +45,9 @@ def parse():
                     help="pipeline: streaming verify pipeline, one tick (= one batch of work) per step; "
                          "oneshot: each step verifies one batch start to finish")
     ap.add_argument("--streams", type=int, default=2, help="oneshot mode: HIP streams batches rotate over")
+    ap.add_argument("--pipes", type=int, default=2,
+                    help="pipeline mode: verify pipelines on their own streams, batches alternate over them "
+                         "(concurrent ticks fill each other's tails)")
     ap.add_argument("--msm-log2", type=int, default=20)
     ap.add_argument("--ipa-n", type=int, default=4096, help="configs[3]: inner-product-argument size")
     ap.add_argument("--ipa-batch", type=int, default=64, help="IPA proofs per pipeline tick")
@@ -261,38 +264,44 @@ def ipa_leg(args, dev):
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)
     Gd, Hd, Qd = T(G), T(H), T(h)
     GH = torch.cat([Gd, Hd]).contiguous()
-    nb = 2
+    npipe = max(1, args.pipes)   # as the verify leg: concurrent pipelines on their own streams
+    nb = 2 * npipe
     batches = [bp.RangeProofBatch.from_numpy(n, synth.proofs(B, n, seed=90 + i), dev) for i in range(nb)]
     wit = [T(synth._rand_fe(np.random.default_rng(60 + i), (B * 2 * n,))) for i in range(nb)]   # a||b per proof
     Ps = [torch.zeros(B, 16, dtype=torch.int64, device=dev) for _ in range(nb)]
     oks = [torch.zeros(B, dtype=torch.uint8, device=dev) for _ in range(nb)]
-    stream = torch.cuda.Stream(dev)
-    pipe = bp.VerifyPipeline(B, n, Gd, Hd, Qd, range_mode=False, stream=stream)
+    streams = [torch.cuda.Stream(dev) for _ in range(npipe)]
+    pipes = [bp.VerifyPipeline(B, n, Gd, Hd, Qd, range_mode=False, stream=st) for st in streams]
+    pipe = pipes[0]
 
-    def tick(k, with_P):
+    def tick(k, with_P):   # P of batch k on its pipeline's stream (per-stream MSM workspaces), then the tick
+        j = k % npipe
         if with_P:
-            bp.msm_batch(Ps[k % nb], wit[k % nb], GH, stream=stream)
-        pipe.push(batches[k % nb], oks[k % nb], P_in=Ps[k % nb])
+            bp.msm_batch(Ps[k % nb], wit[k % nb], GH, stream=streams[j])
+        pipes[j].push(batches[k % nb], oks[k % nb], P_in=Ps[k % nb])
 
     res = {}
+    steps = max(args.ipa_steps, npipe) // npipe * npipe
     for with_P in (True, False):
-        for k in range(pipe.depth - 1):   # fill: every timed tick then completes one batch
+        for k in range((pipe.depth - 1) * npipe):   # fill: every timed tick then completes one batch
             tick(k, with_P)
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        for k in range(args.ipa_steps):
+        for k in range(steps):
             tick(k, with_P)
         torch.cuda.synchronize(dev)
         res[with_P] = time.perf_counter() - t0
-        pipe.flush()
+        for pp in pipes:
+            pp.flush()
         torch.cuda.synchronize(dev)
-    pipe.close()
+    for pp in pipes:
+        pp.close()
     sm = 4 * (n - 1) + 3   # fold rounds + a0*G', b0*H', c*Q (crv:160-296)
     dt = res[True]
-    return {"metric": f"{n}-element inner-product-argument verifies/sec", "value": B * args.ipa_steps / dt,
-            "unit": "verifies/s", "batch": B, "n": n, "ms_per_tick": dt / args.ipa_steps * 1e3,
-            "scalar_mults_per_verify": sm + 2 * n, "scalar_mults_per_s": B * args.ipa_steps * (sm + 2 * n) / dt,
-            "value_P_given": B * args.ipa_steps / res[False],
+    return {"metric": f"{n}-element inner-product-argument verifies/sec", "value": B * steps / dt,
+            "unit": "verifies/s", "batch": B, "n": n, "ms_per_tick": dt / steps * 1e3, "pipelines": npipe,
+            "scalar_mults_per_verify": sm + 2 * n, "scalar_mults_per_s": B * steps * (sm + 2 * n) / dt,
+            "value_P_given": B * steps / res[False],
             "semantics": "P = canonical-tree MSM(a||b, G||H) (hipbp_msm_batch) + cuda_inner_product_verify "
                          "(crv:130)", "pipeline_depth": pipe.depth}
 
@@ -389,20 +398,31 @@ def main():
     else:
         batches = [bp.RangeProofBatch.from_numpy(n, synth.proofs(B, n, seed=1 + 1000 * rank + i), dev)
                    for i in range(nb)]
-    ns = max(1, args.streams)
+    # configs[2] first, before the verify streams exist: hipbp_msm_pippenger overlaps its chains on
+    # an internal side stream, which needs a hardware queue of its own (HIP spreads streams over
+    # GPU_MAX_HW_QUEUES = 4; with the verify pipelines' streams bound first it shared one: 312 -> 190
+    # M points/s); at N > 1 one MSM sharded over all ranks (strong scaling)
+    msm = None
+    if not args.no_msm:
+        msm = msm_leg(args, dev, world, rank, T)
+    ns = max(1, args.streams, args.pipes)
     streams = [torch.cuda.Stream(dev) for _ in range(ns)]
     oks = [torch.zeros(B, dtype=torch.uint8, device=dev) for _ in range(max(ns, nb))]
     stream = torch.cuda.current_stream(dev)
     torch.cuda.synchronize(dev)
     pipe = None
+    pipes = []
     if args.mode == "pipeline":
-        pipe = bp.VerifyPipeline(B, n, Gd, Hd, hd, stream=streams[0])
-        if gens is not None:
-            pipe.use_gens(gens)
+        npipe = max(1, args.pipes)
+        pipes = [bp.VerifyPipeline(B, n, Gd, Hd, hd, stream=streams[i]) for i in range(npipe)]
+        for pp in pipes:
+            if gens is not None:
+                pp.use_gens(gens)
+        pipe = pipes[0]
 
         def step(k):   # one tick: stage s of the batch pushed s ticks earlier, for every s
-            pipe.push(batches[k % nb], oks[k % nb])
-        warm = max(args.warmup, pipe.depth)   # fill the pipeline before timing
+            pipes[k % npipe].push(batches[k % nb], oks[k % nb])
+        warm = max(args.warmup, pipe.depth * npipe)   # fill the pipelines before timing
     else:
         def step(k):
             bp.batch_range_proof_verify(batches[k % nb], Gd, Hd, gd, hd, oks[k % ns], stream=streams[k % ns])
@@ -410,13 +430,13 @@ def main():
 
     for k in range(warm):
         step(k)
-    if pipe:
-        pipe.flush()
+    for pp in pipes:
+        pp.flush()
     torch.cuda.synchronize(dev)
     passes_warm = int(oks[0].sum().item())
 
     if pipe:   # refill (flush drained it) so every timed tick carries a full batch of work
-        for k in range(pipe.depth - 1):
+        for k in range((pipe.depth - 1) * len(pipes)):
             step(k)
         torch.cuda.synchronize(dev)
     bp.timing_enable(True)
@@ -432,10 +452,11 @@ def main():
     dt = time.perf_counter() - t0
     stats = bp.timing_collect()
     bp.timing_enable(False)
-    if pipe:
-        pipe.flush()
-        torch.cuda.synchronize(dev)
-        pipe.close()
+    for pp in pipes:
+        pp.flush()
+    torch.cuda.synchronize(dev)
+    for pp in pipes:
+        pp.close()
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -456,26 +477,31 @@ def main():
     per_launch = ab_batch * args.steps / launches if ab_batch else None
     achieved = (per_launch / (avg_ms * 1e-3)) / 1e9 if per_launch else None
     pcfg = {"batch_per_gpu": B, "n": n, "prefix_bits": prefix["bits"] if prefix else 0}
+    # with P > 1 pipelines two ticks run concurrently, so a launch's own duration includes its
+    # overlap with the other's: the aggregate rate (work of every launch in the timed region / the
+    # region's wall time) is reported beside the per-launch one
+    agg = ab_batch * args.steps / dt / 1e9 if ab_batch else None
     roofline = {
         "bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": pmc(dom, "bytes_per_launch", pcfg),
-        "avg_launch_ms": avg_ms, "launches": launches,
+        "achieved_aggregate": agg, "frac_aggregate": agg / HBM_PEAK_GBS if agg else None,
+        "avg_launch_ms": avg_ms, "launches": launches, "concurrent_pipelines": len(pipes) or None,
         "kernel_ms_share": {k: round(v / sum(kern_ms.values()), 4) for k, v in kern_ms.items()},
         "binding": "VALU integer (not HBM, not MFMA): see DESIGN.md and valu_roofline",
         "scalar_mults_per_s": value * sm_per_verify(n),
     }
     vi = pmc(dom, "valu_instr_per_launch", pcfg)
+    vagg = vi * launches / dt if vi else None   # all launches of the timed region / its wall time
     valu_roofline = {
         "kernel": dom, "unit": "wave64 VALU instr/s", "peak": VALU_PEAK_WINSTR,
-        "instr_per_launch": vi, "achieved": vi / (avg_ms * 1e-3) if vi else None,
-        "frac": vi / (avg_ms * 1e-3) / VALU_PEAK_WINSTR if vi else None,
+        "instr_per_launch": vi, "achieved": vagg, "frac": vagg / VALU_PEAK_WINSTR if vagg else None,
+        "achieved_per_launch": vi / (avg_ms * 1e-3) if vi else None,
         "valu_busy_pct": pmc(dom, "valu_busy_pct", pcfg), "pmc_config": pcfg,
-        "source": "SQ_INSTS_VALU per steady-state launch (profiles/pmc_traffic.json) / live HIP-event launch time",
+        "source": "SQ_INSTS_VALU per steady-state launch (profiles/pmc_traffic.json) x launches in the timed "
+                  "region / its wall time (per_launch: / the live HIP-event launch time, which overlaps "
+                  "the other pipeline's launch when pipes > 1)",
     }
 
-    msm = None
-    if not args.no_msm:   # configs[2]; at N > 1 one MSM sharded over all ranks (strong scaling)
-        msm = msm_leg(args, dev, world, rank, T)
 
     ipa = None
     if not args.no_ipa and rank == 0:   # configs[3]: single-GPU
@@ -501,7 +527,8 @@ def main():
             "config": {"workload": f"batch {B} x {n}-bit range-proof verify per GPU (BASELINE configs[1])",
                        "batch_per_gpu": B, "n": n, "semantics": "cuda_range_proof_verify (crv:82)",
                        "parallelism": f"independent proof shards x{world}", "mode": args.mode,
-                       "pipeline_depth": pipe.depth if pipe else None, "prefix_tables": prefix,
+                       "pipeline_depth": pipe.depth if pipe else None, "pipelines": len(pipes) or None,
+                       "prefix_tables": prefix,
                        "proof_bytes": proof_bytes(n, 1), "passes_in_warmup_batch": passes_warm},
             "roofline": roofline, "valu_roofline": valu_roofline, "cpu_baseline": cpu, "msm": msm, "ipa": ipa, "prove": prove,
         }
