@@ -86,7 +86,7 @@ def main():
     stats = list(csv.DictReader(open(os.path.join(base, "trace", "run_kernel_stats.csv"))))
     lines = [f"# rocprofv3 summary — {tag}", "",
              "Command: `tools/profile.sh " + tag + "` on one MI355X "
-             "(bench.py --steps 6 --warmup 2 --no-cpu --no-ipa --no-prove --msm-log2 18 under rocprofv3).", "",
+             "(bench.py --steps 6 --warmup 2 --no-cpu --no-ipa --no-prove --msm-log2 $MSM_LOG2 under rocprofv3, defaults otherwise).", "",
              "## Kernel trace (`rocprofv3 --kernel-trace --stats`)", "",
              "| kernel | calls | avg ms | min ms | max ms | % time |", "|---|---|---|---|---|---|"]
     for r in stats:
