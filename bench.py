@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--prefix-bits", type=int, default=22,
                     help="fixed-base prefix tables of the generators (hipbp_pipeline_prefix_tables; "
                          "0 = off): one-time setup, same bits")
+    ap.add_argument("--shard-total", type=int, default=1 << 16, help="configs[4]: proofs in the sharded batch")
+    ap.add_argument("--no-shard", action="store_true")
     ap.add_argument("--rehearse", action="store_true",
                     help="exercise the N>1 path on one GPU (all ranks on cuda:0, gloo collectives); not a measurement")
     return ap.parse_args()
@@ -306,6 +308,65 @@ def ipa_leg(args, dev):
                          "(crv:130)", "pipeline_depth": pipe.depth}
 
 
+def shard_leg(args, dev, world, rank, pipes, gens, G, H, g, h):
+    """configs[4]: ONE batch of 2^16 64-bit proofs (1024 x 4 distinct proofs, tiled: the kernels do
+    not dedupe) split into equal contiguous shards over the ranks (shard.shard_bounds).  Each rank
+    verifies its shard through its pipelines; the pass counts meet in one all_reduce(SUM) and the
+    2^16 verdict bytes in one all_gather over RCCL (every rank ends with all verdicts).  Timed
+    from a barrier to the end of the collectives (pipeline fill and drain included), max over ranks;
+    strong scaling: the same 2^16 proofs whatever N."""
+    import torch
+    import torch.distributed as dist
+    import cudabulletproof_amd as bp
+    from cudabulletproof_amd import shard, synth
+    B, n, total = args.batch, args.n, args.shard_total
+    lo, hi = shard.shard_bounds(total, world, rank)
+    tiles = []
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)
+    for t in range(4):   # rank-independent tiles: the global set is the same for every N
+        pi = {k: T(v) for k, v in synth.prove_inputs(B, n, seed=5001 + t).items()}
+        out = bp.batch_generate_range_proof(n, pi["v"], pi["gamma"], pi["sL"], pi["sR"], pi["rnd"], G, H, g, h,
+                                            gens=gens)
+        tiles.append({k: out[k] for k in bp.RangeProofBatch.FIELDS})
+    torch.cuda.synchronize(dev)
+    jobs = []   # (tile, first row, rows) per push; proof j of the global set is tile (j // B) % 4, row j % B
+    j = lo
+    while j < hi:
+        m = min(B - j % B, hi - j)
+        jobs.append(((j // B) % 4, j % B, m))
+        j += m
+    batches = [bp.RangeProofBatch(n, **{k: v[r0:r0 + m] for k, v in tiles[t].items()}) for t, r0, m in jobs]
+    ok = torch.zeros(hi - lo, dtype=torch.uint8, device=dev)
+    offs = np.cumsum([0] + [m for _, _, m in jobs])
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k, b in enumerate(batches):
+        pipes[k % len(pipes)].push(b, ok[offs[k]:offs[k + 1]])
+    for pp in pipes:
+        pp.flush()
+    torch.cuda.synchronize(dev)   # the pipelines' streams have written every verdict
+    passes = ok.sum(dtype=torch.int64)
+    allv = ok
+    if world > 1:
+        dist.all_reduce(passes, op=dist.ReduceOp.SUM)
+        nccl = dist.get_backend() == "nccl"   # --rehearse runs gloo, which gathers host tensors
+        allv = shard.gather_verdicts(ok if nccl else ok.cpu(), total)
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    import hashlib as _h
+    return {"metric": "2^16-proof 64-bit range-proof batch verify (BASELINE configs[4])", "value": total / dt,
+            "unit": "verifies/s", "proofs": total, "n_gpus": world, "scaling": "strong", "ms": dt * 1e3,
+            "passes": int(passes.item()), "verdicts_sha256": _h.sha256(allv.cpu().numpy().tobytes()).hexdigest()[:16],
+            "collectives": "all_reduce(SUM) of pass counts + all_gather of the verdict bytes (RCCL at N > 1)",
+            "data": "1024 x 4 distinct GPU-prover proofs (rank-independent seeds), tiled to 2^16"}
+
+
 def prove_leg(args, dev, gens=None):
     """§8(f) rank 1: generate_range_proof (rp.cu:1159) batched on the GPU, n = args.n, synthetic
     values and random scalars; proofs/s over whole batches (inputs resident in HBM)."""
@@ -455,6 +516,9 @@ def main():
     for pp in pipes:
         pp.flush()
     torch.cuda.synchronize(dev)
+    sharded = None
+    if pipes and not args.no_shard:   # configs[4] on the same pipelines (all ranks take part)
+        sharded = shard_leg(args, dev, world, rank, pipes, gens, Gd, Hd, gd, hd)
     for pp in pipes:
         pp.close()
     if world > 1:
@@ -531,6 +595,7 @@ def main():
                        "prefix_tables": prefix,
                        "proof_bytes": proof_bytes(n, 1), "passes_in_warmup_batch": passes_warm},
             "roofline": roofline, "valu_roofline": valu_roofline, "cpu_baseline": cpu, "msm": msm, "ipa": ipa, "prove": prove,
+            "sharded_2p16": sharded,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -9,8 +9,8 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SMALL = ["--steps", "2", "--warmup", "1", "--batch", "128", "--msm-log2", "12", "--prefix-bits", "12", "--no-cpu",
-         "--no-ipa", "--no-prove"]
+SMALL = ["--steps", "2", "--warmup", "1", "--batch", "128", "--msm-log2", "12", "--prefix-bits", "12",
+         "--shard-total", "3000", "--no-cpu", "--no-ipa", "--no-prove"]
 
 
 # rank 0's single-GPU legs (IPA, prover) while the other rank waits at the closing barrier
@@ -36,5 +36,9 @@ def test_bench_two_ranks_rehearsal_matches_one_rank():
     assert l1["n_gpus"] == 1 and l2["n_gpus"] == 2
     assert l2["msm"]["scaling"] == "strong" and l2["scaling"] == "weak"
     assert l1["msm"]["result_sha256"] == l2["msm"]["result_sha256"]
+    # configs[4]: the same proof set sharded over 1 or 2 ranks -> the same verdicts on every rank
+    s1, s2 = l1["sharded_2p16"], l2["sharded_2p16"]
+    assert s1["proofs"] == s2["proofs"] == 3000 and s2["scaling"] == "strong"
+    assert s1["passes"] == s2["passes"] > 0 and s1["verdicts_sha256"] == s2["verdicts_sha256"]
     assert l2["config"]["passes_in_warmup_batch"] >= l1["config"]["passes_in_warmup_batch"]
     assert l2["ipa"]["n_gpus"] == 1 and l2["prove"]["n_gpus"] == 1 and l2["prove"]["valid"] == 256
