@@ -18,6 +18,8 @@
 // chunk (W 2^c / 16 lanes) for the running sums and the small scalar-mult, (4) one block per
 // window: the chunk tree in LDS, (5) one lane quad: the Horner chain (~256 doublings,
 // latency-bound), on a side stream so its top-half part overlaps the bottom half's buckets.
+// The host never waits: the tree depth is read on the device (pip_steps), so independent MSMs
+// on different streams overlap one's latency-bound chains with another's bucket trees.
 #include <hipcub/hipcub.hpp>
 
 #include <map>
@@ -75,13 +77,90 @@ __global__ __launch_bounds__(PTPB) void k_pip_len0(const uint32_t* __restrict__ 
     if (L) atomicMax(maxlen, L);
 }
 
-__global__ __launch_bounds__(PTPB) void k_pip_nextlen(const uint32_t* __restrict__ len, uint32_t* len2, uint32_t* pad2,
-                                                     size_t nb) {
-    const size_t b = (size_t)blockIdx.x * PTPB + threadIdx.x;
-    if (b >= nb) return;
-    const uint32_t L = (len[b] + 3) >> 2;
-    len2[b] = L;
-    pad2[b] = (L + 3) & ~3u;
+// Tree steps needed for the longest bucket list (levels = ceil(log2 maxlen), at least 1; two
+// levels per step).  Every step kernel reads it on the device, so the host never waits for the
+// bucket-size histogram: it launches the worst-case number of steps (lists are at most n long)
+// and the steps past the data's depth exit at once.
+__device__ __forceinline__ int pip_steps(const unsigned* maxlen) {
+    const unsigned m = *maxlen;
+    int levels = 1;
+    while (levels < 31 && (1u << levels) < m) levels++;
+    return (levels + 1) / 2;
+}
+
+// Next layout (len, pad)[b] of step t and its exclusive scan off[b], in two launches:
+// k_pip_scan_part forms len/pad for SCAN_PER consecutive buckets per thread and one partial sum
+// per block; k_pip_scan_fin adds the partial sums of the blocks before it and scans its own.
+constexpr int SCAN_PER = 8;
+constexpr int SCAN_BLK = PTPB * SCAN_PER;
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t u = __shfl_up(v, d, 64);
+        if (lane >= d) v += u;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(PTPB) void k_pip_scan_part(int t, const unsigned* __restrict__ maxlen,
+                                                       const uint32_t* __restrict__ len, uint32_t* len2,
+                                                       uint32_t* pad2, size_t nb, uint32_t* part) {
+    if (t >= pip_steps(maxlen)) return;
+    __shared__ uint32_t wsum[PTPB / 64];
+    const size_t b0 = (size_t)blockIdx.x * SCAN_BLK + (size_t)threadIdx.x * SCAN_PER;
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; k++) {
+        const size_t b = b0 + k;
+        if (b < nb) {
+            const uint32_t L = (len[b] + 3) >> 2, pd = (L + 3) & ~3u;
+            len2[b] = L;
+            pad2[b] = pd;
+            sum += pd;
+        }
+    }
+    const uint32_t inc = wave_incl_scan(sum);
+    if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+#pragma unroll
+        for (int w = 0; w < PTPB / 64; w++) tot += wsum[w];
+        part[blockIdx.x] = tot;
+    }
+}
+
+__global__ __launch_bounds__(PTPB) void k_pip_scan_fin(int t, const unsigned* __restrict__ maxlen,
+                                                      const uint32_t* __restrict__ pad2,
+                                                      const uint32_t* __restrict__ part, size_t nb, uint32_t* off2) {
+    if (t >= pip_steps(maxlen)) return;
+    __shared__ uint32_t wsum[PTPB / 64];
+    __shared__ uint32_t pre;
+    if (threadIdx.x < 64) {   // sum of the partial sums of the blocks before this one
+        uint32_t v = 0;
+        for (unsigned i = threadIdx.x; i < blockIdx.x; i += 64) v += part[i];
+        v = wave_incl_scan(v);
+        if (threadIdx.x == 63) pre = v;
+    }
+    const size_t b0 = (size_t)blockIdx.x * SCAN_BLK + (size_t)threadIdx.x * SCAN_PER;
+    uint32_t p[SCAN_PER], sum = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; k++) {
+        p[k] = b0 + k < nb ? pad2[b0 + k] : 0u;
+        sum += p[k];
+    }
+    const uint32_t inc = wave_incl_scan(sum);
+    if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = inc;
+    __syncthreads();
+    uint32_t run = pre + inc - sum;
+    for (int w = 0; w < (int)(threadIdx.x >> 6); w++) run += wsum[w];
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; k++) {
+        if (b0 + k < nb) off2[b0 + k] = run;
+        run += p[k];
+    }
 }
 
 __global__ __launch_bounds__(PTPB) void k_pip_bid0(const uint32_t* __restrict__ keys, size_t N,
@@ -93,7 +172,7 @@ __global__ __launch_bounds__(PTPB) void k_pip_bid0(const uint32_t* __restrict__ 
     bid[off[b] + (p - start[b])] = b;
 }
 
-__global__ __launch_bounds__(PTPB) void k_pip_step(int first, const ge* __restrict__ P,
+__global__ __launch_bounds__(PTPB) void k_pip_step(int t, const unsigned* __restrict__ maxlen, const ge* __restrict__ P,
                                                   const uint32_t* __restrict__ vals,
                                                   const uint32_t* __restrict__ start, const ge* __restrict__ Qin,
                                                   const uint32_t* __restrict__ bid, const uint32_t* __restrict__ off,
@@ -101,7 +180,8 @@ __global__ __launch_bounds__(PTPB) void k_pip_step(int first, const ge* __restri
                                                   const uint32_t* __restrict__ off2, ge* Qout, uint32_t* bid2,
                                                   size_t nb, size_t lanes) {
     const size_t k = (size_t)blockIdx.x * PTPB + threadIdx.x;
-    if (k >= lanes) return;
+    if (k >= lanes || t >= pip_steps(maxlen)) return;
+    const bool first = t == 0;
     const uint32_t total = off[nb - 1] + pad[nb - 1];
     const uint32_t pos = (uint32_t)(4 * k);
     if (pos >= total) return;
@@ -229,9 +309,16 @@ __device__ __forceinline__ ge ge_row_move(const ge& a) {
 // quad B walks S one step behind, fed each new R over DPP — both quads run the same point add in
 // lockstep on their own operands, 15 dependent adds instead of 29.  (kM) R is
 // ge25519_scalarmult's double-and-add on the scalar's raw bits, leading zeros from dtab.
-__global__ __launch_bounds__(PTPB) void k_pip_chunks(const ge* __restrict__ Q, const uint32_t* __restrict__ off,
-                                                    const uint32_t* __restrict__ cnt, int c, int W, ge* V,
+__global__ __launch_bounds__(PTPB) void k_pip_chunks(const ge* __restrict__ Q0, const ge* __restrict__ Q1,
+                                                    const uint32_t* __restrict__ off0, const uint32_t* __restrict__ off1,
+                                                    const uint32_t* __restrict__ cnt0, const uint32_t* __restrict__ cnt1,
+                                                    const unsigned* __restrict__ maxlen, int c, int W, ge* V,
                                                     const ge* __restrict__ dtab) {
+    // after the last step every non-empty bucket holds its sum on side (steps & 1)
+    const bool f1 = (pip_steps(maxlen) & 1) != 0;
+    const ge* __restrict__ Q = f1 ? Q1 : Q0;
+    const uint32_t* __restrict__ off = f1 ? off1 : off0;
+    const uint32_t* __restrict__ cnt = f1 ? cnt1 : cnt0;
     const size_t NB = (size_t)1 << c, NC = NB / PM;
     const size_t g = ((size_t)blockIdx.x * PTPB + threadIdx.x) >> 3;
     if (g >= (size_t)W * NC) return;   // whole octets leave together
@@ -264,7 +351,13 @@ struct DBuf {
     size_t cap = 0;
     hipError_t need(size_t bytes) {
         if (bytes <= cap) return hipSuccess;
-        if (p) { hipError_t e = hipFree(p); if (e != hipSuccess) return e; p = nullptr; cap = 0; }
+        if (p) {   // growing: earlier MSMs on this workspace's streams may still read the old buffer
+            hipError_t e = hipDeviceSynchronize();
+            if (e == hipSuccess) e = hipFree(p);
+            if (e != hipSuccess) return e;
+            p = nullptr;
+            cap = 0;
+        }
         hipError_t e = hipMalloc(&p, bytes ? bytes : 1);
         if (e == hipSuccess) cap = bytes;
         return e;
@@ -272,11 +365,9 @@ struct DBuf {
     template <typename T> T* as() const { return (T*)p; }
 };
 struct PipWs {
-    DBuf keys_in, vals_in, keys, vals, temp, start, len[2], pad[2], off[2], bid[2], Q[2], V, Sw, Tmid, maxlen;
-    unsigned* host_max = nullptr;
+    DBuf keys_in, vals_in, keys, vals, temp, start, len[2], pad[2], off[2], bid[2], Q[2], V, Sw, Tmid, maxlen, part;
     hipStream_t side = nullptr;           // the Horner chain's stream
     hipEvent_t ev[4] = {};   // [1] top half's buckets done, [2] bottom half done, [3] chain done
-    int fin = 0;
 };
 // Workspaces per (device, stream): torch's default stream is handle 0 on every device, so the
 // stream alone does not identify a workspace.  Each pair holds the top and bottom part's
@@ -291,7 +382,7 @@ inline unsigned nb_of(size_t items) { return (unsigned)((items + PTPB - 1) / PTP
 
 #define PIP_RET(x) do { hipError_t _e = (x); if (_e != hipSuccess) return _e; } while (0)
 
-// Bucket sums of windows [w0, w1) on stream s (ws.fin: the ping-pong side holding them).
+// Bucket sums of windows [w0, w1) on stream s (they end on ping-pong side pip_steps & 1).
 static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, int c, int w0, int w1,
                               hipStream_t s) {
     const int W = w1 - w0;
@@ -332,37 +423,40 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
                                              (int)nb, s));
     k_pip_bid0<<<nb_of(N), PTPB, 0, s>>>(ws.keys.as<uint32_t>(), N, ws.start.as<uint32_t>(), ws.off[0].as<uint32_t>(),
                                          ws.bid[0].as<uint32_t>());
-    PIP_RET(hipMemcpyAsync(ws.host_max, ws.maxlen.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
-    PIP_RET(hipStreamSynchronize(s));   // the bucket-tree depth (only this stream: the side stream runs on)
+    // the worst-case step count (a bucket list is at most n long); steps past the depth of the
+    // data exit on the device (pip_steps), so nothing here waits for the GPU
     int levels = 1;
-    while (((size_t)1 << levels) < *ws.host_max) levels++;
+    while (levels < 31 && ((size_t)1 << levels) < n) levels++;
     const int steps = (levels + 1) / 2;
+    const unsigned nparts = (unsigned)((nb + SCAN_BLK - 1) / SCAN_BLK);
+    PIP_RET(ws.part.need((size_t)nparts * 4));
     // step t: layout (off, len, pad, bid)[t & 1] -> [(t + 1) & 1], data -> Q[(t + 1) & 1]
     size_t lanes = (tot0 + 3) / 4;
     for (int t = 0; t < steps; t++) {
         const int a = t & 1, b = a ^ 1;
-        k_pip_nextlen<<<nb_of(nb), PTPB, 0, s>>>(ws.len[a].as<uint32_t>(), ws.len[b].as<uint32_t>(),
-                                                  ws.pad[b].as<uint32_t>(), nb);
-        PIP_RET(hipcub::DeviceScan::ExclusiveSum(ws.temp.p, tb_scan, ws.pad[b].as<uint32_t>(),
-                                                 ws.off[b].as<uint32_t>(), (int)nb, s));
-        k_pip_step<<<nb_of(lanes), PTPB, 0, s>>>(t == 0, P, ws.vals.as<uint32_t>(), ws.start.as<uint32_t>(),
-                                                  ws.Q[a].as<ge>(), ws.bid[a].as<uint32_t>(), ws.off[a].as<uint32_t>(),
-                                                  ws.len[a].as<uint32_t>(), ws.pad[a].as<uint32_t>(),
-                                                  ws.off[b].as<uint32_t>(), ws.Q[b].as<ge>(), ws.bid[b].as<uint32_t>(),
-                                                  nb, lanes);
+        k_pip_scan_part<<<nparts, PTPB, 0, s>>>(t, ws.maxlen.as<unsigned>(), ws.len[a].as<uint32_t>(),
+                                                ws.len[b].as<uint32_t>(), ws.pad[b].as<uint32_t>(), nb,
+                                                ws.part.as<uint32_t>());
+        k_pip_scan_fin<<<nparts, PTPB, 0, s>>>(t, ws.maxlen.as<unsigned>(), ws.pad[b].as<uint32_t>(),
+                                               ws.part.as<uint32_t>(), nb, ws.off[b].as<uint32_t>());
+        k_pip_step<<<nb_of(lanes), PTPB, 0, s>>>(t, ws.maxlen.as<unsigned>(), P, ws.vals.as<uint32_t>(),
+                                                  ws.start.as<uint32_t>(), ws.Q[a].as<ge>(), ws.bid[a].as<uint32_t>(),
+                                                  ws.off[a].as<uint32_t>(), ws.len[a].as<uint32_t>(),
+                                                  ws.pad[a].as<uint32_t>(), ws.off[b].as<uint32_t>(), ws.Q[b].as<ge>(),
+                                                  ws.bid[b].as<uint32_t>(), nb, lanes);
         lanes = lanes / 4 + nb;
     }
-    // after the last step every non-empty bucket holds its sum at off[steps & 1][b]
-    ws.fin = steps & 1;
     return hipGetLastError();
 }
 
 // Chunks -> window sums of windows [w0, w1) into Sw[w0 .. w1-1], on stream s (latency-bound).
 static hipError_t pip_finish(PipWs& ws, int c, int w0, int w1, ge* Sw, const ge* dtab, hipStream_t s) {
-    const int W = w1 - w0, fin = ws.fin;
+    const int W = w1 - w0;
     const size_t NC = ((size_t)1 << c) / PM;
-    k_pip_chunks<<<nb_of(8 * (size_t)W * NC), PTPB, 0, s>>>(ws.Q[fin].as<ge>(), ws.off[fin].as<uint32_t>(),
-                                                         ws.len[fin].as<uint32_t>(), c, W, ws.V.as<ge>(), dtab);
+    k_pip_chunks<<<nb_of(8 * (size_t)W * NC), PTPB, 0, s>>>(ws.Q[0].as<ge>(), ws.Q[1].as<ge>(), ws.off[0].as<uint32_t>(),
+                                                         ws.off[1].as<uint32_t>(), ws.len[0].as<uint32_t>(),
+                                                         ws.len[1].as<uint32_t>(), ws.maxlen.as<unsigned>(), c, W,
+                                                         ws.V.as<ge>(), dtab);
     k_pip_window<<<W, PTPB, 0, s>>>(ws.V.as<ge>(), (int)NC, Sw + w0);
     return hipGetLastError();
 }
@@ -382,14 +476,13 @@ static hipError_t pip_pair(PipPair** out, hipStream_t s) {
     if (it != g_pip.end()) { *out = it->second; return hipSuccess; }
     PipPair* pp = new PipPair();
     auto fail = [&](hipError_t e) {   // a half-made pair is never cached
-        if (pp->hi.host_max) (void)hipHostFree(pp->hi.host_max);
-        if (pp->lo.host_max) (void)hipHostFree(pp->lo.host_max);
+        if (pp->hi.side) (void)hipStreamDestroy(pp->hi.side);
+        for (auto& ev : pp->hi.ev)
+            if (ev) (void)hipEventDestroy(ev);
         delete pp;
         return e;
     };
     hipError_t e;
-    if ((e = hipHostMalloc(&pp->hi.host_max, sizeof(unsigned))) != hipSuccess) return fail(e);
-    if ((e = hipHostMalloc(&pp->lo.host_max, sizeof(unsigned))) != hipSuccess) return fail(e);
     // a high-priority stream: HIP spreads streams over a few hardware queues, and one that
     // shared the caller's queue would serialize the chains behind the bottom half again
     int lo_pr = 0, hi_pr = 0;

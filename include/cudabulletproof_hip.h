@@ -234,10 +234,11 @@ int hipbp_msm_batch(ge25519* results, const fe25519* scalars, const ge25519* poi
  * for cuda_point_vector_multi_scalar_mul: the reference's MSM bits come from per-point
  * double-and-add + the canonical tree (hipbp_msm), and this arithmetic is not associative, so a
  * bucket regrouping yields different bits.  Its own result is fixed (stable bucket order, fixed
- * trees) and equals the C restatement oracle/bp_oracle.c orc_msm_pippenger.  Synchronizes the
- * stream twice (the bucket-tree depth of each half of the windows) and runs the Horner chain on
- * an internal side stream that the caller's stream waits on before returning, so it cannot be
- * captured into a graph.  Workspaces are per (device, stream).  No reference counterpart. */
+ * trees) and equals the C restatement oracle/bp_oracle.c orc_msm_pippenger.  Asynchronous: the
+ * host does not wait (the bucket-tree depth is read on the device); the Horner chain runs on an
+ * internal side stream that the caller's stream waits on, so the result is ready in the caller's
+ * stream order.  Workspaces are per (device, stream): MSMs on different streams run concurrently.
+ * No reference counterpart. */
 int hipbp_msm_pippenger(ge25519* result, const fe25519* scalars, const ge25519* points, size_t n,
                         int window_bits, void* stream);
 /* Canonical tree over n device points: for stride 1, 2, 4, ...: T[i] = Ndev(T[i] + T[i+stride])

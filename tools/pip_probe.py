@@ -1,5 +1,8 @@
-"""Run hipbp_msm_pippenger on the 2^20 config-3 inputs a few times (for rocprofv3).
-    python tools/pip_probe.py [log2_n] [window_bits] [reps]"""
+"""Run hipbp_msm_pippenger on the 2^20 config-3 inputs (for rocprofv3 and stream A/B runs).
+    python tools/pip_probe.py [log2_n] [window_bits] [reps] [streams]
+streams > 1: reps MSMs rotate over that many streams (independent workspaces); prints the
+throughput and checks every result against the single-stream one."""
+import hashlib
 import os
 import sys
 import time
@@ -14,6 +17,7 @@ from cudabulletproof_amd import synth  # noqa: E402
 lg = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 c = int(sys.argv[2]) if len(sys.argv) > 2 else 12
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+ns = int(sys.argv[4]) if len(sys.argv) > 4 else 1
 dev = torch.device("cuda:0")
 bp.lib()
 s, P = synth.msm_config3(0, 1 << lg, dev)
@@ -22,8 +26,24 @@ sd, Pd = T(s), T(P)
 out = torch.zeros(16, dtype=torch.int64, device=dev)
 bp.msm_pippenger(out, sd, Pd, c)
 torch.cuda.synchronize()
+ref = hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest()[:16]
 t0 = time.perf_counter()
 for _ in range(reps):
     bp.msm_pippenger(out, sd, Pd, c)
 torch.cuda.synchronize()
-print(f"n=2^{lg} c={c}: {(time.perf_counter() - t0) / reps * 1e3:.3f} ms")
+dt = (time.perf_counter() - t0) / reps
+print(f"n=2^{lg} c={c}: {dt * 1e3:.3f} ms  {(1 << lg) / dt / 1e6:.1f} M points/s  digest {ref}", flush=True)
+if ns > 1:
+    st = [torch.cuda.Stream(dev) for _ in range(ns)]
+    outs = [torch.zeros(reps, 16, dtype=torch.int64, device=dev) for _ in range(ns)]
+    for i in range(ns):   # warm each stream's workspace
+        bp.msm_pippenger(outs[i][0], sd, Pd, c, stream=st[i])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(reps):
+        bp.msm_pippenger(outs[k % ns][k], sd, Pd, c, stream=st[k % ns])
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    ok = all(hashlib.sha256(outs[k % ns][k].cpu().numpy().tobytes()).hexdigest()[:16] == ref for k in range(reps))
+    print(f"  {ns} streams: {dt * 1e3:.3f} ms per MSM  {(1 << lg) / dt / 1e6:.1f} M points/s  same bits: {ok}",
+          flush=True)
