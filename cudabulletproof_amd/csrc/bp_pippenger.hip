@@ -190,11 +190,17 @@ __global__ __launch_bounds__(PTPB) void k_pip_step(int t, const unsigned* __rest
     const uint32_t r = L - j < 4 ? L - j : 4;
     const size_t base = first ? (size_t)start[b] + j : (size_t)off[b] + j;
     auto load = [&](uint32_t t) -> ge { return first ? P[vals[base + t]] : Qin[base + t]; };
+    // the first level adds two input points: when every active lane's second one has Z exactly 1
+    // (affine inputs, a wave-uniform test), Z1 Z2 is fe_mul_one(Z1) — same bits, no product
+    auto add_in = [&](const ge& a, const ge& b) -> ge {
+        const geq q = ge_prep(b);
+        return ge_add_qp<false>(a, &q, first && __all(fe_is_one(b.Z)));
+    };
     ge y0 = load(0);
-    if (r > 1) y0 = ge_add(y0, load(1));
+    if (r > 1) y0 = add_in(y0, load(1));
     if (r > 2) {
         ge y1 = load(2);
-        if (r > 3) y1 = ge_add(y1, load(3));
+        if (r > 3) y1 = add_in(y1, load(3));
         y0 = ge_add(y0, y1);
     }
     const uint32_t o = off2[b] + j / 4;
@@ -382,6 +388,13 @@ inline unsigned nb_of(size_t items) { return (unsigned)((items + PTPB - 1) / PTP
 
 #define PIP_RET(x) do { hipError_t _e = (x); if (_e != hipSuccess) return _e; } while (0)
 
+// stable sort of (key, value) pairs on the low `bits` key bits (hipCUB onesweep: 2 passes for 12
+// bits; a single 12-bit pass does not fit the LDS, and custom 6/8-bit configurations make 2 too)
+static hipError_t pip_sort(void* temp, size_t& tb, const uint32_t* kin, uint32_t* kout, const uint32_t* vin,
+                           uint32_t* vout, size_t N, int bits, hipStream_t s) {
+    return hipcub::DeviceRadixSort::SortPairs(temp, tb, kin, kout, vin, vout, (int)N, 0, bits, s);
+}
+
 // Bucket sums of windows [w0, w1) on stream s (they end on ping-pong side pip_steps & 1).
 static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, int c, int w0, int w1,
                               hipStream_t s) {
@@ -404,15 +417,15 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
     PIP_RET(ws.V.need((size_t)W * NC * sizeof(ge)));
     PIP_RET(ws.maxlen.need(sizeof(unsigned)));
     size_t tb_sort = 0, tb_scan = 0;
-    PIP_RET(hipcub::DeviceRadixSort::SortPairs(nullptr, tb_sort, ws.keys_in.as<uint32_t>(), ws.keys.as<uint32_t>(),
-                                               ws.vals_in.as<uint32_t>(), ws.vals.as<uint32_t>(), (int)N, 0, kbits, s));
+    PIP_RET(pip_sort(nullptr, tb_sort, ws.keys_in.as<uint32_t>(), ws.keys.as<uint32_t>(),
+                     ws.vals_in.as<uint32_t>(), ws.vals.as<uint32_t>(), N, kbits, s));
     PIP_RET(hipcub::DeviceScan::ExclusiveSum(nullptr, tb_scan, ws.pad[0].as<uint32_t>(), ws.off[0].as<uint32_t>(),
                                              (int)nb, s));
     PIP_RET(ws.temp.need(tb_sort > tb_scan ? tb_sort : tb_scan));
 
     k_pip_keys<<<nb_of(N), PTPB, 0, s>>>(scal, n, c, w0, W, ws.keys_in.as<uint32_t>(), ws.vals_in.as<uint32_t>());
-    PIP_RET(hipcub::DeviceRadixSort::SortPairs(ws.temp.p, tb_sort, ws.keys_in.as<uint32_t>(), ws.keys.as<uint32_t>(),
-                                               ws.vals_in.as<uint32_t>(), ws.vals.as<uint32_t>(), (int)N, 0, kbits, s));
+    PIP_RET(pip_sort(ws.temp.p, tb_sort, ws.keys_in.as<uint32_t>(), ws.keys.as<uint32_t>(),
+                     ws.vals_in.as<uint32_t>(), ws.vals.as<uint32_t>(), N, kbits, s));
     PIP_RET(hipMemsetAsync(ws.start.p, 0, nb * 4, s));
     PIP_RET(hipMemsetAsync(ws.len[0].p, 0, nb * 4, s));
     PIP_RET(hipMemsetAsync(ws.maxlen.p, 0, sizeof(unsigned), s));
