@@ -9,9 +9,10 @@
 //   in index order;  chunk k of M = 16 buckets: running sums R, S, then V = S + (kM) R;
 //   S_w = pairwise tree over the chunks;  T = Horner over the windows (c doublings + add).
 //
-// GPU mapping.  (1) one (key = w<<c | digit, value = i) pair per window and point, generated
-// window-major, stable radix sort (hipCUB) on the digit bits -> each bucket's points contiguous in
-// index order; bucket bounds from the sorted keys (no atomics).  (2) the bucket trees level by level over ALL buckets at once: a level's
+// GPU mapping.  (1) one (key = digit, value = w n + i) pair per window and point, generated
+// window-major, stable radix sort (rocPRIM, 16-bit keys, values from a counting iterator) on the
+// digit bits -> each bucket's points contiguous in index order; bucket bounds from the sorted
+// pairs (no atomics).  (2) the bucket trees level by level over ALL buckets at once: a level's
 // lane takes one adjacent pair of one bucket's current list (lists compacted and padded to even
 // length after every level, offsets by an exclusive scan), so every lane of every wave adds —
 // ~W n point additions at the VALU roof instead of one lane walking a bucket.  (3) one lane per
@@ -21,6 +22,8 @@
 // The host never waits: the tree depth is read on the device (pip_steps), so independent MSMs
 // on different streams overlap one's latency-bound chains with another's bucket trees.
 #include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 
 #include <map>
 #include <mutex>
@@ -34,9 +37,12 @@ namespace {
 constexpr int PTPB = 256;
 constexpr int PM = 16;   // buckets per chunk
 
-// windows w0 .. w0+W-1 (local index lw = w - w0 in the key)
+// Sort input: element g = lw n + i (window lw = w - w0, point i), generated window-major; its
+// key is the c-bit digit alone (16 bits) and its value is g itself (a counting iterator, never
+// stored), so after a STABLE sort on the digit each bucket (lw, d) is contiguous and in index
+// order, and the bucket of a sorted element is ((g / n) << c) | digit.
 __global__ __launch_bounds__(PTPB) void k_pip_keys(const fe* __restrict__ s, size_t n, int c, int w0, int W,
-                                                  uint32_t* keys, uint32_t* vals) {
+                                                  uint16_t* keys) {
     const size_t g = (size_t)blockIdx.x * PTPB + threadIdx.x;
     if (g >= (size_t)W * n) return;
     const int w = (int)(g / n);
@@ -47,19 +53,23 @@ __global__ __launch_bounds__(PTPB) void k_pip_keys(const fe* __restrict__ s, siz
     const int li = lo >> 6, sh = lo & 63;
     uint64_t v = sc[li] >> sh;
     if (sh && li < 3) v |= sc[li + 1] << (64 - sh);
-    const uint32_t d = (uint32_t)(v & ((1ull << c) - 1));
-    keys[g] = ((uint32_t)w << c) | d;
-    vals[g] = (uint32_t)i;
+    keys[g] = (uint16_t)(v & ((1ull << c) - 1));
 }
 
-// first/last occurrence of each key in the sorted array -> bucket start and length
-__global__ __launch_bounds__(PTPB) void k_pip_bounds(const uint32_t* __restrict__ keys, size_t N,
+__device__ __forceinline__ uint32_t pip_bucket(const uint16_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+                                               size_t p, uint32_t n, int c) {
+    return ((vals[p] / n) << c) | keys[p];
+}
+
+// first/last occurrence of each bucket in the sorted array -> bucket start and length
+__global__ __launch_bounds__(PTPB) void k_pip_bounds(const uint16_t* __restrict__ keys,
+                                                    const uint32_t* __restrict__ vals, size_t N, uint32_t n, int c,
                                                     uint32_t* start, uint32_t* len) {
     const size_t p = (size_t)blockIdx.x * PTPB + threadIdx.x;
     if (p >= N) return;
-    const uint32_t k = keys[p];
-    if (p == 0 || keys[p - 1] != k) start[k] = (uint32_t)p;
-    if (p == N - 1 || keys[p + 1] != k) len[k] = (uint32_t)(p + 1);   // end, made a length below
+    const uint32_t k = pip_bucket(keys, vals, p, n, c);
+    if (p == 0 || pip_bucket(keys, vals, p - 1, n, c) != k) start[k] = (uint32_t)p;
+    if (p == N - 1 || pip_bucket(keys, vals, p + 1, n, c) != k) len[k] = (uint32_t)(p + 1);   // end, made a length below
 }
 
 // Bucket lists are processed two tree levels per launch ("steps"): a step's lane takes one
@@ -163,16 +173,17 @@ __global__ __launch_bounds__(PTPB) void k_pip_scan_fin(int t, const unsigned* __
     }
 }
 
-__global__ __launch_bounds__(PTPB) void k_pip_bid0(const uint32_t* __restrict__ keys, size_t N,
-                                                  const uint32_t* __restrict__ start, const uint32_t* __restrict__ off,
-                                                  uint32_t* bid) {
+__global__ __launch_bounds__(PTPB) void k_pip_bid0(const uint16_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+                                                  size_t N, uint32_t n, int c, const uint32_t* __restrict__ start,
+                                                  const uint32_t* __restrict__ off, uint32_t* bid) {
     const size_t p = (size_t)blockIdx.x * PTPB + threadIdx.x;
     if (p >= N) return;
-    const uint32_t b = keys[p];
+    const uint32_t b = pip_bucket(keys, vals, p, n, c);
     bid[off[b] + (p - start[b])] = b;
 }
 
 __global__ __launch_bounds__(PTPB) void k_pip_step(int t, const unsigned* __restrict__ maxlen, const ge* __restrict__ P,
+                                                  uint32_t n,
                                                   const uint32_t* __restrict__ vals,
                                                   const uint32_t* __restrict__ start, const ge* __restrict__ Qin,
                                                   const uint32_t* __restrict__ bid, const uint32_t* __restrict__ off,
@@ -189,7 +200,7 @@ __global__ __launch_bounds__(PTPB) void k_pip_step(int t, const unsigned* __rest
     const uint32_t j = pos - off[b], L = len[b];
     const uint32_t r = L - j < 4 ? L - j : 4;
     const size_t base = first ? (size_t)start[b] + j : (size_t)off[b] + j;
-    auto load = [&](uint32_t t) -> ge { return first ? P[vals[base + t]] : Qin[base + t]; };
+    auto load = [&](uint32_t t) -> ge { return first ? P[vals[base + t] % n] : Qin[base + t]; };
     // the first level adds two input points: when every active lane's second one has Z exactly 1
     // (affine inputs, a wave-uniform test), Z1 Z2 is fe_mul_one(Z1) — same bits, no product
     auto add_in = [&](const ge& a, const ge& b) -> ge {
@@ -371,7 +382,7 @@ struct DBuf {
     template <typename T> T* as() const { return (T*)p; }
 };
 struct PipWs {
-    DBuf keys_in, vals_in, keys, vals, temp, start, len[2], pad[2], off[2], bid[2], Q[2], V, Sw, Tmid, maxlen, part;
+    DBuf keys_in, keys, vals, temp, start, len[2], pad[2], off[2], bid[2], Q[2], V, Sw, Tmid, maxlen, part;
     hipStream_t side = nullptr;           // the Horner chain's stream
     hipEvent_t ev[4] = {};   // [1] top half's buckets done, [2] bottom half done, [3] chain done
 };
@@ -388,11 +399,12 @@ inline unsigned nb_of(size_t items) { return (unsigned)((items + PTPB - 1) / PTP
 
 #define PIP_RET(x) do { hipError_t _e = (x); if (_e != hipSuccess) return _e; } while (0)
 
-// stable sort of (key, value) pairs on the low `bits` key bits (hipCUB onesweep: 2 passes for 12
-// bits; a single 12-bit pass does not fit the LDS, and custom 6/8-bit configurations make 2 too)
-static hipError_t pip_sort(void* temp, size_t& tb, const uint32_t* kin, uint32_t* kout, const uint32_t* vin,
-                           uint32_t* vout, size_t N, int bits, hipStream_t s) {
-    return hipcub::DeviceRadixSort::SortPairs(temp, tb, kin, kout, vin, vout, (int)N, 0, bits, s);
+// stable sort of the 16-bit digit keys on their low `bits` bits, values = 0, 1, 2, ... (rocPRIM
+// onesweep with a counting iterator: 2 passes for 12 bits, no value array read)
+static hipError_t pip_sort(void* temp, size_t& tb, const uint16_t* kin, uint16_t* kout, uint32_t* vout, size_t N,
+                           int bits, hipStream_t s) {
+    return rocprim::radix_sort_pairs(temp, tb, kin, kout, rocprim::counting_iterator<uint32_t>(0u), vout,
+                                     (unsigned)N, 0u, (unsigned)bits, s);
 }
 
 // Bucket sums of windows [w0, w1) on stream s (they end on ping-pong side pip_steps & 1).
@@ -404,8 +416,8 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
     // keys are generated window-major, so a STABLE sort on the c digit bits alone leaves each
     // (window, digit) bucket contiguous and in index order (buckets ordered digit-major)
     const int kbits = c;
-    PIP_RET(ws.keys_in.need(N * 4)); PIP_RET(ws.vals_in.need(N * 4));
-    PIP_RET(ws.keys.need(N * 4)); PIP_RET(ws.vals.need(N * 4));
+    PIP_RET(ws.keys_in.need(N * 2));
+    PIP_RET(ws.keys.need(N * 2)); PIP_RET(ws.vals.need(N * 4));
     PIP_RET(ws.start.need(nb * 4));
     for (int i = 0; i < 2; i++) {
         PIP_RET(ws.len[i].need(nb * 4)); PIP_RET(ws.pad[i].need(nb * 4)); PIP_RET(ws.off[i].need(nb * 4));
@@ -417,25 +429,26 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
     PIP_RET(ws.V.need((size_t)W * NC * sizeof(ge)));
     PIP_RET(ws.maxlen.need(sizeof(unsigned)));
     size_t tb_sort = 0, tb_scan = 0;
-    PIP_RET(pip_sort(nullptr, tb_sort, ws.keys_in.as<uint32_t>(), ws.keys.as<uint32_t>(),
-                     ws.vals_in.as<uint32_t>(), ws.vals.as<uint32_t>(), N, kbits, s));
+    PIP_RET(pip_sort(nullptr, tb_sort, ws.keys_in.as<uint16_t>(), ws.keys.as<uint16_t>(), ws.vals.as<uint32_t>(), N,
+                     kbits, s));
     PIP_RET(hipcub::DeviceScan::ExclusiveSum(nullptr, tb_scan, ws.pad[0].as<uint32_t>(), ws.off[0].as<uint32_t>(),
                                              (int)nb, s));
     PIP_RET(ws.temp.need(tb_sort > tb_scan ? tb_sort : tb_scan));
 
-    k_pip_keys<<<nb_of(N), PTPB, 0, s>>>(scal, n, c, w0, W, ws.keys_in.as<uint32_t>(), ws.vals_in.as<uint32_t>());
-    PIP_RET(pip_sort(ws.temp.p, tb_sort, ws.keys_in.as<uint32_t>(), ws.keys.as<uint32_t>(),
-                     ws.vals_in.as<uint32_t>(), ws.vals.as<uint32_t>(), N, kbits, s));
+    k_pip_keys<<<nb_of(N), PTPB, 0, s>>>(scal, n, c, w0, W, ws.keys_in.as<uint16_t>());
+    PIP_RET(pip_sort(ws.temp.p, tb_sort, ws.keys_in.as<uint16_t>(), ws.keys.as<uint16_t>(), ws.vals.as<uint32_t>(), N,
+                     kbits, s));
     PIP_RET(hipMemsetAsync(ws.start.p, 0, nb * 4, s));
     PIP_RET(hipMemsetAsync(ws.len[0].p, 0, nb * 4, s));
     PIP_RET(hipMemsetAsync(ws.maxlen.p, 0, sizeof(unsigned), s));
-    k_pip_bounds<<<nb_of(N), PTPB, 0, s>>>(ws.keys.as<uint32_t>(), N, ws.start.as<uint32_t>(), ws.len[0].as<uint32_t>());
+    k_pip_bounds<<<nb_of(N), PTPB, 0, s>>>(ws.keys.as<uint16_t>(), ws.vals.as<uint32_t>(), N, (uint32_t)n, c,
+                                           ws.start.as<uint32_t>(), ws.len[0].as<uint32_t>());
     k_pip_len0<<<nb_of(nb), PTPB, 0, s>>>(ws.start.as<uint32_t>(), ws.len[0].as<uint32_t>(), ws.pad[0].as<uint32_t>(),
                                           nb, ws.maxlen.as<unsigned>());
     PIP_RET(hipcub::DeviceScan::ExclusiveSum(ws.temp.p, tb_scan, ws.pad[0].as<uint32_t>(), ws.off[0].as<uint32_t>(),
                                              (int)nb, s));
-    k_pip_bid0<<<nb_of(N), PTPB, 0, s>>>(ws.keys.as<uint32_t>(), N, ws.start.as<uint32_t>(), ws.off[0].as<uint32_t>(),
-                                         ws.bid[0].as<uint32_t>());
+    k_pip_bid0<<<nb_of(N), PTPB, 0, s>>>(ws.keys.as<uint16_t>(), ws.vals.as<uint32_t>(), N, (uint32_t)n, c,
+                                         ws.start.as<uint32_t>(), ws.off[0].as<uint32_t>(), ws.bid[0].as<uint32_t>());
     // the worst-case step count (a bucket list is at most n long); steps past the depth of the
     // data exit on the device (pip_steps), so nothing here waits for the GPU
     int levels = 1;
@@ -452,7 +465,7 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
                                                 ws.part.as<uint32_t>());
         k_pip_scan_fin<<<nparts, PTPB, 0, s>>>(t, ws.maxlen.as<unsigned>(), ws.pad[b].as<uint32_t>(),
                                                ws.part.as<uint32_t>(), nb, ws.off[b].as<uint32_t>());
-        k_pip_step<<<nb_of(lanes), PTPB, 0, s>>>(t, ws.maxlen.as<unsigned>(), P, ws.vals.as<uint32_t>(),
+        k_pip_step<<<nb_of(lanes), PTPB, 0, s>>>(t, ws.maxlen.as<unsigned>(), P, (uint32_t)n, ws.vals.as<uint32_t>(),
                                                   ws.start.as<uint32_t>(), ws.Q[a].as<ge>(), ws.bid[a].as<uint32_t>(),
                                                   ws.off[a].as<uint32_t>(), ws.len[a].as<uint32_t>(),
                                                   ws.pad[a].as<uint32_t>(), ws.off[b].as<uint32_t>(), ws.Q[b].as<ge>(),
