@@ -568,6 +568,86 @@ def test_fold_corners_vs_reference_rule(bp):
         assert [int(x) for x in got[i]] == _ref_fold(t), (i, [hex(x) for x in t])
 
 
+def _edge_cases(op, rng):
+    """Operand pairs that put one lane on each rare edge the field asm tests for (fe_add_asm /
+    fe_sub_asm / fe_fold_asm in field_asm.h): every exact-form branch taken by exactly the case
+    that needs it."""
+    P0, P3 = P_LIMBS[0], P_LIMBS[3]
+    r = lambda: int(rng.integers(0, 2**64, dtype=np.uint64))
+    top = lambda: r() | (1 << 63)
+    fix = [[r(), r(), M64, top()], [P0 + 3, r(), r(), top()], [P0, M64, M64, P3], [P0 + 18, M64, M64, P3],
+           [P0 + 5, M64, r(), top()], [r(), r(), M64, P3], [M64, M64, M64, M64], [P0 - 1, r(), M64, top()]]
+    out = []
+    if op in ("add", "fold"):   # the fix-up's edges: b = 0 makes the sum / fold the edge vector itself
+        out += [(f, [0, 0, 0, 0]) for f in fix]
+    if op == "fold":            # x_i = 19 WRAP19 = 2^64 - 1: the reference's dropped carry
+        for i in (1, 2, 3):
+            for _ in range(3):
+                hi = [r() if k != i else WRAP19 for k in range(4)]
+                out.append(([r(), r(), r(), r()], hi))
+    if op == "sub":
+        for i in (1, 2, 3):     # g_i = 2^64 - 1: the lossy borrow
+            for _ in range(3):
+                out.append(([r(), r(), r(), r()], [r() if k != i else M64 for k in range(4)]))
+        for t in ([5, r(), r(), 7], [18, r(), r(), 9], [0, r(), r(), 3], [r() | 0x100, M64, r(), 5],
+                  [r() | 0x100, r(), M64, 6], [2, M64, M64, 1]):   # the "+ p" pass's edges, with a borrow
+            g = [r(), r() & 0xFFFFFFFF7FFFFFFF, r() & 0xFFFFFFFF7FFFFFFF, 0xFFFFFFFFFFFFFFFE]
+            tv = sum(x << (64 * k) for k, x in enumerate(t))
+            gv = sum(x << (64 * k) for k, x in enumerate(g))
+            av = (tv + gv) % (1 << 256)
+            assert av < gv
+            out.append(([(av >> (64 * k)) & M64 for k in range(4)], g))
+    return out
+
+
+@pytest.mark.parametrize("op", ["add", "sub", "fold", "mul"])
+def test_field_fast_forms_one_edge_lane_per_wave(bp, oracle, op):
+    """The field asm runs a short form unless some lane of the wave sits on one of the rare edges
+    (a limb or word equal to 2^64-1 / 2^32-1, t0 >= p0, t0 < 19): the exact form then runs for the
+    whole wave.  Here each edge case sits alone in its own wave, at a rotating lane, among 63
+    common lanes (the exact form must give those the same bits); further waves hold edge limbs at
+    random, and the last ones near-edge values only (words 2^32-2, high words all ones with low
+    words not) that the short form must get right."""
+    import torch
+    rng = np.random.default_rng({"add": 1, "sub": 2, "fold": 3, "mul": 4}[op])
+    cases = _edge_cases(op, rng)
+    waves = len(cases) + 64
+    N = 64 * waves
+    a = rand_fe(rng, N, top=True)
+    b = rand_fe(rng, N, top=True)
+    for w, (f, g) in enumerate(cases):
+        i = 64 * w + (w * 37) % 64
+        a[i], b[i] = np.array(f, np.uint64), np.array(g, np.uint64)
+    edges = [M64, M64 - 1, 0xFFFFFFFF00000000, 0x00000000FFFFFFFF, P_LIMBS[0], P_LIMBS[0] - 1, 18, 19, 0,
+             P_LIMBS[3], 1 << 63, WRAP19, WRAP19 + 1, 0xFFFFFFFFFFFFFFEE]
+    for w in range(len(cases), len(cases) + 32):   # one lane with edge limbs at random
+        i = 64 * w + (w * 37) % 64
+        for arr in (a, b):
+            for limb in range(4):
+                if rng.random() < 0.6:
+                    arr[i, limb] = np.uint64(edges[int(rng.integers(0, len(edges)))])
+    near = [0xFFFFFFFEFFFFFFFE, 0xFFFFFFFE00000000, 0xFFFFFFFF7FFFFFFF, 0x7FFFFFFFFFFFFFFE, 0xFFFFFFFEFFFFFFFF,
+            20, 0x100000000, 0xFFFFFFFEFFFFFF00]
+    for w in range(len(cases) + 32, waves):   # near-edge values only (the short form)
+        for i in range(64 * w, 64 * w + 64):
+            for arr in (a, b):
+                for limb in range(4):
+                    if rng.random() < 0.5:
+                        arr[i, limb] = np.uint64(near[int(rng.integers(0, len(near)))])
+    dev = torch.device("cuda:0")
+    T = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(np.int64)).to(dev)
+    r = torch.empty(N, 4, dtype=torch.int64, device=dev)
+    bp.field_op(op, r, T(a), T(b))
+    torch.cuda.synchronize()
+    got = r.cpu().numpy().view(np.uint64)
+    for i in range(N):
+        if op == "fold":
+            want = _ref_fold([int(x) for x in a[i]] + [int(x) for x in b[i]])
+        else:
+            want = [int(x) for x in getattr(oracle, "fe_" + op)(a[i], b[i])]
+        assert [int(x) for x in got[i]] == want, (op, i, [hex(int(x)) for x in a[i]], [hex(int(x)) for x in b[i]])
+
+
 def test_sq_matches_mul(bp, oracle):
     """Dedicated squaring (36 products) == fe25519_mul(x, x) on edge-heavy limbs."""
     import torch

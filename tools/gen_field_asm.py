@@ -20,9 +20,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 OUT = os.path.join(HERE, "..", "cudabulletproof_amd", "csrc", "field_asm.h")
 
 
-def schedule(ins):
-    """ins: (text, sgpr_writes, sgpr_reads, is_valu).  Returns the lines with s_nop inserted."""
+def schedule(ins, state=None):
+    """ins: (text, sgpr_writes, sgpr_reads, is_valu).  Returns the lines with s_nop inserted and the
+    end state {sgpr: wait states since its VALU write}.  `state` carries the predecessors' end
+    state into a segment (branch targets: the merged, most recent writes)."""
     lines, pos, wpos = [], 0, {}
+    for r, d in (state or {}).items():
+        wpos[r] = -1 - d
     for text, writes, reads, is_valu in ins:
         if is_valu:
             need = 0
@@ -39,7 +43,15 @@ def schedule(ins):
             else:
                 wpos.pop(w, None)
         pos += 1
-    return lines
+    return lines, {r: pos - p - 1 for r, p in wpos.items()}
+
+
+def merge(*states):
+    out = {}
+    for st in states:
+        for r, d in st.items():
+            out[r] = min(d, out.get(r, d))
+    return out
 
 
 def V(t, w=(), r=()):
@@ -93,12 +105,39 @@ def fix_seq(h, o, carry):
 FIX_SGPRS = ["sf1", "sf2", "se3", "stp", "sg0", "sg1", "sm", "sd1", "sd2", "sd3", "sk0", "sk1", "sk2", "sk3"]
 
 
-def emit(name, doc, args, ins, outs, vtemps, sgprs, body):
-    """args: [(param, prefix)] array params bound to scalars prefix0..7."""
+def fix_test(h, carry):
+    """Wave-uniform test for fix_seq's fast form.  With h0 < P0 (br1 = 1) the fix-up's m is
+    carry | top (the equality case needs h0 >= P0), br2 = 0 and br3 = !(h2 == M), so when also
+    h2 != M every lane's result is h + m (19, 0, 1, 2^63).  h0 >= P0 implies h0's high word is
+    2^32-1 and h2 == M implies its low word is: srare = max(those words) == 2^32-1 is a superset of
+    the lanes that need the exact form.  Also forms m = carry | top in sm."""
+    return [V(f"v_max_u32 %[vt3], %[{h[1]}], %[{h[4]}]"),
+            V(f"v_cmp_gt_i32 %[stp], 0, %[{h[7]}]", ["stp"]),
+            V("v_cmp_eq_u32 %[srare], -1, %[vt3]", ["srare"]),
+            S(f"s_or_b64 %[sm], %[{carry}], %[stp]", ["sm"])]
+
+
+def fix_fast(h):
+    """h += m (19, 0, 1, 2^63) per limb, in place (valid when fix_test found no rare lane)."""
+    return [V("v_cndmask_b32 %[vt1], 0, 19, %[sm]", [], ["sm"]),
+            V("v_cndmask_b32 %[vt2], 0, %[c80], %[sm]", [], ["sm"]),
+            V(f"v_add_co_u32 %[{h[0]}], %[sk0], %[{h[0]}], %[vt1]", ["sk0"]),
+            V(f"v_addc_co_u32 %[{h[4]}], %[sk2], %[{h[4]}], 0, %[sm]", ["sk2"], ["sm"]),
+            V(f"v_add_u32 %[{h[7]}], %[{h[7]}], %[vt2]"),
+            V(f"v_addc_co_u32 %[{h[1]}], %[sk0], %[{h[1]}], 0, %[sk0]", ["sk0"], ["sk0"]),
+            V(f"v_addc_co_u32 %[{h[5]}], %[sk2], %[{h[5]}], 0, %[sk2]", ["sk2"], ["sk2"])]
+
+
+def branch_if_rare(label):
+    return [S("s_cmp_lg_u64 %[srare], 0"), S(f"s_cbranch_scc1 {label}")]
+
+
+def emit(name, doc, args, ins, outs, vtemps, sgprs, lines):
+    """args: [(param, prefix)] array params bound to scalars prefix0..7.  lines: scheduled asm."""
     # the block's last VALU instructions write SGPRs (carry-outs) that the compiler may reuse at once
     # for a VMEM address: a VALU SGPR write followed by a VMEM read of it needs 5 wait states
     # (gfx940/gfx950), and the compiler does not see inside the block
-    text = "\\n\\t".join(schedule(body) + ["s_nop 4"])
+    text = "\\n\\t".join(lines + ["s_nop 4"])
     out = [f"// {d}" for d in doc]
     out.append(f"__device__ __forceinline__ void {name}(uint32_t out[8], " +
                ", ".join(f"const uint32_t {p}[8]" for p, _ in args) + ") {")
@@ -121,83 +160,134 @@ def emit(name, doc, args, ins, outs, vtemps, sgprs, body):
     return out
 
 
+def two_way(pre, fast, slow):
+    """pre; if any lane is rare: slow, else fast (wave-uniform branch on srare, set in pre).
+    Layout: pre, branch, fast, s_branch to the end, slow (label 3), end (label 4)."""
+    lp, sp = schedule(pre + branch_if_rare("3f"))
+    lf, sf = schedule(fast, sp)
+    ls, ss = schedule(slow, sp)
+    _, _ = merge(sf, ss), None
+    return lp + lf + ["s_branch 4f", "3:"] + ls + ["4:"]
+
+
 def gen_add():
     h = [f"h{i}" for i in range(8)]
-    o = [f"o{i}" for i in range(8)]
-    q = [V("v_add_co_u32 %[h0], %[scy], %[a0], %[b0]", ["scy"])]
+    chain = [V("v_add_co_u32 %[h0], %[scy], %[a0], %[b0]", ["scy"])]
     for i in range(1, 8):
-        q.append(V(f"v_addc_co_u32 %[h{i}], %[scy], %[a{i}], %[b{i}], %[scy]", ["scy"], ["scy"]))
-    q += fix_seq(h, o, "scy")
+        chain.append(V(f"v_addc_co_u32 %[h{i}], %[scy], %[a{i}], %[b{i}], %[scy]", ["scy"], ["scy"]))
+    lines = two_way(chain + fix_test(h, "scy"), fix_fast(h), fix_seq(h, h, "scy"))
     return emit("fe_add_asm", ["fe25519_add (curve25519_ops.cu:41-68) on limb halves: exact 257-bit sum, then",
-                               "one lossy \"- p\" when it carried out or is >= p."],
+                               "one lossy \"- p\" when it carried out or is >= p (fast form unless a lane is",
+                               "on one of the fix-up's rare edges: fix_test)."],
                 [("fa", "a"), ("ga", "b")], [f"a{i}" for i in range(8)] + [f"b{i}" for i in range(8)],
-                o, h + ["vt1", "vt2", "vt3"], FIX_SGPRS + ["scy"], q)
+                h, ["vt1", "vt2", "vt3"], FIX_SGPRS + ["scy", "srare"], lines)
 
 
 def gen_fold():
+    """Two wave-uniform branches: (1) some x_i (i = 1..3) may be 2^64-1 (its low word is), so the
+    lossy carry can differ from the true one -> the exact chain + exact fix-up; else the plain
+    carry chain, then (2) fix_test -> fast or exact fix-up."""
     h = [f"h{i}" for i in range(8)]
-    o = [f"o{i}" for i in range(8)]
-    q = []
+    test1 = [V("v_max3_u32 %[vt3], %[x2], %[x4], %[x6]"),
+             V("v_cmp_eq_u32 %[srare], -1, %[vt3]", ["srare"])]
+    plain = [V("v_add_co_u32 %[h0], %[scy], %[a0], %[x0]", ["scy"])]
+    for i in range(1, 8):
+        plain.append(V(f"v_addc_co_u32 %[h{i}], %[scy], %[a{i}], %[x{i}], %[scy]", ["scy"], ["scy"]))
+    exact = []
     for i in (1, 2, 3):   # x_i == 2^64-1 (limb 0 has no carry-in)
-        q.append(V(f"v_and_b32 %[vt1], %[x{2 * i}], %[x{2 * i + 1}]"))
-        q.append(V(f"v_cmp_eq_u32 %[sq{i}], -1, %[vt1]", [f"sq{i}"]))
-    q.append(V("v_add_co_u32 %[h0], %[sk0], %[a0], %[x0]", ["sk0"]))
-    q.append(V("v_addc_co_u32 %[h1], %[scy], %[a1], %[x1], %[sk0]", ["scy"], ["sk0"]))
+        exact.append(V(f"v_and_b32 %[vt1], %[x{2 * i}], %[x{2 * i + 1}]"))
+        exact.append(V(f"v_cmp_eq_u32 %[sq{i}], -1, %[vt1]", [f"sq{i}"]))
+    exact.append(V("v_add_co_u32 %[h0], %[sk0], %[a0], %[x0]", ["sk0"]))
+    exact.append(V("v_addc_co_u32 %[h1], %[scy], %[a1], %[x1], %[sk0]", ["scy"], ["sk0"]))
     for i in (1, 2, 3):
-        q.append(V(f"v_addc_co_u32 %[h{2 * i}], %[sk0], %[a{2 * i}], %[x{2 * i}], %[scy]", ["sk0"], ["scy"]))
-        q.append(V(f"v_addc_co_u32 %[h{2 * i + 1}], %[sk1], %[a{2 * i + 1}], %[x{2 * i + 1}], %[sk0]", ["sk1"],
-                   ["sk0"]))
-        q.append(S(f"s_and_b64 %[sq{i}], %[sq{i}], %[scy]", [f"sq{i}"]))   # x_i == M & carry-in
-        q.append(S(f"s_andn2_b64 %[scy], %[sk1], %[sq{i}]", ["scy"]))      # the reference's carry
-    q += fix_seq(h, o, "scy")
+        exact.append(V(f"v_addc_co_u32 %[h{2 * i}], %[sk0], %[a{2 * i}], %[x{2 * i}], %[scy]", ["sk0"], ["scy"]))
+        exact.append(V(f"v_addc_co_u32 %[h{2 * i + 1}], %[sk1], %[a{2 * i + 1}], %[x{2 * i + 1}], %[sk0]",
+                       ["sk1"], ["sk0"]))
+        exact.append(S(f"s_and_b64 %[sq{i}], %[sq{i}], %[scy]", [f"sq{i}"]))   # x_i == M & carry-in
+        exact.append(S(f"s_andn2_b64 %[scy], %[sk1], %[sq{i}]", ["scy"]))      # the reference's carry
+    # layout: test1, branch -> 5 (exact chain); plain chain, fix_test, branch -> 3 (exact fix);
+    # fast fix, s_branch 4; 5: exact chain (falls through); 3: exact fix; 4: end
+    l1, s1 = schedule(test1 + [S("s_cmp_lg_u64 %[srare], 0"), S("s_cbranch_scc1 5f")])
+    l2, s2 = schedule(plain + fix_test(h, "scy") + branch_if_rare("3f"), s1)
+    l3, _ = schedule(fix_fast(h), s2)
+    l5, s5 = schedule(exact, s1)
+    l6, _ = schedule(fix_seq(h, h, "scy"), merge(s2, s5))
+    lines = l1 + l2 + l3 + ["s_branch 4f", "5:"] + l5 + ["3:"] + l6 + ["4:"]
     return emit("fe_fold_asm", ["Fold of the exact 512-bit product (curve25519_ops.cu:114-145): t_lo as halves",
                                 "ta[0..7], x_i = lo64(19 t_{i+4}) as halves xa[0..7]; carry chain with the lossy",
-                                "carry cy_i = c_i & !(x_i == 2^64-1 & cy_{i-1}), then the fix-up."],
+                                "carry cy_i = c_i & !(x_i == 2^64-1 & cy_{i-1}), then the fix-up.  The plain",
+                                "chain and the fast fix-up unless a lane is on a rare edge (wave-uniform tests)."],
                 [("ta", "a"), ("xa", "x")], [f"a{i}" for i in range(8)] + [f"x{i}" for i in range(8)],
-                o, h + ["vt1", "vt2", "vt3"], FIX_SGPRS + ["scy", "sq1", "sq2", "sq3"], q)
+                h, ["vt1", "vt2", "vt3"], FIX_SGPRS + ["scy", "sq1", "sq2", "sq3", "srare"], lines)
 
 
 def gen_sub():
     """fe25519_sub (curve25519_ops.cu:71-90): t = f - g with the lossy borrow
     br_i = b_i & !(g_i == 2^64-1 & br_{i-1}); on a final borrow m, the literal "+ p" pass:
     o0 = t0 - 19m; o1 = t1 - (m & t0 < 19); o2 = t2 - (m & o1 == M); o3 = t3 + m 2^63 - (m & o2 == M)
-    (fe25519_dev.h fe_sub).  m & t0 < 19 is exactly the borrow out of o0's subtraction."""
+    (fe25519_dev.h fe_sub).  m & t0 < 19 is exactly the borrow out of o0's subtraction.
+    Fast form (wave-uniform tests): no lane's g_1..g_3 may be 2^64-1 (their low words are not),
+    so the borrow chain is the plain one; and no lane has t0 < 19 (implies t0's high word is 0),
+    t1 == M or t2 == M (their low words are 2^32-1), so the "+ p" pass is t + m (-19, 0, 0, 2^63)."""
     t = [f"h{i}" for i in range(8)]
     o = [f"o{i}" for i in range(8)]
-    q = []
+    test1 = [V("v_max3_u32 %[vt3], %[b2], %[b4], %[b6]"),
+             V("v_cmp_eq_u32 %[srare], -1, %[vt3]", ["srare"])]
+    plain = [V("v_sub_co_u32 %[h0], %[scy], %[a0], %[b0]", ["scy"])]
+    for i in range(1, 8):
+        plain.append(V(f"v_subb_co_u32 %[h{i}], %[scy], %[a{i}], %[b{i}], %[scy]", ["scy"], ["scy"]))
+    test2 = [V("v_not_b32 %[vt3], %[h1]"),
+             V("v_max3_u32 %[vt3], %[vt3], %[h2], %[h4]"),
+             V("v_cmp_eq_u32 %[srare], -1, %[vt3]", ["srare"])]
+    fastp = [V("v_cndmask_b32 %[vt1], 0, 19, %[scy]", [], ["scy"]),
+             V("v_cndmask_b32 %[vt2], 0, %[c80], %[scy]", [], ["scy"]),
+             V("v_sub_co_u32 %[o0], %[sk0], %[h0], %[vt1]", ["sk0"]),
+             V("v_mov_b32 %[o2], %[h2]"), V("v_mov_b32 %[o3], %[h3]"),
+             V("v_subb_co_u32 %[o1], %[sk0], %[h1], 0, %[sk0]", ["sk0"], ["sk0"]),
+             V("v_mov_b32 %[o4], %[h4]"), V("v_mov_b32 %[o5], %[h5]"), V("v_mov_b32 %[o6], %[h6]"),
+             V("v_add_u32 %[o7], %[h7], %[vt2]")]
+    exact = []
     for i in (1, 2, 3):   # g_i == 2^64-1
-        q.append(V(f"v_and_b32 %[vt1], %[b{2 * i}], %[b{2 * i + 1}]"))
-        q.append(V(f"v_cmp_eq_u32 %[sq{i}], -1, %[vt1]", [f"sq{i}"]))
-    q.append(V("v_sub_co_u32 %[h0], %[sk0], %[a0], %[b0]", ["sk0"]))
-    q.append(V("v_subb_co_u32 %[h1], %[scy], %[a1], %[b1], %[sk0]", ["scy"], ["sk0"]))
+        exact.append(V(f"v_and_b32 %[vt1], %[b{2 * i}], %[b{2 * i + 1}]"))
+        exact.append(V(f"v_cmp_eq_u32 %[sq{i}], -1, %[vt1]", [f"sq{i}"]))
+    exact.append(V("v_sub_co_u32 %[h0], %[sk0], %[a0], %[b0]", ["sk0"]))
+    exact.append(V("v_subb_co_u32 %[h1], %[scy], %[a1], %[b1], %[sk0]", ["scy"], ["sk0"]))
     for i in (1, 2, 3):
-        q.append(V(f"v_subb_co_u32 %[h{2 * i}], %[sk0], %[a{2 * i}], %[b{2 * i}], %[scy]", ["sk0"], ["scy"]))
-        q.append(V(f"v_subb_co_u32 %[h{2 * i + 1}], %[sk1], %[a{2 * i + 1}], %[b{2 * i + 1}], %[sk0]", ["sk1"],
-                   ["sk0"]))
-        q.append(S(f"s_and_b64 %[sq{i}], %[sq{i}], %[scy]", [f"sq{i}"]))
-        q.append(S(f"s_andn2_b64 %[scy], %[sk1], %[sq{i}]", ["scy"]))      # lossy borrow
-    q += [V("v_cndmask_b32 %[vt1], 0, 19, %[scy]", [], ["scy"]),
-          V("v_cndmask_b32 %[vt2], 0, %[c80], %[scy]", [], ["scy"]),
-          V("v_sub_co_u32 %[o0], %[sk0], %[h0], %[vt1]", ["sk0"]),
-          V("v_subb_co_u32 %[o1], %[sd1], %[h1], 0, %[sk0]", ["sd1"], ["sk0"]),        # d1 = m & t0 < 19
-          V("v_subb_co_u32 %[o2], %[sk1], %[h2], 0, %[sd1]", ["sk1"], ["sd1"]),
-          V("v_subb_co_u32 %[o3], %[sk1], %[h3], 0, %[sk1]", ["sk1"], ["sk1"]),
-          V("v_and_b32 %[vt1], %[o2], %[o3]"),
-          V("v_cmp_eq_u32 %[sd2], -1, %[vt1]", ["sd2"]),
-          S("s_and_b64 %[sd2], %[sd2], %[scy]", ["sd2"]),                              # d2 = m & o1 == M
-          V("v_subb_co_u32 %[o4], %[sk2], %[h4], 0, %[sd2]", ["sk2"], ["sd2"]),
-          V("v_subb_co_u32 %[o5], %[sk2], %[h5], 0, %[sk2]", ["sk2"], ["sk2"]),
-          V("v_and_b32 %[vt1], %[o4], %[o5]"),
-          V("v_cmp_eq_u32 %[sd3], -1, %[vt1]", ["sd3"]),
-          S("s_and_b64 %[sd3], %[sd3], %[scy]", ["sd3"]),                              # d3 = m & o2 == M
-          V("v_subb_co_u32 %[o6], %[sk3], %[h6], 0, %[sd3]", ["sk3"], ["sd3"]),
-          V("v_subb_co_u32 %[vt3], %[sk3], %[h7], 0, %[sk3]", ["sk3"], ["sk3"]),
-          V("v_add_u32 %[o7], %[vt3], %[vt2]")]                                         # + m 2^63
+        exact.append(V(f"v_subb_co_u32 %[h{2 * i}], %[sk0], %[a{2 * i}], %[b{2 * i}], %[scy]", ["sk0"], ["scy"]))
+        exact.append(V(f"v_subb_co_u32 %[h{2 * i + 1}], %[sk1], %[a{2 * i + 1}], %[b{2 * i + 1}], %[sk0]",
+                       ["sk1"], ["sk0"]))
+        exact.append(S(f"s_and_b64 %[sq{i}], %[sq{i}], %[scy]", [f"sq{i}"]))
+        exact.append(S(f"s_andn2_b64 %[scy], %[sk1], %[sq{i}]", ["scy"]))      # lossy borrow
+    exactp = [V("v_cndmask_b32 %[vt1], 0, 19, %[scy]", [], ["scy"]),
+              V("v_cndmask_b32 %[vt2], 0, %[c80], %[scy]", [], ["scy"]),
+              V("v_sub_co_u32 %[o0], %[sk0], %[h0], %[vt1]", ["sk0"]),
+              V("v_subb_co_u32 %[o1], %[sd1], %[h1], 0, %[sk0]", ["sd1"], ["sk0"]),        # d1 = m & t0 < 19
+              V("v_subb_co_u32 %[o2], %[sk1], %[h2], 0, %[sd1]", ["sk1"], ["sd1"]),
+              V("v_subb_co_u32 %[o3], %[sk1], %[h3], 0, %[sk1]", ["sk1"], ["sk1"]),
+              V("v_and_b32 %[vt1], %[o2], %[o3]"),
+              V("v_cmp_eq_u32 %[sd2], -1, %[vt1]", ["sd2"]),
+              S("s_and_b64 %[sd2], %[sd2], %[scy]", ["sd2"]),                              # d2 = m & o1 == M
+              V("v_subb_co_u32 %[o4], %[sk2], %[h4], 0, %[sd2]", ["sk2"], ["sd2"]),
+              V("v_subb_co_u32 %[o5], %[sk2], %[h5], 0, %[sk2]", ["sk2"], ["sk2"]),
+              V("v_and_b32 %[vt1], %[o4], %[o5]"),
+              V("v_cmp_eq_u32 %[sd3], -1, %[vt1]", ["sd3"]),
+              S("s_and_b64 %[sd3], %[sd3], %[scy]", ["sd3"]),                              # d3 = m & o2 == M
+              V("v_subb_co_u32 %[o6], %[sk3], %[h6], 0, %[sd3]", ["sk3"], ["sd3"]),
+              V("v_subb_co_u32 %[vt3], %[sk3], %[h7], 0, %[sk3]", ["sk3"], ["sk3"]),
+              V("v_add_u32 %[o7], %[vt3], %[vt2]")]                                         # + m 2^63
+    # layout: test1, branch -> 5 (exact chain); plain chain, test2, branch -> 3 (exact "+ p");
+    # fast "+ p", s_branch 4; 5: exact chain (falls through); 3: exact "+ p"; 4: end
+    l1, s1 = schedule(test1 + [S("s_cmp_lg_u64 %[srare], 0"), S("s_cbranch_scc1 5f")])
+    l2, s2 = schedule(plain + test2 + branch_if_rare("3f"), s1)
+    l3, _ = schedule(fastp, s2)
+    l5, s5 = schedule(exact, s1)
+    l6, _ = schedule(exactp, merge(s2, s5))
+    lines = l1 + l2 + l3 + ["s_branch 4f", "5:"] + l5 + ["3:"] + l6 + ["4:"]
     return emit("fe_sub_asm", ["fe25519_sub (curve25519_ops.cu:71-90) on limb halves: lossy borrow chain, then the",
-                               "literal \"+ p\" pass on a final borrow."],
+                               "literal \"+ p\" pass on a final borrow (fast forms unless a lane is on a rare edge)."],
                 [("fa", "a"), ("ga", "b")], [f"a{i}" for i in range(8)] + [f"b{i}" for i in range(8)],
                 o, t + ["vt1", "vt2", "vt3"], ["sk0", "sk1", "sk2", "sk3", "sd1", "sd2", "sd3", "scy", "sq1", "sq2",
-                                               "sq3"], q)
+                                               "sq3", "srare"], lines)
 
 
 def main():
