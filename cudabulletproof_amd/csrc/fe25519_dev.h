@@ -104,7 +104,21 @@ BP_DEV uint64_t mul19(uint64_t x) {
 }
 
 // host fe25519_tobytes (curve25519_ops.cu:220-251) minus the byte store: canonicalising limbs.
-BP_DEV fe fe_canon(const fe& t) { return fe_cond_sub_p(t, fe_ge_p(t)); }
+BP_DEV fe fe_canon(const fe& t) {
+#if BP_FIELD_ASM && defined(__HIP_DEVICE_COMPILE__)   // generated gfx950 form (field_asm.h), same bits
+    uint32_t a[8], o[8];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        a[2 * i] = (uint32_t)t.v[i];
+        a[2 * i + 1] = (uint32_t)(t.v[i] >> 32);
+    }
+    fe_canon_asm(o, a);
+    return fe{{(uint64_t)o[0] | ((uint64_t)o[1] << 32), (uint64_t)o[2] | ((uint64_t)o[3] << 32),
+               (uint64_t)o[4] | ((uint64_t)o[5] << 32), (uint64_t)o[6] | ((uint64_t)o[7] << 32)}};
+#else
+    return fe_cond_sub_p(t, fe_ge_p(t));
+#endif
+}
 
 BP_DEV uint32_t lo32(uint64_t x) { return (uint32_t)x; }
 BP_DEV uint32_t hi32(uint64_t x) { return (uint32_t)(x >> 32); }

@@ -62,6 +62,11 @@ def S(t, w=()):
     return (t, list(w), [], False)
 
 
+def cref(carry):
+    """carry-out mask operand: an SGPR pair name, or the literal 0 (no carry)."""
+    return "0" if carry == "0" else f"%[{carry}]"
+
+
 def fix_seq(h, o, carry):
     """(carry || h >= p) ? lossy "- p" : h (curve25519_ops.cu:54-66), halves h[0..7] -> o[0..7].
     m = carry | top | (h3 == P3 & h2 == M & h1 == M & h0 >= P0);
@@ -81,7 +86,7 @@ def fix_seq(h, o, carry):
          S("s_and_b64 %[se3], %[se3], %[sf1]", ["se3"]),
          S("s_and_b64 %[se3], %[se3], %[sf2]", ["se3"]),
          S("s_and_b64 %[se3], %[se3], %[sg0]", ["se3"]),
-         S(f"s_or_b64 %[sm], %[{carry}], %[stp]", ["sm"]),
+         S(f"s_or_b64 %[sm], {cref(carry)}, %[stp]", ["sm"]),
          S("s_or_b64 %[sm], %[sm], %[se3]", ["sm"]),                      # m
          S("s_and_b64 %[sd1], %[sm], %[sg0]", ["sd1"]),                   # m & !br1
          S("s_orn2_b64 %[sg1], %[sf1], %[sg0]", ["sg1"]),                 # !br2 = f1 | !ge0
@@ -114,7 +119,7 @@ def fix_test(h, carry):
     return [V(f"v_max_u32 %[vt3], %[{h[1]}], %[{h[4]}]"),
             V(f"v_cmp_gt_i32 %[stp], 0, %[{h[7]}]", ["stp"]),
             V("v_cmp_eq_u32 %[srare], -1, %[vt3]", ["srare"]),
-            S(f"s_or_b64 %[sm], %[{carry}], %[stp]", ["sm"])]
+            S(f"s_or_b64 %[sm], {cref(carry)}, %[stp]", ["sm"])]
 
 
 def fix_fast(h):
@@ -132,8 +137,9 @@ def branch_if_rare(label):
     return [S("s_cmp_lg_u64 %[srare], 0"), S(f"s_cbranch_scc1 {label}")]
 
 
-def emit(name, doc, args, ins, outs, vtemps, sgprs, lines):
-    """args: [(param, prefix)] array params bound to scalars prefix0..7.  lines: scheduled asm."""
+def emit(name, doc, args, ins, outs, vtemps, sgprs, lines, inout=False):
+    """args: [(param, prefix)] array params bound to scalars prefix0..7.  lines: scheduled asm.
+    inout: the outputs are read-write, initialised from the first array argument."""
     # the block's last VALU instructions write SGPRs (carry-outs) that the compiler may reuse at once
     # for a VMEM address: a VALU SGPR write followed by a VMEM read of it needs 5 wait states
     # (gfx940/gfx950), and the compiler does not see inside the block
@@ -141,12 +147,17 @@ def emit(name, doc, args, ins, outs, vtemps, sgprs, lines):
     out = [f"// {d}" for d in doc]
     out.append(f"__device__ __forceinline__ void {name}(uint32_t out[8], " +
                ", ".join(f"const uint32_t {p}[8]" for p, _ in args) + ") {")
-    for p, pre in args:
-        out.append("    const uint32_t " + ", ".join(f"{pre}{i} = {p}[{i}]" for i in range(8)) + ";")
-    out.append("    uint32_t " + ", ".join(outs + vtemps) + ";")
+    if inout:
+        out.append("    uint32_t " + ", ".join(f"{x} = {args[0][0]}[{i}]" for i, x in enumerate(outs)) + ";")
+        out.append("    uint32_t " + ", ".join(vtemps) + ";")
+    else:
+        for p, pre in args:
+            out.append("    const uint32_t " + ", ".join(f"{pre}{i} = {p}[{i}]" for i in range(8)) + ";")
+        out.append("    uint32_t " + ", ".join(outs + vtemps) + ";")
     out.append("    uint64_t " + ", ".join(sgprs) + ";")
     out.append(f'    asm volatile("{text}"')
-    out.append("                 : " + ", ".join([f'[{x}] "=&v"({x})' for x in outs + vtemps] +
+    out.append("                 : " + ", ".join([f'[{x}] "{"+v" if inout else "=&v"}"({x})' for x in outs] +
+                                          [f'[{x}] "=&v"({x})' for x in vtemps] +
                                           [f'[{x}] "=&s"({x})' for x in sgprs]))
     out.append("                 : " + ", ".join([f'[{x}] "v"({x})' for x in ins] +
                                           ['[c80] "v"(0x80000000u)', '[p0l] "s"(0xFFFFFFEDu)']))
@@ -230,7 +241,6 @@ def gen_sub():
     so the borrow chain is the plain one; and no lane has t0 < 19 (implies t0's high word is 0),
     t1 == M or t2 == M (their low words are 2^32-1), so the "+ p" pass is t + m (-19, 0, 0, 2^63)."""
     t = [f"h{i}" for i in range(8)]
-    o = [f"o{i}" for i in range(8)]
     test1 = [V("v_max3_u32 %[vt3], %[b2], %[b4], %[b6]"),
              V("v_cmp_eq_u32 %[srare], -1, %[vt3]", ["srare"])]
     plain = [V("v_sub_co_u32 %[h0], %[scy], %[a0], %[b0]", ["scy"])]
@@ -241,11 +251,9 @@ def gen_sub():
              V("v_cmp_eq_u32 %[srare], -1, %[vt3]", ["srare"])]
     fastp = [V("v_cndmask_b32 %[vt1], 0, 19, %[scy]", [], ["scy"]),
              V("v_cndmask_b32 %[vt2], 0, %[c80], %[scy]", [], ["scy"]),
-             V("v_sub_co_u32 %[o0], %[sk0], %[h0], %[vt1]", ["sk0"]),
-             V("v_mov_b32 %[o2], %[h2]"), V("v_mov_b32 %[o3], %[h3]"),
-             V("v_subb_co_u32 %[o1], %[sk0], %[h1], 0, %[sk0]", ["sk0"], ["sk0"]),
-             V("v_mov_b32 %[o4], %[h4]"), V("v_mov_b32 %[o5], %[h5]"), V("v_mov_b32 %[o6], %[h6]"),
-             V("v_add_u32 %[o7], %[h7], %[vt2]")]
+             V("v_sub_co_u32 %[h0], %[sk0], %[h0], %[vt1]", ["sk0"]),
+             V("v_add_u32 %[h7], %[h7], %[vt2]"),
+             V("v_subb_co_u32 %[h1], %[sk0], %[h1], 0, %[sk0]", ["sk0"], ["sk0"])]
     exact = []
     for i in (1, 2, 3):   # g_i == 2^64-1
         exact.append(V(f"v_and_b32 %[vt1], %[b{2 * i}], %[b{2 * i + 1}]"))
@@ -260,21 +268,21 @@ def gen_sub():
         exact.append(S(f"s_andn2_b64 %[scy], %[sk1], %[sq{i}]", ["scy"]))      # lossy borrow
     exactp = [V("v_cndmask_b32 %[vt1], 0, 19, %[scy]", [], ["scy"]),
               V("v_cndmask_b32 %[vt2], 0, %[c80], %[scy]", [], ["scy"]),
-              V("v_sub_co_u32 %[o0], %[sk0], %[h0], %[vt1]", ["sk0"]),
-              V("v_subb_co_u32 %[o1], %[sd1], %[h1], 0, %[sk0]", ["sd1"], ["sk0"]),        # d1 = m & t0 < 19
-              V("v_subb_co_u32 %[o2], %[sk1], %[h2], 0, %[sd1]", ["sk1"], ["sd1"]),
-              V("v_subb_co_u32 %[o3], %[sk1], %[h3], 0, %[sk1]", ["sk1"], ["sk1"]),
-              V("v_and_b32 %[vt1], %[o2], %[o3]"),
+              V("v_sub_co_u32 %[h0], %[sk0], %[h0], %[vt1]", ["sk0"]),
+              V("v_subb_co_u32 %[h1], %[sd1], %[h1], 0, %[sk0]", ["sd1"], ["sk0"]),        # d1 = m & t0 < 19
+              V("v_subb_co_u32 %[h2], %[sk1], %[h2], 0, %[sd1]", ["sk1"], ["sd1"]),
+              V("v_subb_co_u32 %[h3], %[sk1], %[h3], 0, %[sk1]", ["sk1"], ["sk1"]),
+              V("v_and_b32 %[vt1], %[h2], %[h3]"),
               V("v_cmp_eq_u32 %[sd2], -1, %[vt1]", ["sd2"]),
               S("s_and_b64 %[sd2], %[sd2], %[scy]", ["sd2"]),                              # d2 = m & o1 == M
-              V("v_subb_co_u32 %[o4], %[sk2], %[h4], 0, %[sd2]", ["sk2"], ["sd2"]),
-              V("v_subb_co_u32 %[o5], %[sk2], %[h5], 0, %[sk2]", ["sk2"], ["sk2"]),
-              V("v_and_b32 %[vt1], %[o4], %[o5]"),
+              V("v_subb_co_u32 %[h4], %[sk2], %[h4], 0, %[sd2]", ["sk2"], ["sd2"]),
+              V("v_subb_co_u32 %[h5], %[sk2], %[h5], 0, %[sk2]", ["sk2"], ["sk2"]),
+              V("v_and_b32 %[vt1], %[h4], %[h5]"),
               V("v_cmp_eq_u32 %[sd3], -1, %[vt1]", ["sd3"]),
               S("s_and_b64 %[sd3], %[sd3], %[scy]", ["sd3"]),                              # d3 = m & o2 == M
-              V("v_subb_co_u32 %[o6], %[sk3], %[h6], 0, %[sd3]", ["sk3"], ["sd3"]),
-              V("v_subb_co_u32 %[vt3], %[sk3], %[h7], 0, %[sk3]", ["sk3"], ["sk3"]),
-              V("v_add_u32 %[o7], %[vt3], %[vt2]")]                                         # + m 2^63
+              V("v_subb_co_u32 %[h6], %[sk3], %[h6], 0, %[sd3]", ["sk3"], ["sd3"]),
+              V("v_subb_co_u32 %[h7], %[sk3], %[h7], 0, %[sk3]", ["sk3"], ["sk3"]),
+              V("v_add_u32 %[h7], %[h7], %[vt2]")]                                         # + m 2^63
     # layout: test1, branch -> 5 (exact chain); plain chain, test2, branch -> 3 (exact "+ p");
     # fast "+ p", s_branch 4; 5: exact chain (falls through); 3: exact "+ p"; 4: end
     l1, s1 = schedule(test1 + [S("s_cmp_lg_u64 %[srare], 0"), S("s_cbranch_scc1 5f")])
@@ -286,15 +294,25 @@ def gen_sub():
     return emit("fe_sub_asm", ["fe25519_sub (curve25519_ops.cu:71-90) on limb halves: lossy borrow chain, then the",
                                "literal \"+ p\" pass on a final borrow (fast forms unless a lane is on a rare edge)."],
                 [("fa", "a"), ("ga", "b")], [f"a{i}" for i in range(8)] + [f"b{i}" for i in range(8)],
-                o, t + ["vt1", "vt2", "vt3"], ["sk0", "sk1", "sk2", "sk3", "sd1", "sd2", "sd3", "scy", "sq1", "sq2",
-                                               "sq3", "srare"], lines)
+                t, ["vt1", "vt2", "vt3"], ["sk0", "sk1", "sk2", "sk3", "sd1", "sd2", "sd3", "scy", "sq1", "sq2",
+                                           "sq3", "srare"], lines)
+
+
+def gen_canon():
+    """host fe25519_tobytes' conditional "- p" (curve25519_ops.cu:220-251) = device fe_mul_one:
+    the fix-up with no carry, in place."""
+    h = [f"h{i}" for i in range(8)]
+    lines = two_way(fix_test(h, "0"), fix_fast(h), fix_seq(h, h, "0"))
+    return emit("fe_canon_asm", ["Canonicalising \"- p\" of fe25519_tobytes (curve25519_ops.cu:220-251), in place:",
+                                 "h >= p ? lossy - p : h (fast form unless a lane is on a rare edge)."],
+                [("ha", "h")], [], h, ["vt1", "vt2", "vt3"], FIX_SGPRS + ["srare"], lines, inout=True)
 
 
 def main():
     out = ["// GENERATED by tools/gen_field_asm.py -- do not edit by hand.",
            "// gfx950 inline-asm fe25519 add and product fold: the same bits as the C forms in fe25519_dev.h.",
            "#pragma once", "#include <stdint.h>", "namespace bp {"]
-    out += gen_add() + [""] + gen_sub() + [""] + gen_fold()
+    out += gen_add() + [""] + gen_sub() + [""] + gen_fold() + [""] + gen_canon()
     out.append("}  // namespace bp")
     open(OUT, "w").write("\n".join(out) + "\n")
     print("wrote", OUT)

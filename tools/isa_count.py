@@ -1,4 +1,5 @@
-"""Compile tools/isa_ops.hip for gfx950 and print per-kernel VALU / s_nop counts.
+"""Compile tools/isa_ops.hip for gfx950 and print per-kernel VALU / s_nop counts (common path:
+the field asm's exact forms for rare edges are skipped).
 
   python tools/isa_count.py [extra hipcc flags]
 """
@@ -36,8 +37,20 @@ def main():
     for name in [l.split(":")[0] for l in s.split("\n") if l.startswith("p_") and l.split(":")[0].isidentifier()]:
         body = s[s.index("\n" + name + ":"):]
         body = body[:body.index("s_endpgm")]
-        ins = [l.split()[0] for l in body.split("\n")
-               if l.startswith("\t") and l.strip() and not l.startswith("\t.") and not l.startswith("\t;")]
+        # the field asm's exact forms for rare edges sit between "s_branch 4f" and the "4:" label:
+        # count the common path only (what a wave executes unless a lane is on a rare edge)
+        ins, skip = [], False
+        for l in body.split("\n"):
+            t = l.strip()
+            if skip:
+                skip = t != "4:"
+                continue
+            if t == "s_branch 4f":
+                skip = True
+                ins.append("s_branch")
+                continue
+            if l.startswith("\t") and t and not l.startswith("\t.") and not l.startswith("\t;"):
+                ins.append(t.split()[0])
         c = collections.Counter(ins)
         valu = sum(n for i, n in c.items() if i.startswith("v_"))
         top = ", ".join(f"{k}:{v}" for k, v in c.most_common(8))

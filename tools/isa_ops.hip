@@ -28,3 +28,4 @@ extern "C" __global__ void p_ge_add_sel_zone(ge* o, const ge* p, const geq* q, c
     qs[threadIdx.x] = q[threadIdx.x];
     o[threadIdx.x] = ge_add_sel<true, true>(p[threadIdx.x], &qs[threadIdx.x], u[threadIdx.x] != 0);
 }
+extern "C" __global__ void p_fe_canon(fe* o, const fe* a) { o[threadIdx.x] = fe_canon(a[threadIdx.x]); }
