@@ -308,14 +308,14 @@ def gen_canon():
                 [("ha", "h")], [], h, ["vt1", "vt2", "vt3"], FIX_SGPRS + ["srare"], lines, inout=True)
 
 
-def main():
+def main(path=OUT):
     out = ["// GENERATED by tools/gen_field_asm.py -- do not edit by hand.",
            "// gfx950 inline-asm fe25519 add and product fold: the same bits as the C forms in fe25519_dev.h.",
            "#pragma once", "#include <stdint.h>", "namespace bp {"]
     out += gen_add() + [""] + gen_sub() + [""] + gen_fold() + [""] + gen_canon()
     out.append("}  // namespace bp")
-    open(OUT, "w").write("\n".join(out) + "\n")
-    print("wrote", OUT)
+    open(path, "w").write("\n".join(out) + "\n")
+    print("wrote", path)
 
 
 if __name__ == "__main__":
