@@ -69,6 +69,8 @@ def parse():
                          "0 = off): one-time setup, same bits")
     ap.add_argument("--shard-total", type=int, default=1 << 16, help="configs[4]: proofs in the sharded batch")
     ap.add_argument("--no-shard", action="store_true")
+    ap.add_argument("--host-count", type=int, default=16384, help="proofs per host-struct API call")
+    ap.add_argument("--no-host", action="store_true")
     ap.add_argument("--rehearse", action="store_true",
                     help="exercise the N>1 path on one GPU (all ranks on cuda:0, gloo collectives); not a measurement")
     return ap.parse_args()
@@ -383,6 +385,45 @@ def shard_leg(args, dev, world, rank, pipes, gens, G, H, g, h):
             "data": "1024 x 4 distinct GPU-prover proofs (rank-independent seeds), tiled to 2^16"}
 
 
+def host_leg(args, batches, G, H, g, h):
+    """The host-struct entry point hipbp_batch_range_proof_verify_host: an array of the reference's
+    own RangeProof structs in host memory (cuda_range_proof_verify semantics per proof), so the
+    rate includes packing, one H2D, the pipeline and one D2H (PCIe-inclusive; never `value`)."""
+    import ctypes
+    import cudabulletproof_amd as bp
+    host = [{k: getattr(b, k).cpu().numpy().view(np.uint64) for k in bp.RangeProofBatch.FIELDS} for b in batches]
+    count = args.host_count
+    keep, proofs, V = [], [], []
+    for i in range(count):
+        a = host[(i // len(host[0]["V"])) % len(host)]
+        j = i % len(a["V"])
+        head = np.concatenate([a[k][j] for k in ("V", "A", "S", "T1", "T2")] +
+                              [np.zeros(8, np.uint64), a["t"][j], a["c"][j], a["x"][j]])
+        proofs.append(bp._range_proof_struct(dict(head=head, a=a["a"][j], b=a["b"][j], L=a["L"][j], R=a["R"][j]),
+                                             args.n, keep))
+        V.append(a["V"][j])
+    arr = (bp.RangeProofC * count)(*proofs)
+    V = np.ascontiguousarray(np.stack(V))
+    G, H, g, h = (np.ascontiguousarray(x.cpu().numpy().view(np.uint64)) for x in (G, H, g, h))
+    gv, hv = bp.PointVector(G.ctypes.data, len(G)), bp.PointVector(H.ctypes.data, len(H))
+    ok = np.zeros(count, np.uint8)
+    L = bp.lib()
+    call = lambda: bp._chk(L.hipbp_batch_range_proof_verify_host(
+        arr, ctypes.c_void_p(V.ctypes.data), ctypes.c_size_t(count), ctypes.c_size_t(args.n), ctypes.byref(gv),
+        ctypes.byref(hv), ctypes.c_void_p(g.ctypes.data), ctypes.c_void_p(h.ctypes.data), ctypes.c_int(1),
+        ctypes.c_void_p(ok.ctypes.data)))
+    call()
+    reps = 2
+    t1 = time.perf_counter()
+    for _ in range(reps):
+        call()
+    dt = (time.perf_counter() - t1) / reps
+    return {"metric": "64-bit range-proof verifies/sec, host RangeProof structs (PCIe-inclusive)",
+            "value": count / dt, "unit": "verifies/s", "proofs": count, "ms": dt * 1e3, "passes": int(ok.sum()),
+            "n_gpus": 1, "entry_point": "hipbp_batch_range_proof_verify_host",
+            "bytes_h2d": int(count * (5 * 128 + 3 * 32 + 2 * 32 + 2 * 128 * int(np.log2(args.n))))}
+
+
 def prove_leg(args, dev, gens=None):
     """§8(f) rank 1: generate_range_proof (rp.cu:1159) batched on the GPU, n = args.n, synthetic
     values and random scalars; proofs/s over whole batches (inputs resident in HBM)."""
@@ -588,6 +629,10 @@ def main():
         ipa = ipa_leg(args, dev)
         ipa["n_gpus"] = 1
 
+    host_api = None
+    if not args.no_host and rank == 0 and world == 1:
+        host_api = host_leg(args, batches, Gd, Hd, gd, hd)
+
     prove = None
     if not args.no_prove and rank == 0:
         prove = prove_leg(args, dev, gens)
@@ -611,7 +656,7 @@ def main():
                        "prefix_tables": prefix,
                        "proof_bytes": proof_bytes(n, 1), "passes_in_warmup_batch": passes_warm},
             "roofline": roofline, "valu_roofline": valu_roofline, "cpu_baseline": cpu, "msm": msm, "ipa": ipa, "prove": prove,
-            "sharded_2p16": sharded,
+            "sharded_2p16": sharded, "host_api": host_api,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -132,7 +132,8 @@ def lib():
         L.hipbp_last_error.restype = ctypes.c_char_p
         for f in ("cuda_range_proof_verify", "cuda_inner_product_verify"):
             getattr(L, f).restype = ctypes.c_bool
-        for f in ("hipbp_batch_range_proof_verify", "hipbp_batch_range_proof_verify_std",
+        for f in ("hipbp_batch_range_proof_verify", "hipbp_batch_range_proof_verify_host",
+                  "hipbp_batch_range_proof_verify_std",
                   "hipbp_batch_inner_product_verify", "hipbp_batch_generate_range_proof", "hipbp_msm",
                   "hipbp_msm_pippenger", "hipbp_msm_batch",
                   "hipbp_point_tree",
@@ -275,6 +276,26 @@ def cuda_range_proof_verify(proof, V, n, G, H, g, h):
     gv, hv = PointVector(_p(G).value, len(G)), PointVector(_p(H).value, len(H))
     return bool(lib().cuda_range_proof_verify(ctypes.byref(rp), _p(V), _sz(n), ctypes.byref(gv), ctypes.byref(hv),
                                               _p(g), _p(h)))
+
+
+def batch_range_proof_verify_host(proofs, V, n, G, H, g, h, num_gpus=0):
+    """hipbp_batch_range_proof_verify_host: cuda_range_proof_verify over a list of proofs (the
+    dicts cuda_range_proof_verify takes) packed as an array of the reference's RangeProof structs,
+    sharded over num_gpus devices (0: all).  Host arrays in, (count,) bool verdicts out."""
+    require_gpu()
+    keep = []
+    count = len(proofs)
+    arr = (RangeProofC * max(count, 1))()
+    for i, pr in enumerate(proofs):
+        arr[i] = _range_proof_struct(pr, n, keep)
+    V = _u64(V, 16).reshape(-1, 16)
+    g, h = _u64(g, 16), _u64(h, 16)
+    G, H = _u64(G, 16), _u64(H, 16)
+    gv, hv = PointVector(_p(G).value, len(G)), PointVector(_p(H).value, len(H))
+    ok = np.zeros(max(count, 1), np.uint8)
+    _chk(lib().hipbp_batch_range_proof_verify_host(arr, _p(V), _sz(count), _sz(n), ctypes.byref(gv), ctypes.byref(hv),
+                                                   _p(g), _p(h), ctypes.c_int(num_gpus), _p(ok)))
+    return ok[:count].astype(bool)
 
 
 def cuda_inner_product_verify(proof, P, G, H, Q):

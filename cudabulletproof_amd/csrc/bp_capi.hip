@@ -14,7 +14,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <chrono>
+#include <thread>
 
 #include "../../include/cudabulletproof_hip.h"
 #include "bp_kernels.h"
@@ -128,6 +130,12 @@ struct Engine {
     int two_cap = 0;
     // single-call staging (Part 1: the engine's own stream, synchronous calls)
     Buf h2d[8], scratch[8];
+    // hipbp_batch_range_proof_verify_host: a second stream (chunks alternate over two pipelines)
+    // and grow-only staging (pinned host + device), reused across calls
+    hipStream_t stream2 = nullptr;
+    Buf host_dev;
+    uint8_t* host_pinned = nullptr;
+    size_t host_pinned_cap = 0;
     // MSM / point-tree workspaces, one set per stream: the Part-2 calls run asynchronously on
     // the caller's stream, so two MSMs on two streams (or an async MSM and a Part-1 call on the
     // engine stream) must never share buffers.  [0] per-point terms, [1..2] block roots,
@@ -563,6 +571,27 @@ hipError_t msm_run(Engine& e, bp::ge* results, const bp::fe* scalars, const bp::
     return hipGetLastError();
 }
 
+// The engine's cached one-shot pipeline for (stream, n, mode); created on first use.  Cached only
+// once fully initialised (a failed init is released, never reused).
+int pipeline_for(Engine& e, hipStream_t s, size_t max_batch, int n, int range_mode, Pipeline** out) {
+    auto key = std::make_tuple(s, n, range_mode);
+    auto it = e.pipes.find(key);
+    if (it != e.pipes.end()) {
+        *out = it->second;
+        return HIPBP_OK;
+    }
+    Pipeline* pl = new Pipeline();
+    hipError_t ierr = pl->init(&e, s, max_batch, n, range_mode);
+    if (ierr != hipSuccess) {
+        pl->release();
+        delete pl;
+        BP_RET_ON(ierr);
+    }
+    e.pipes[key] = pl;
+    *out = pl;
+    return HIPBP_OK;
+}
+
 // One-shot verify of a whole batch on `s` (push + drain of a cached pipeline).
 int run_verify(Engine& e, const hipbp_proof_batch* batch, const ge25519* P_in, const ge25519* G, const ge25519* H,
                const ge25519* h, uint8_t* ok, ge25519* P_out, ge25519* chk_out, int range_mode, hipStream_t s,
@@ -570,21 +599,8 @@ int run_verify(Engine& e, const hipbp_proof_batch* batch, const ge25519* P_in, c
     int rc = check_batch(batch, range_mode);
     if (rc != HIPBP_OK || batch->count == 0) return rc;
     if (range_mode) BP_RET_ON(e.ensure_two((int)batch->n));
-    auto key = std::make_tuple(s, (int)batch->n, range_mode);
     Pipeline* pl = nullptr;
-    auto it = e.pipes.find(key);
-    if (it != e.pipes.end()) {
-        pl = it->second;
-    } else {   // cached only once fully initialised (a failed init is released, never reused)
-        pl = new Pipeline();
-        hipError_t ierr = pl->init(&e, s, batch->count, (int)batch->n, range_mode);
-        if (ierr != hipSuccess) {
-            pl->release();
-            delete pl;
-            BP_RET_ON(ierr);
-        }
-        e.pipes[key] = pl;
-    }
+    if ((rc = pipeline_for(e, s, batch->count, (int)batch->n, range_mode, &pl)) != HIPBP_OK) return rc;
     pl->G = (const bp::ge*)G;
     pl->H = (const bp::ge*)H;
     pl->h = (const bp::ge*)h;
@@ -1198,6 +1214,212 @@ bool cuda_inner_product_verify(const InnerProductProof* proof, const ge25519* P,
         return false;
     }
     return verify_single(proof, nullptr, nullptr, P, proof->n, G, H, Q);
+}
+
+// ---- batch form of cuda_range_proof_verify over the reference's host RangeProof structs
+}  // extern "C"
+
+namespace {
+
+// one device's shard of hipbp_batch_range_proof_verify_host (its own host thread).  The shard is cut
+// into chunks of CHUNK proofs, each staged as its own little flat batch; each chunk is packed,
+// copied and pushed as soon as it is packed (the GPU starts while the host packs the rest), and
+// the chunks alternate over two pipelines on two streams, whose ticks fill each other's tails.
+int host_shard(int dev, const RangeProof* proofs, const ge25519* V, const size_t* idx, size_t B, size_t abl,
+               size_t Lr, size_t n, const PointVector* G, const PointVector* H, const ge25519* h, uint8_t* ok) {
+    BP_RET_ON(hipSetDevice(dev));
+    hipError_t err;
+    Engine* e = engine_or_null(&err);
+    BP_RET_ON(err);
+    constexpr size_t CHUNK = 1024;
+    const size_t GE = sizeof(ge25519), FE = sizeof(fe25519);
+    // per chunk of c proofs: V A S T1 T2 [c] | t c x [c] | a b [c abl] | L R [c Lr]
+    auto chunk_bytes = [&](size_t c) { return c * (5 * GE + 3 * FE + 2 * abl * FE + 2 * Lr * GE); };
+    const size_t nch = (B + CHUNK - 1) / CHUNK;
+    const size_t gen_off = chunk_bytes(CHUNK) * (nch - 1) + chunk_bytes(B - CHUNK * (nch - 1));
+    const size_t ok_off = gen_off + (2 * n + 1) * GE, bytes = ok_off + B;
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (!e->stream2) BP_RET_ON(hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking));
+    hipStream_t st[2] = {e->stream, e->stream2};
+    if (bytes > e->host_pinned_cap) {
+        if (e->host_pinned) {
+            BP_RET_ON(hipStreamSynchronize(st[0]));
+            BP_RET_ON(hipStreamSynchronize(st[1]));
+            BP_RET_ON(hipHostFree(e->host_pinned));
+            e->host_pinned = nullptr;
+            e->host_pinned_cap = 0;
+        }
+        BP_RET_ON(hipHostMalloc((void**)&e->host_pinned, bytes));
+        e->host_pinned_cap = bytes;
+    }
+    if (bytes > e->host_dev.cap) {   // Buf::need frees the old buffer: nothing may still read it
+        BP_RET_ON(hipStreamSynchronize(st[0]));
+        BP_RET_ON(hipStreamSynchronize(st[1]));
+    }
+    BP_RET_ON(e->host_dev.need(bytes));
+    uint8_t* host = e->host_pinned;
+    uint8_t* dbuf = e->host_dev.as<uint8_t>();
+    memcpy(host + gen_off, G->elements, n * GE);
+    memcpy(host + gen_off + n * GE, H->elements, n * GE);
+    memcpy(host + gen_off + 2 * n * GE, h, GE);
+    BP_RET_ON(hipMemcpyAsync(dbuf + gen_off, host + gen_off, (2 * n + 1) * GE, hipMemcpyHostToDevice, st[0]));
+    BP_RET_ON(e->ensure_two((int)n));   // engine stream: ordered before the pipeline's first tick
+    const ge25519* dgen = (const ge25519*)(dbuf + gen_off);
+    Pipeline* pl[2] = {nullptr, nullptr};
+    int rc = HIPBP_OK;
+    for (int k = 0; k < 2 && rc == HIPBP_OK; k++) {
+        rc = pipeline_for(*e, st[k], std::min(B, CHUNK), (int)n, 1, &pl[k]);
+        if (rc == HIPBP_OK) {
+            pl[k]->G = (const bp::ge*)dgen;
+            pl[k]->H = (const bp::ge*)(dgen + n);
+            pl[k]->h = (const bp::ge*)(dgen + 2 * n);
+            pl[k]->g = nullptr;
+        }
+    }
+    hipEvent_t gens_ready = nullptr;
+    if (rc == HIPBP_OK) {   // the second stream waits for the generators' copy
+        BP_RET_ON(hipEventCreateWithFlags(&gens_ready, hipEventDisableTiming));
+        BP_RET_ON(hipEventRecord(gens_ready, st[0]));
+        BP_RET_ON(hipStreamWaitEvent(st[1], gens_ready, 0));
+    }
+    uint8_t* dok = dbuf + ok_off;
+    size_t off = 0;
+    for (size_t ch = 0; ch < nch && rc == HIPBP_OK; ch++) {
+        const size_t c0 = ch * CHUNK, c = std::min(CHUNK, B - c0), cb = chunk_bytes(c);
+        uint8_t* hc = host + off;
+        ge25519* hg = (ge25519*)hc;
+        fe25519* hf = (fe25519*)(hc + 5 * c * GE);
+        fe25519* hab = hf + 3 * c;
+        ge25519* hlr = (ge25519*)(hab + 2 * c * abl);
+        for (size_t k = 0; k < c; k++) {
+            const RangeProof& p = proofs[idx[c0 + k]];
+            const InnerProductProof& ip = p.ip_proof;
+            hg[k] = V[idx[c0 + k]];
+            hg[c + k] = p.A;
+            hg[2 * c + k] = p.S;
+            hg[3 * c + k] = p.T1;
+            hg[4 * c + k] = p.T2;
+            hf[k] = p.t;
+            hf[c + k] = ip.c;
+            hf[2 * c + k] = ip.x;
+            memcpy(hab + k * abl, ip.a.elements, abl * FE);
+            memcpy(hab + (c + k) * abl, ip.b.elements, abl * FE);
+            if (Lr) {
+                memcpy(hlr + k * Lr, ip.L.elements, Lr * GE);
+                memcpy(hlr + (c + k) * Lr, ip.R.elements, Lr * GE);
+            }
+        }
+        hipStream_t s = st[ch & 1];
+        if ((err = hipMemcpyAsync(dbuf + off, hc, cb, hipMemcpyHostToDevice, s)) != hipSuccess) {
+            g_err = std::string("chunk H2D: ") + hipGetErrorString(err);
+            rc = HIPBP_ERR_DEVICE;
+            break;
+        }
+        const uint8_t* dc = dbuf + off;
+        const ge25519* dg = (const ge25519*)dc;
+        const fe25519* df = (const fe25519*)(dc + 5 * c * GE);
+        hipbp_proof_batch b;
+        memset(&b, 0, sizeof b);
+        b.count = c;
+        b.n = n;
+        b.ab_len = abl;
+        b.L_len = Lr;
+        b.V = dg; b.A = dg + c; b.S = dg + 2 * c; b.T1 = dg + 3 * c; b.T2 = dg + 4 * c;
+        b.t = df; b.c = df + c; b.x = df + 2 * c;
+        b.a = df + 3 * c; b.b = df + 3 * c + c * abl;
+        const ge25519* dlr = (const ge25519*)(df + 3 * c + 2 * c * abl);
+        b.L = Lr ? dlr : nullptr;
+        b.R = Lr ? dlr + c * Lr : nullptr;
+        rc = pl[ch & 1]->push(&b, nullptr, dok + c0, nullptr, nullptr);
+        off += cb;
+    }
+    for (int k = 0; k < 2 && rc == HIPBP_OK; k++) rc = pl[k]->flush();
+    hipError_t s1 = hipStreamSynchronize(st[1]);
+    if (rc == HIPBP_OK && s1 == hipSuccess) {
+        if ((err = hipMemcpyAsync(host + ok_off, dok, B, hipMemcpyDeviceToHost, st[0])) == hipSuccess)
+            err = hipStreamSynchronize(st[0]);
+        if (err != hipSuccess) { g_err = std::string("shard D2H: ") + hipGetErrorString(err); rc = HIPBP_ERR_DEVICE; }
+    } else {
+        (void)hipStreamSynchronize(st[0]);   // nothing in flight reads the staging any more
+        if (rc == HIPBP_OK) { g_err = std::string("stream2: ") + hipGetErrorString(s1); rc = HIPBP_ERR_DEVICE; }
+    }
+    if (gens_ready) (void)hipEventDestroy(gens_ready);
+    if (rc == HIPBP_OK)
+        for (size_t k = 0; k < B; k++) ok[idx[k]] = host[ok_off + k] ? 1 : 0;
+    return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hipbp_batch_range_proof_verify_host(const RangeProof* proofs, const ge25519* V, size_t count, size_t n,
+                                        const PointVector* G, const PointVector* H, const ge25519* g,
+                                        const ge25519* h, int num_gpus, uint8_t* ok) {
+    (void)g;   // g is not read by cuda_range_proof_verify (crv:82-127)
+    if (count == 0) return HIPBP_OK;
+    if (!proofs || !V || !G || !H || !h || !ok || !G->elements || !H->elements) {
+        g_err = "null argument";
+        return HIPBP_ERR_ARG;
+    }
+    int ndev = 0;
+    BP_RET_ON(hipGetDeviceCount(&ndev));
+    if (ndev <= 0) { g_err = "no HIP device"; return HIPBP_ERR_DEVICE; }
+    const int ng = num_gpus <= 0 ? ndev : std::min(num_gpus, ndev);
+    // The flat batch needs one (a/b length, rounds) shape: the first proof that passes the checks
+    // sets it (the reference prover's proofs all share it); proofs of another shape go one by one.
+    size_t abl = 0, Lr = 0;
+    std::vector<size_t> main, other;
+    main.reserve(count);
+    for (size_t i = 0; i < count; i++) {
+        const InnerProductProof& ip = proofs[i].ip_proof;
+        ok[i] = 0;
+        if (G->length != ip.n || H->length != ip.n || n != ip.n) {   // crv:140-143, as the single call
+            fprintf(stderr, "Error: Vector lengths must match for inner product verification\n");
+            continue;
+        }
+        if (ip.b.length != ip.a.length || ip.a.length == 0 || ip.L.length < ip.L_len || ip.R.length < ip.L_len ||
+            !ip.a.elements || !ip.b.elements || (ip.L_len && (!ip.L.elements || !ip.R.elements)))
+            continue;   // stage_single's check: the single call returns false as well
+        if (main.empty()) { abl = ip.a.length; Lr = ip.L_len; }
+        (ip.a.length == abl && ip.L_len == Lr ? main : other).push_back(i);
+    }
+    if (!main.empty()) {   // the shape checks of the device batch (n a power of two, L_len <= log2 n)
+        hipbp_proof_batch probe;
+        memset(&probe, 0, sizeof probe);
+        probe.count = 1; probe.n = n; probe.ab_len = abl; probe.L_len = Lr;
+        const uint8_t dummy[1] = {0};
+        probe.V = probe.A = probe.S = probe.T1 = probe.T2 = (const ge25519*)dummy;
+        probe.t = probe.a = probe.b = probe.c = probe.x = (const fe25519*)dummy;
+        probe.L = probe.R = (const ge25519*)dummy;
+        int rc = check_batch(&probe, 1);
+        if (rc != HIPBP_OK) return rc;
+    }
+    int dev0 = 0;
+    BP_RET_ON(hipGetDevice(&dev0));
+    const size_t M = main.size();
+    std::vector<int> rcs(ng, HIPBP_OK);
+    std::vector<std::string> errs(ng);
+    std::vector<std::thread> workers;
+    for (int d = 0; d < ng; d++) {
+        const size_t lo = M * d / ng, hi = M * (d + 1) / ng;
+        if (hi == lo) continue;
+        workers.emplace_back([&, d, lo, hi]() {
+            rcs[d] = host_shard(d, proofs, V, main.data() + lo, hi - lo, abl, Lr, n, G, H, h, ok);
+            if (rcs[d] != HIPBP_OK) errs[d] = g_err;   // g_err is per thread
+        });
+    }
+    for (auto& w : workers) w.join();
+    for (int d = 0; d < ng; d++)
+        if (rcs[d] != HIPBP_OK) {
+            g_err = "device " + std::to_string(d) + ": " + errs[d];
+            (void)hipSetDevice(dev0);
+            return rcs[d];
+        }
+    BP_RET_ON(hipSetDevice(dev0));
+    for (size_t i : other)
+        ok[i] = verify_single(&proofs[i].ip_proof, &proofs[i], &V[i], nullptr, n, G, H, h) ? 1 : 0;
+    return HIPBP_OK;
 }
 
 // ---- cuda_benchmark_* (declared at cuda_bulletproof.h:81-84, never defined by the reference)

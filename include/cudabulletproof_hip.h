@@ -129,6 +129,20 @@ const char* hipbp_last_error(void);
 /* Number of HIP devices visible. */
 int hipbp_device_count(void);
 
+/* cuda_range_proof_verify (cuda_bulletproof.h:61, crv:82) over an ARRAY of the reference's own host
+ * structs: ok[i] = cuda_range_proof_verify(&proofs[i], &V[i], n, G, H, g, h) for i < count, bit for
+ * bit, with the reference's length check per proof (message on stderr, ok[i] = 0).  The proofs are
+ * packed into the flat batch format, sharded in contiguous blocks over num_gpus devices (<= 0: all
+ * visible), one host thread per device: 1024-proof chunks are packed into pinned staging, copied
+ * and pushed as they are packed, alternating over two verify pipelines on two streams; one D2H of
+ * the verdicts; no data-path exchange between devices.  Proofs whose a/b length or round
+ * count differs from the first valid proof's go through the single-proof path.  Host pointers,
+ * synchronous.  Returns HIPBP_OK or an error code (hipbp_last_error); on an error ok is
+ * undefined.  No reference counterpart (the additive batch entry point). */
+int hipbp_batch_range_proof_verify_host(const RangeProof* proofs, const ge25519* V, size_t count, size_t n,
+                                        const PointVector* G, const PointVector* H, const ge25519* g,
+                                        const ge25519* h, int num_gpus, uint8_t* ok);
+
 /* Batched cuda_range_proof_verify semantics. G/H: n generators, g/h: 1 point (device).
  * ok[count] gets 1/0; P_out / check_out (nullable) get the IPA point P and the check point. */
 int hipbp_batch_range_proof_verify(const hipbp_proof_batch* batch, const ge25519* G, const ge25519* H,

@@ -155,6 +155,51 @@ def test_batch_verify_matches_reference(bp, golden, n):
     assert np.array_equal(chk, d["check"])
 
 
+def _synth_proof_dicts(s, n):
+    out = []
+    for i in range(len(s["V"])):
+        head = np.concatenate([s[k][i] for k in ("V", "A", "S", "T1", "T2")] +
+                              [np.zeros(8, np.uint64), s["t"][i], s["c"][i], s["x"][i]])
+        out.append(dict(head=head, a=s["a"][i], b=s["b"][i], L=s["L"][i], R=s["R"][i]))
+    return out
+
+
+@pytest.mark.parametrize("n", [16, 64])
+def test_batch_verify_host_structs(bp, golden, n):
+    """hipbp_batch_range_proof_verify_host over arrays of the reference's RangeProof structs: the
+    reference proofs give the reference's verdicts; 2500 synthetic proofs (two 2048-proof pipeline
+    ticks) give the device batch API's verdicts; a proof whose ip.n != n fails the reference's
+    length check; one with a different a/b length takes the single-proof path and agrees with it."""
+    import torch
+    from cudabulletproof_amd import synth
+    d = golden(f"proofs_n{n}")
+    ref = [_proof(d, i) for i in range(len(d["head"]))]
+    s = synth.proofs(2500, n, seed=500 + n)
+    syn = _synth_proof_dicts(s, n)
+    dev = torch.device("cuda:0")
+    batch = bp.RangeProofBatch.from_numpy(n, s, dev)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    okd = torch.zeros(2500, dtype=torch.uint8, device=dev)
+    bp.batch_range_proof_verify(batch, T(d["G"]), T(d["H"]), T(d["g"]), T(d["h"]), okd)
+    torch.cuda.synchronize()
+    want_syn = okd.cpu().numpy().astype(bool)
+    # a different a/b length (3): the single-proof path
+    odd = dict(syn[7])
+    rng = np.random.default_rng(n)
+    odd["a"] = rand_fe(rng, 3)
+    odd["b"] = rand_fe(rng, 3)
+    want_odd = bp.cuda_range_proof_verify(odd, s["V"][7], n, d["G"], d["H"], d["g"], d["h"])
+    proofs = ref + syn[:1200] + [odd] + syn[1200:]
+    V = np.concatenate([d["V"], s["V"][:1200], s["V"][7:8], s["V"][1200:]])
+    want = np.concatenate([d["ok_cuda"].astype(bool), want_syn[:1200], [want_odd], want_syn[1200:]])
+    for ng in (1, 0):
+        got = bp.batch_range_proof_verify_host(proofs, V, n, d["G"], d["H"], d["g"], d["h"], num_gpus=ng)
+        assert np.array_equal(got, want), (ng, np.nonzero(got != want)[0][:10])
+    # the reference's length check (crv:140-143): generator vectors shorter than the proofs' n
+    got = bp.batch_range_proof_verify_host(ref[:2], d["V"][:2], n, d["G"][:n // 2], d["H"][:n // 2], d["g"], d["h"])
+    assert not got.any()
+
+
 @pytest.mark.parametrize("n,B,ab_len", [(64, 48, 1), (16, 40, 3), (4, 17, 2), (1, 9, 1), (256, 4, 1), (512, 3, 1),
                                         (1024, 2, 2),
                                         # B >= 64: lanes in chain-length order (the pipeline's lane sort)
