@@ -69,7 +69,7 @@ def parse():
                          "0 = off): one-time setup, same bits")
     ap.add_argument("--shard-total", type=int, default=1 << 16, help="configs[4]: proofs in the sharded batch")
     ap.add_argument("--no-shard", action="store_true")
-    ap.add_argument("--host-count", type=int, default=16384, help="proofs per host-struct API call")
+    ap.add_argument("--host-count", type=int, default=32768, help="proofs per host-struct API call")
     ap.add_argument("--no-host", action="store_true")
     ap.add_argument("--rehearse", action="store_true",
                     help="exercise the N>1 path on one GPU (all ranks on cuda:0, gloo collectives); not a measurement")
