@@ -10,7 +10,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SMALL = ["--steps", "2", "--warmup", "1", "--batch", "128", "--msm-log2", "12", "--prefix-bits", "12",
-         "--shard-total", "3000", "--no-cpu", "--no-ipa", "--no-prove", "--no-host"]
+         "--shard-total", "3000", "--no-host", "--no-cpu", "--no-ipa", "--no-prove"]
 
 
 # rank 0's single-GPU legs (IPA, prover) while the other rank waits at the closing barrier
