@@ -43,6 +43,7 @@ def build(force=False, verbose=False):
             return LIB_PATH
     import tempfile
     flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result"]
+    flags += os.environ.get("HIPBP_EXTRA_CFLAGS", "").split()   # A/B builds (e.g. -DBP_TERMS_OCC=3)
     with tempfile.TemporaryDirectory() as tmp:   # one hipcc per source, in parallel, then link
         objs = [os.path.join(tmp, os.path.basename(s) + ".o") for s in srcs]
         procs = []
