@@ -109,7 +109,7 @@ EXPORTS = [
     "cuda_benchmark_multi_scalar_mul", "cuda_benchmark_inner_product", "cuda_benchmark_field_operations",
     "cuda_benchmark_range_proof", "hipbp_last_error", "hipbp_device_count", "hipbp_batch_range_proof_verify",
     "hipbp_batch_range_proof_verify_std", "hipbp_batch_inner_product_verify", "hipbp_batch_generate_range_proof", "hipbp_msm",
-    "hipbp_msm_pippenger", "hipbp_msm_batch",
+    "hipbp_msm_pippenger", "hipbp_msm_pippenger_batch", "hipbp_msm_batch",
     "hipbp_point_tree", "hipbp_field_op", "hipbp_sync", "hipbp_timing_enable",
     "hipbp_timing_collect", "hipbp_kernel_count", "hipbp_kernel_name", "hipbp_pipeline_create",
     "hipbp_pipeline_push", "hipbp_pipeline_flush", "hipbp_pipeline_depth", "hipbp_pipeline_destroy",
@@ -136,7 +136,7 @@ def lib():
         for f in ("hipbp_batch_range_proof_verify", "hipbp_batch_range_proof_verify_host",
                   "hipbp_batch_range_proof_verify_std",
                   "hipbp_batch_inner_product_verify", "hipbp_batch_generate_range_proof", "hipbp_msm",
-                  "hipbp_msm_pippenger", "hipbp_msm_batch",
+                  "hipbp_msm_pippenger", "hipbp_msm_pippenger_batch", "hipbp_msm_batch",
                   "hipbp_point_tree",
                   "hipbp_field_op", "hipbp_sync", "hipbp_device_count"):
             getattr(L, f).restype = ctypes.c_int
@@ -479,6 +479,16 @@ def msm_pippenger(result, scalars, points, window_bits=12, stream=None):
     see include/cudabulletproof_hip.h)."""
     _chk(lib().hipbp_msm_pippenger(_c(result.data_ptr()), _c(scalars.data_ptr()), _c(points.data_ptr()),
                                    _sz(points.shape[0]), ctypes.c_int(window_bits), _stream_ptr(stream)))
+
+
+def msm_pippenger_batch(results, scalars, points, window_bits=12, stream=None):
+    """count Pippenger MSMs over the same points: results (count,16), scalars (count*n,4) or
+    (count,n,4), points (n,16), device tensors."""
+    count, n = results.shape[0], points.shape[0]
+    if scalars.numel() != count * n * 4:
+        raise BulletproofError("msm_pippenger_batch: scalars must hold count * n rows")
+    _chk(lib().hipbp_msm_pippenger_batch(_c(results.data_ptr()), _c(scalars.data_ptr()), _c(points.data_ptr()),
+                                         _sz(n), _sz(count), ctypes.c_int(window_bits), _stream_ptr(stream)))
 
 
 def point_tree(result, points, stream=None):

@@ -809,19 +809,27 @@ int hipbp_msm_batch(ge25519* results, const fe25519* scalars, const ge25519* poi
     return HIPBP_OK;
 }
 
-int hipbp_msm_pippenger(ge25519* result, const fe25519* scalars, const ge25519* points, size_t n, int window_bits,
-                        void* stream) {
+int hipbp_msm_pippenger_batch(ge25519* results, const fe25519* scalars, const ge25519* points, size_t n,
+                              size_t count, int window_bits, void* stream) {
     hipError_t err;
     Engine* e = engine_or_null(&err);
     BP_RET_ON(err);
-    if (n == 0) return HIPBP_OK;
-    if (!result || !scalars || !points) { g_err = "null argument"; return HIPBP_ERR_ARG; }
+    if (n == 0 || count == 0) return HIPBP_OK;
+    if (!results || !scalars || !points) { g_err = "null argument"; return HIPBP_ERR_ARG; }
     if (window_bits < 4 || window_bits > 12) { g_err = "pippenger: window_bits must be 4..12"; return HIPBP_ERR_ARG; }
-    if (n * ((256 + window_bits - 1) / window_bits) > 0x7FFFFFFFull) { g_err = "pippenger: n too large"; return HIPBP_ERR_ARG; }
+    if (count > 0xFFFFu || n * count * ((256 + window_bits - 1) / window_bits) > 0x7FFFFFFFull) {
+        g_err = "pippenger: n * count too large";
+        return HIPBP_ERR_ARG;
+    }
     std::lock_guard<std::mutex> lk(e->mu);
-    BP_RET_ON(bp::msm_pippenger((bp::ge*)result, (const bp::fe*)scalars, (const bp::ge*)points, n, window_bits, e->dtab,
-                                pick(stream, *e)));
+    BP_RET_ON(bp::msm_pippenger((bp::ge*)results, (const bp::fe*)scalars, (const bp::ge*)points, n, count, window_bits,
+                                e->dtab, pick(stream, *e)));
     return HIPBP_OK;
+}
+
+int hipbp_msm_pippenger(ge25519* result, const fe25519* scalars, const ge25519* points, size_t n, int window_bits,
+                        void* stream) {
+    return hipbp_msm_pippenger_batch(result, scalars, points, n, 1, window_bits, stream);
 }
 
 static int prove_run(const hipbp_prove_input* in, const ge25519* G, const ge25519* H, const ge25519* g,

@@ -183,7 +183,9 @@ void launch_msm_points(ge* pts, const fe* scal, const ge* P, size_t m, uint32_t*
 void launch_tree(ge* out, const ge* in, int S, size_t m, hipStream_t s);
 void launch_ops_scan(unsigned* bins, int longest_first, hipStream_t s);   // bins -> start offsets
 // Pippenger bucket MSM (bp_pippenger.hip; hipbp_msm_pippenger), 4 <= c <= 12
-hipError_t msm_pippenger(ge* result, const fe* scal, const ge* P, size_t n, int c, const ge* dtab, hipStream_t s);
+// count MSMs over the same n points: results[m] = MSM(scal[m n .. m n + n), P)
+hipError_t msm_pippenger(ge* result, const fe* scal, const ge* P, size_t n, size_t count, int c, const ge* dtab,
+                         hipStream_t s);
 
 
 

@@ -37,23 +37,23 @@ namespace {
 constexpr int PTPB = 256;
 constexpr int PM = 16;   // buckets per chunk
 
-// Sort input: element g = lw n + i (window lw = w - w0, point i), generated window-major; its
-// key is the c-bit digit alone (16 bits) and its value is g itself (a counting iterator, never
-// stored), so after a STABLE sort on the digit each bucket (lw, d) is contiguous and in index
-// order, and the bucket of a sorted element is ((g / n) << c) | digit.
-__global__ __launch_bounds__(PTPB) void k_pip_keys(const fe* __restrict__ s, size_t n, int c, int w0, int W,
-                                                  uint16_t* keys) {
+// Sort input: element g = v n + i (virtual window v = m Wp + lw: MSM m of the batch, window
+// lw = w - w0 of the part, point i), generated window-major; its key is the c-bit digit alone (16
+// bits) and its value is g itself (a counting iterator, never stored), so after a STABLE sort on
+// the digit each bucket (v, d) is contiguous and in index order, and the bucket of a sorted element
+// is ((g / n) << c) | digit.  MSM m's scalars are s[m n .. m n + n); all share the points.
+__global__ __launch_bounds__(PTPB) void k_pip_keys(const fe* __restrict__ s, size_t n, int c, int w0, int Wp,
+                                                  size_t Wv, uint16_t* keys) {
     const size_t g = (size_t)blockIdx.x * PTPB + threadIdx.x;
-    if (g >= (size_t)W * n) return;
-    const int w = (int)(g / n);
-    const size_t i = g % n;
-    const int lo = c * (w0 + w);
+    if (g >= Wv * n) return;
+    const size_t v = g / n, i = g % n, m = v / (size_t)Wp;
+    const int lo = c * (w0 + (int)(v % (size_t)Wp));
     // bits [lo, lo + c) of the 256-bit scalar (a window may straddle two limbs or end past bit 255)
-    const uint64_t* sc = s[i].v;   // only the limb(s) the window touches
+    const uint64_t* sc = s[m * n + i].v;   // only the limb(s) the window touches
     const int li = lo >> 6, sh = lo & 63;
-    uint64_t v = sc[li] >> sh;
-    if (sh && li < 3) v |= sc[li + 1] << (64 - sh);
-    keys[g] = (uint16_t)(v & ((1ull << c) - 1));
+    uint64_t x = sc[li] >> sh;
+    if (sh && li < 3) x |= sc[li + 1] << (64 - sh);
+    keys[g] = (uint16_t)(x & ((1ull << c) - 1));
 }
 
 __device__ __forceinline__ uint32_t pip_bucket(const uint16_t* __restrict__ keys, const uint32_t* __restrict__ vals,
@@ -224,8 +224,9 @@ __device__ __forceinline__ ge bucket_sum(const ge* __restrict__ Q, const uint32_
     return cnt[b] ? Q[off[b]] : ge_zero();
 }
 
-// one block per window: pairwise tree over its NC <= PTPB chunk values, in LDS
-__global__ __launch_bounds__(PTPB) void k_pip_window(const ge* __restrict__ V, int NC, ge* Sw) {
+// one block per (virtual) window v = m Wp + lw: pairwise tree over its NC <= PTPB chunk values, in
+// LDS, into Sw[m W + w0 + lw] (MSM m's window sums, absolute window index)
+__global__ __launch_bounds__(PTPB) void k_pip_window(const ge* __restrict__ V, int NC, int Wp, int W, int w0, ge* Sw) {
     __shared__ ge sh[PTPB];
     const int t = threadIdx.x;
     if (t < NC) sh[t] = V[(size_t)blockIdx.x * NC + t];
@@ -234,7 +235,7 @@ __global__ __launch_bounds__(PTPB) void k_pip_window(const ge* __restrict__ V, i
         if ((t % (2 * st)) == 0 && t + st < NC) sh[t] = ge_add(sh[t], sh[t + st]);
         __syncthreads();
     }
-    if (t == 0) Sw[blockIdx.x] = sh[0];
+    if (t == 0) Sw[(size_t)(blockIdx.x / Wp) * W + w0 + blockIdx.x % Wp] = sh[0];
 }
 
 // ---- latency-bound chains: one point operation per lane QUAD.  ge25519_add / the doubling are
@@ -285,14 +286,17 @@ __device__ __forceinline__ ge ge_op_quad(const ge& p, const ge& q) {
 }
 
 // Horner over windows w_top .. w_end (descending): T = Tin ? *Tin : S_{w_top} (then from
-// w_top - 1); per window c doublings, then + S_w.  One quad (the block's wave runs 16 identical
-// quads; lane 0 stores).  Split at any window, two calls give the single chain's bits.
-__global__ __launch_bounds__(64) void k_pip_horner(const ge* __restrict__ Sw, int w_top, int w_end, int c,
+// w_top - 1); per window c doublings, then + S_w.  One quad per MSM (a block per MSM of the
+// batch; its wave runs 16 identical quads; lane 0 stores).  Split at any window, two calls give
+// the single chain's bits.
+__global__ __launch_bounds__(64) void k_pip_horner(const ge* __restrict__ Sw, int W, int w_top, int w_end, int c,
                                                   const ge* __restrict__ Tin, ge* out) {
+    Sw += (size_t)blockIdx.x * W;   // block m: MSM m of the batch
+    out += blockIdx.x;
     ge T;
     int w = w_top;
     if (Tin) {
-        T = *Tin;
+        T = Tin[blockIdx.x];
     } else {
         T = Sw[w_top];
         w--;
@@ -408,10 +412,11 @@ static hipError_t pip_sort(void* temp, size_t& tb, const uint16_t* kin, uint16_t
 }
 
 // Bucket sums of windows [w0, w1) on stream s (they end on ping-pong side pip_steps & 1).
-static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, int c, int w0, int w1,
+static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, size_t count, int c, int w0, int w1,
                               hipStream_t s) {
-    const int W = w1 - w0;
-    const size_t NB = (size_t)1 << c, nb = (size_t)W * NB, N = (size_t)W * n, NC = NB / PM;
+    const int Wp = w1 - w0;
+    const size_t W = (size_t)Wp * count;   // virtual windows: the part's windows of every MSM
+    const size_t NB = (size_t)1 << c, nb = W * NB, N = W * n, NC = NB / PM;
     (void)P;
     // keys are generated window-major, so a STABLE sort on the c digit bits alone leaves each
     // (window, digit) bucket contiguous and in index order (buckets ordered digit-major)
@@ -435,7 +440,7 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
                                              (int)nb, s));
     PIP_RET(ws.temp.need(tb_sort > tb_scan ? tb_sort : tb_scan));
 
-    k_pip_keys<<<nb_of(N), PTPB, 0, s>>>(scal, n, c, w0, W, ws.keys_in.as<uint16_t>());
+    k_pip_keys<<<nb_of(N), PTPB, 0, s>>>(scal, n, c, w0, Wp, W, ws.keys_in.as<uint16_t>());
     PIP_RET(pip_sort(ws.temp.p, tb_sort, ws.keys_in.as<uint16_t>(), ws.keys.as<uint16_t>(), ws.vals.as<uint32_t>(), N,
                      kbits, s));
     PIP_RET(hipMemsetAsync(ws.start.p, 0, nb * 4, s));
@@ -476,14 +481,15 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
 }
 
 // Chunks -> window sums of windows [w0, w1) into Sw[w0 .. w1-1], on stream s (latency-bound).
-static hipError_t pip_finish(PipWs& ws, int c, int w0, int w1, ge* Sw, const ge* dtab, hipStream_t s) {
-    const int W = w1 - w0;
+static hipError_t pip_finish(PipWs& ws, size_t count, int c, int Wtot, int w0, int w1, ge* Sw, const ge* dtab,
+                             hipStream_t s) {
+    const int Wp = w1 - w0, W = Wp * (int)count;
     const size_t NC = ((size_t)1 << c) / PM;
     k_pip_chunks<<<nb_of(8 * (size_t)W * NC), PTPB, 0, s>>>(ws.Q[0].as<ge>(), ws.Q[1].as<ge>(), ws.off[0].as<uint32_t>(),
                                                          ws.off[1].as<uint32_t>(), ws.len[0].as<uint32_t>(),
                                                          ws.len[1].as<uint32_t>(), ws.maxlen.as<unsigned>(), c, W,
                                                          ws.V.as<ge>(), dtab);
-    k_pip_window<<<W, PTPB, 0, s>>>(ws.V.as<ge>(), (int)NC, Sw + w0);
+    k_pip_window<<<W, PTPB, 0, s>>>(ws.V.as<ge>(), (int)NC, Wp, Wtot, w0, Sw);
     return hipGetLastError();
 }
 
@@ -521,8 +527,9 @@ static hipError_t pip_pair(PipPair** out, hipStream_t s) {
     return hipSuccess;
 }
 
-hipError_t msm_pippenger(ge* result, const fe* scal, const ge* P, size_t n, int c, const ge* dtab, hipStream_t s) {
-    if (n == 0) return hipSuccess;
+hipError_t msm_pippenger(ge* result, const fe* scal, const ge* P, size_t n, size_t count, int c, const ge* dtab,
+                         hipStream_t s) {
+    if (n == 0 || count == 0) return hipSuccess;
     PipPair* pp = nullptr;
     PIP_RET(pip_pair(&pp, s));
     PipWs& hi = pp->hi;
@@ -531,20 +538,20 @@ hipError_t msm_pippenger(ge* result, const fe* scal, const ge* P, size_t n, int 
 #define BP_PIP_SPLIT8 3   // the bottom part's share of the windows, in eighths (3: measured best)
 #endif
     const int W = (256 + c - 1) / c, wm = (W * BP_PIP_SPLIT8) / 8 > 0 ? (W * BP_PIP_SPLIT8) / 8 : 1;
-    PIP_RET(hi.Sw.need((size_t)W * sizeof(ge)));
-    PIP_RET(hi.Tmid.need(sizeof(ge)));
+    PIP_RET(hi.Sw.need(count * W * sizeof(ge)));
+    PIP_RET(hi.Tmid.need(count * sizeof(ge)));
     ge* Sw = hi.Sw.as<ge>();
-    PIP_RET(pip_buckets(hi, scal, P, n, c, wm, W, s));
+    PIP_RET(pip_buckets(hi, scal, P, n, count, c, wm, W, s));
     PIP_RET(hipEventRecord(hi.ev[1], s));
     PIP_RET(hipStreamWaitEvent(hi.side, hi.ev[1], 0));
-    PIP_RET(pip_finish(hi, c, wm, W, Sw, dtab, hi.side));
-    k_pip_horner<<<1, 64, 0, hi.side>>>(Sw, W - 1, wm, c, nullptr, hi.Tmid.as<ge>());
+    PIP_RET(pip_finish(hi, count, c, W, wm, W, Sw, dtab, hi.side));
+    k_pip_horner<<<(unsigned)count, 64, 0, hi.side>>>(Sw, W, W - 1, wm, c, nullptr, hi.Tmid.as<ge>());
     PIP_RET(hipGetLastError());
-    PIP_RET(pip_buckets(lo, scal, P, n, c, 0, wm, s));
-    PIP_RET(pip_finish(lo, c, 0, wm, Sw, dtab, s));
+    PIP_RET(pip_buckets(lo, scal, P, n, count, c, 0, wm, s));
+    PIP_RET(pip_finish(lo, count, c, W, 0, wm, Sw, dtab, s));
     PIP_RET(hipEventRecord(hi.ev[2], s));
     PIP_RET(hipStreamWaitEvent(hi.side, hi.ev[2], 0));
-    k_pip_horner<<<1, 64, 0, hi.side>>>(Sw, wm - 1, 0, c, hi.Tmid.as<ge>(), result);
+    k_pip_horner<<<(unsigned)count, 64, 0, hi.side>>>(Sw, W, wm - 1, 0, c, hi.Tmid.as<ge>(), result);
     PIP_RET(hipGetLastError());
     PIP_RET(hipEventRecord(hi.ev[3], hi.side));
     PIP_RET(hipStreamWaitEvent(s, hi.ev[3], 0));          // the result is ready in the caller's stream order

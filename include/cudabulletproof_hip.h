@@ -255,6 +255,11 @@ int hipbp_msm_batch(ge25519* results, const fe25519* scalars, const ge25519* poi
  * No reference counterpart. */
 int hipbp_msm_pippenger(ge25519* result, const fe25519* scalars, const ge25519* points, size_t n,
                         int window_bits, void* stream);
+/* count Pippenger MSMs over the SAME n device points in one call: results[m] = hipbp_msm_pippenger
+ * of scalars[m n .. m n + n) (bit for bit).  One sort, one set of bucket-tree launches and one
+ * Horner launch serve all of them, so the latency-bound chains are shared.  count <= 65535. */
+int hipbp_msm_pippenger_batch(ge25519* results, const fe25519* scalars, const ge25519* points, size_t n,
+                              size_t count, int window_bits, void* stream);
 /* Canonical tree over n device points: for stride 1, 2, 4, ...: T[i] = Ndev(T[i] + T[i+stride])
  * for i % (2 stride) == 0 and i + stride < n; result = T[0] (the reduction half of
  * cuda_bulletproof_kernels.cu:45-115).  hipbp_msm = this tree over the per-point

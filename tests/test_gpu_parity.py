@@ -756,6 +756,27 @@ def test_msm_pippenger_concurrent_streams(bp, oracle):
             assert np.array_equal(got[r * len(cases) + k], want), (r, k)
 
 
+@pytest.mark.parametrize("n,count,c", [(300, 3, 12), (1000, 5, 8), (1, 4, 4), (4096, 2, 12), (777, 1, 4)])
+def test_msm_pippenger_batch_vs_oracle(bp, oracle, n, count, c):
+    """hipbp_msm_pippenger_batch: count MSMs over the same points in one call, each equal to
+    orc_msm_pippenger of its own scalars (shared sort / bucket trees / Horner launch)."""
+    import torch
+    rng = np.random.default_rng(n * 7 + count)
+    P = oracle.base_points(n, 31)
+    s = rand_fe(rng, count * n)
+    s[::11] = 0
+    if n > 100:
+        s[5::13] = s[5]                           # crowded buckets across the MSMs
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    out = torch.zeros(count, 16, dtype=torch.int64, device=dev)
+    bp.msm_pippenger_batch(out, T(s), T(P), c)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint64)
+    for m in range(count):
+        assert np.array_equal(got[m], oracle.msm_pippenger(s[m * n:(m + 1) * n], P, c)), m
+
+
 def test_msm_pippenger_rejects_bad_window(bp):
     import torch
     dev = torch.device("cuda:0")
