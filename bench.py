@@ -248,6 +248,7 @@ def msm_leg(args, dev, world, rank, T):
         ns, m = 2, 4 * reps
         sts = [torch.cuda.Stream(dev) for _ in range(ns)]
         outs = torch.zeros(m, 16, dtype=torch.int64, device=dev)
+        torch.cuda.synchronize(dev)   # the zero fill is on torch's stream, the MSMs are not
         for i in range(ns):
             bp.msm_pippenger(outs[i], scd, ptd, 12, stream=sts[i])
         torch.cuda.synchronize(dev)
@@ -257,9 +258,32 @@ def msm_leg(args, dev, world, rank, T):
         torch.cuda.synchronize(dev)
         tdt = (time.perf_counter() - t1) / m
         same = bool((outs == out.unsqueeze(0)).all().item())
+        # batched: hipbp_msm_pippenger_batch, bc MSMs over the same points in one sort/tree pass
+        # (MSM j's scalars = the config-3 scalars rolled by j rows), bc-batches on two streams
+        bc = 4
+        sb = torch.cat([torch.roll(scd, j, 0) for j in range(bc)]).contiguous()
+        want = torch.zeros(bc, 16, dtype=torch.int64, device=dev)
+        for j in range(bc):
+            bp.msm_pippenger(want[j], sb[j * nm:(j + 1) * nm], ptd, 12)
+        bouts = [torch.zeros(bc, 16, dtype=torch.int64, device=dev) for _ in range(ns)]
+        torch.cuda.synchronize(dev)
+        for i in range(ns):
+            bp.msm_pippenger_batch(bouts[i], sb, ptd, 12, stream=sts[i])
+        torch.cuda.synchronize(dev)
+        bm = 2 * reps
+        t1 = time.perf_counter()
+        for k in range(bm):
+            bp.msm_pippenger_batch(bouts[k % ns], sb, ptd, 12, stream=sts[k % ns])
+        torch.cuda.synchronize(dev)
+        bdt = (time.perf_counter() - t1) / (bm * bc)
+        bsame = all(bool((o == want).all().item()) for o in bouts)
+        del sb
         pip = {"metric": "MSM points/sec (Pippenger, window 12)", "value": nm / tdt, "unit": "points/s",
                "ms_per_msm": tdt * 1e3, "msms_in_flight": ns, "msms_timed": m, "all_results_equal": same,
                "single_stream": {"value": nm / pdt, "ms_per_msm": pdt * 1e3},
+               "batched": {"value": nm / bdt, "ms_per_msm": bdt * 1e3, "msms_per_call": bc, "streams": ns,
+                           "msms_timed": bm * bc, "all_match_single_calls": bsame,
+                           "api": "hipbp_msm_pippenger_batch (same points, count scalar sets)"},
                "window_bits": 12, "result_sha256": pd,
                "matches_oracle_golden": (pd == gold["pippenger_w12"]["digest"]) if gold else None,
                "semantics": "labelled alternative (hipbp_msm_pippenger): bucket algorithm over the reference's "

@@ -37,54 +37,113 @@ namespace {
 constexpr int PTPB = 256;
 constexpr int PM = 16;   // buckets per chunk
 
+// Division of 32-bit values by a run-time invariant d >= 1 (round-up multiplier, Granlund and
+// Montgomery): q = (t + ((x - t) >> s1)) >> s2 with t = umulhi(m, x), exact for every 32-bit x.
+struct FastDiv {
+    uint32_t d, m;
+    int s1, s2;
+};
+inline FastDiv fastdiv_make(uint32_t d) {
+    int l = 0;
+    while (l < 32 && (1ull << l) < d) l++;
+    FastDiv f;
+    f.d = d;
+    f.m = (uint32_t)((((1ull << l) - d) << 32) / d + 1);
+    f.s1 = l < 1 ? l : 1;
+    f.s2 = l > 1 ? l - 1 : 0;
+    return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t x, const FastDiv& f) {
+    const uint32_t t = __umulhi(f.m, x);
+    return (t + ((x - t) >> f.s1)) >> f.s2;
+}
+
 // Sort input: element g = v n + i (virtual window v = m Wp + lw: MSM m of the batch, window
 // lw = w - w0 of the part, point i), generated window-major; its key is the c-bit digit alone (16
 // bits) and its value is g itself (a counting iterator, never stored), so after a STABLE sort on
 // the digit each bucket (v, d) is contiguous and in index order, and the bucket of a sorted element
-// is ((g / n) << c) | digit.  MSM m's scalars are s[m n .. m n + n); all share the points.
-__global__ __launch_bounds__(PTPB) void k_pip_keys(const fe* __restrict__ s, size_t n, int c, int w0, int Wp,
-                                                  size_t Wv, uint16_t* keys) {
-    const size_t g = (size_t)blockIdx.x * PTPB + threadIdx.x;
-    if (g >= Wv * n) return;
-    const size_t v = g / n, i = g % n, m = v / (size_t)Wp;
-    const int lo = c * (w0 + (int)(v % (size_t)Wp));
-    // bits [lo, lo + c) of the 256-bit scalar (a window may straddle two limbs or end past bit 255)
-    const uint64_t* sc = s[m * n + i].v;   // only the limb(s) the window touches
-    const int li = lo >> 6, sh = lo & 63;
-    uint64_t x = sc[li] >> sh;
-    if (sh && li < 3) x |= sc[li + 1] << (64 - sh);
-    keys[g] = (uint16_t)(x & ((1ull << c) - 1));
+// is ((g / n) << c) | digit.  MSM m's scalars are s[m n .. m n + n); all share the points.  One
+// thread per scalar (m, i): it reads the scalar once and writes its Wp keys, each store coalesced
+// over consecutive i.
+template <int V>   // V consecutive scalars per thread (V > 1 needs n % V == 0: one V-key store per window)
+__global__ __launch_bounds__(PTPB) void k_pip_keys(const fe* __restrict__ s, FastDiv fn, uint32_t count, int c,
+                                                  int w0, int Wp, uint16_t* keys) {
+    const uint32_t n = fn.d, g = (blockIdx.x * PTPB + threadIdx.x) * V;
+    if (g >= count * n) return;
+    const uint32_t m = fdiv(g, fn), i = g - m * n;
+    fe sc[V];
+#pragma unroll
+    for (int u = 0; u < V; u++) sc[u] = s[g + u];
+    const uint64_t mask = (1ull << c) - 1;
+    uint16_t* out = keys + (size_t)m * Wp * n + i;
+    for (int lw = 0; lw < Wp; lw++) {
+        // bits [lo, lo + c) of the 256-bit scalar (a window may straddle two limbs or end past bit 255)
+        const int lo = c * (w0 + lw), li = lo >> 6, sh = lo & 63;
+        uint16_t d[V];
+#pragma unroll
+        for (int u = 0; u < V; u++) {
+            uint64_t x = sc[u].v[li] >> sh;
+            if (sh && li < 3) x |= sc[u].v[li + 1] << (64 - sh);
+            d[u] = (uint16_t)(x & mask);
+        }
+        if constexpr (V == 4) {
+            *(uint64_t*)(out + (size_t)lw * n) =
+                (uint64_t)d[0] | ((uint64_t)d[1] << 16) | ((uint64_t)d[2] << 32) | ((uint64_t)d[3] << 48);
+        } else {
+            out[(size_t)lw * n] = d[0];
+        }
+    }
 }
 
 __device__ __forceinline__ uint32_t pip_bucket(const uint16_t* __restrict__ keys, const uint32_t* __restrict__ vals,
-                                               size_t p, uint32_t n, int c) {
-    return ((vals[p] / n) << c) | keys[p];
+                                               size_t p, const FastDiv& fn, int c) {
+    return (fdiv(vals[p], fn) << c) | keys[p];
 }
 
-// first/last occurrence of each bucket in the sorted array -> bucket start and length
-__global__ __launch_bounds__(PTPB) void k_pip_bounds(const uint16_t* __restrict__ keys,
-                                                    const uint32_t* __restrict__ vals, size_t N, uint32_t n, int c,
-                                                    uint32_t* start, uint32_t* len) {
-    const size_t p = (size_t)blockIdx.x * PTPB + threadIdx.x;
-    if (p >= N) return;
-    const uint32_t k = pip_bucket(keys, vals, p, n, c);
-    if (p == 0 || pip_bucket(keys, vals, p - 1, n, c) != k) start[k] = (uint32_t)p;
-    if (p == N - 1 || pip_bucket(keys, vals, p + 1, n, c) != k) len[k] = (uint32_t)(p + 1);   // end, made a length below
+// Bucket sizes straight from the unsorted keys (the sort only orders them): a block takes a tile
+// of one virtual window's keys, counts the digits in LDS and adds its counts to cnt[(v << c) | d].
+constexpr uint32_t HIST_TILE = 65536;
+__global__ __launch_bounds__(PTPB) void k_pip_hist(const uint16_t* __restrict__ keys, uint32_t n, int c,
+                                                  uint32_t tpw, uint32_t* cnt) {
+    extern __shared__ uint32_t h[];
+    const uint32_t NB = 1u << c, v = blockIdx.x / tpw, t = blockIdx.x - v * tpw;
+    for (uint32_t d = threadIdx.x; d < NB; d += PTPB) h[d] = 0;
+    __syncthreads();
+    const uint16_t* __restrict__ k = keys + (size_t)v * n;
+    const uint32_t e = (t + 1) * HIST_TILE < n ? (t + 1) * HIST_TILE : n;
+    for (uint32_t j = t * HIST_TILE + threadIdx.x; j < e; j += PTPB) atomicAdd(&h[k[j]], 1u);
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < NB; d += PTPB)
+        if (h[d]) atomicAdd(&cnt[((size_t)v << c) | d], h[d]);
 }
 
 // Bucket lists are processed two tree levels per launch ("steps"): a step's lane takes one
 // aligned group of 4 consecutive elements of one bucket's current list and reduces it exactly as
 // levels s and 2s of the pairwise tree do (x0+x1, x2+x3, then their sum; a short last group
 // carries), so lists are padded to a multiple of 4.  bid[pos] = the bucket of element pos (every
-// group head is a real element, so no search is needed).
-__global__ __launch_bounds__(PTPB) void k_pip_len0(const uint32_t* __restrict__ start, uint32_t* len, uint32_t* pad,
-                                                  size_t nb, unsigned* maxlen) {
+// group head is a real element, so no search is needed).  k_pip_len0: the padded lengths, the
+// longest list (one atomic per wave), and the counts in sorted order — digit-major, virtual
+// window minor — whose exclusive scan is each bucket's start in the sorted array.
+__global__ __launch_bounds__(PTPB) void k_pip_len0(const uint32_t* __restrict__ len, uint32_t* pad, uint32_t* cnt_t,
+                                                  size_t nb, int c, uint32_t Wv, unsigned* maxlen) {
     const size_t b = (size_t)blockIdx.x * PTPB + threadIdx.x;
-    if (b >= nb) return;
-    const uint32_t L = len[b] ? len[b] - start[b] : 0;
-    len[b] = L;
-    pad[b] = (L + 3) & ~3u;
-    if (L) atomicMax(maxlen, L);
+    uint32_t L = 0;
+    if (b < nb) {
+        L = len[b];
+        pad[b] = (L + 3) & ~3u;
+        cnt_t[(b & ((1u << c) - 1)) * Wv + (b >> c)] = L;
+    }
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+        const uint32_t o = __shfl_xor(L, d, 64);
+        L = o > L ? o : L;
+    }
+    if ((threadIdx.x & 63) == 0 && L) atomicMax(maxlen, L);
+}
+__global__ __launch_bounds__(PTPB) void k_pip_start(const uint32_t* __restrict__ start_t, size_t nb, int c, uint32_t Wv,
+                                                   uint32_t* start) {
+    const size_t b = (size_t)blockIdx.x * PTPB + threadIdx.x;
+    if (b < nb) start[b] = start_t[(b & ((1u << c) - 1)) * Wv + (b >> c)];
 }
 
 // Tree steps needed for the longest bucket list (levels = ceil(log2 maxlen), at least 1; two
@@ -174,16 +233,16 @@ __global__ __launch_bounds__(PTPB) void k_pip_scan_fin(int t, const unsigned* __
 }
 
 __global__ __launch_bounds__(PTPB) void k_pip_bid0(const uint16_t* __restrict__ keys, const uint32_t* __restrict__ vals,
-                                                  size_t N, uint32_t n, int c, const uint32_t* __restrict__ start,
+                                                  size_t N, FastDiv fn, int c, const uint32_t* __restrict__ start,
                                                   const uint32_t* __restrict__ off, uint32_t* bid) {
     const size_t p = (size_t)blockIdx.x * PTPB + threadIdx.x;
     if (p >= N) return;
-    const uint32_t b = pip_bucket(keys, vals, p, n, c);
+    const uint32_t b = pip_bucket(keys, vals, p, fn, c);
     bid[off[b] + (p - start[b])] = b;
 }
 
 __global__ __launch_bounds__(PTPB) void k_pip_step(int t, const unsigned* __restrict__ maxlen, const ge* __restrict__ P,
-                                                  uint32_t n,
+                                                  FastDiv fn,
                                                   const uint32_t* __restrict__ vals,
                                                   const uint32_t* __restrict__ start, const ge* __restrict__ Qin,
                                                   const uint32_t* __restrict__ bid, const uint32_t* __restrict__ off,
@@ -200,7 +259,11 @@ __global__ __launch_bounds__(PTPB) void k_pip_step(int t, const unsigned* __rest
     const uint32_t j = pos - off[b], L = len[b];
     const uint32_t r = L - j < 4 ? L - j : 4;
     const size_t base = first ? (size_t)start[b] + j : (size_t)off[b] + j;
-    auto load = [&](uint32_t t) -> ge { return first ? P[vals[base + t] % n] : Qin[base + t]; };
+    auto load = [&](uint32_t t) -> ge {
+        if (!first) return Qin[base + t];
+        const uint32_t g = vals[base + t];
+        return P[g - fdiv(g, fn) * fn.d];
+    };
     // the first level adds two input points: when every active lane's second one has Z exactly 1
     // (affine inputs, a wave-uniform test), Z1 Z2 is fe_mul_one(Z1) — same bits, no product
     auto add_in = [&](const ge& a, const ge& b) -> ge {
@@ -440,19 +503,29 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
                                              (int)nb, s));
     PIP_RET(ws.temp.need(tb_sort > tb_scan ? tb_sort : tb_scan));
 
-    k_pip_keys<<<nb_of(N), PTPB, 0, s>>>(scal, n, c, w0, Wp, W, ws.keys_in.as<uint16_t>());
-    PIP_RET(pip_sort(ws.temp.p, tb_sort, ws.keys_in.as<uint16_t>(), ws.keys.as<uint16_t>(), ws.vals.as<uint32_t>(), N,
-                     kbits, s));
-    PIP_RET(hipMemsetAsync(ws.start.p, 0, nb * 4, s));
+    const FastDiv fn = fastdiv_make((uint32_t)n);
+    if (n % 4 == 0)   // keys_in rows start 8-byte aligned (DBuf memory, n % 4 == 0)
+        k_pip_keys<4><<<nb_of(count * n / 4), PTPB, 0, s>>>(scal, fn, (uint32_t)count, c, w0, Wp,
+                                                            ws.keys_in.as<uint16_t>());
+    else
+        k_pip_keys<1><<<nb_of(count * n), PTPB, 0, s>>>(scal, fn, (uint32_t)count, c, w0, Wp,
+                                                        ws.keys_in.as<uint16_t>());
     PIP_RET(hipMemsetAsync(ws.len[0].p, 0, nb * 4, s));
     PIP_RET(hipMemsetAsync(ws.maxlen.p, 0, sizeof(unsigned), s));
-    k_pip_bounds<<<nb_of(N), PTPB, 0, s>>>(ws.keys.as<uint16_t>(), ws.vals.as<uint32_t>(), N, (uint32_t)n, c,
-                                           ws.start.as<uint32_t>(), ws.len[0].as<uint32_t>());
-    k_pip_len0<<<nb_of(nb), PTPB, 0, s>>>(ws.start.as<uint32_t>(), ws.len[0].as<uint32_t>(), ws.pad[0].as<uint32_t>(),
-                                          nb, ws.maxlen.as<unsigned>());
+    const uint32_t tpw = (uint32_t)((n + HIST_TILE - 1) / HIST_TILE);
+    k_pip_hist<<<(unsigned)(W * tpw), PTPB, NB * 4, s>>>(ws.keys_in.as<uint16_t>(), (uint32_t)n, c, tpw,
+                                                          ws.len[0].as<uint32_t>());
+    // len[1] / off[1] are free until step 0: the transposed counts and their scan
+    k_pip_len0<<<nb_of(nb), PTPB, 0, s>>>(ws.len[0].as<uint32_t>(), ws.pad[0].as<uint32_t>(), ws.len[1].as<uint32_t>(),
+                                          nb, c, (uint32_t)W, ws.maxlen.as<unsigned>());
+    PIP_RET(hipcub::DeviceScan::ExclusiveSum(ws.temp.p, tb_scan, ws.len[1].as<uint32_t>(), ws.off[1].as<uint32_t>(),
+                                             (int)nb, s));
+    k_pip_start<<<nb_of(nb), PTPB, 0, s>>>(ws.off[1].as<uint32_t>(), nb, c, (uint32_t)W, ws.start.as<uint32_t>());
     PIP_RET(hipcub::DeviceScan::ExclusiveSum(ws.temp.p, tb_scan, ws.pad[0].as<uint32_t>(), ws.off[0].as<uint32_t>(),
                                              (int)nb, s));
-    k_pip_bid0<<<nb_of(N), PTPB, 0, s>>>(ws.keys.as<uint16_t>(), ws.vals.as<uint32_t>(), N, (uint32_t)n, c,
+    PIP_RET(pip_sort(ws.temp.p, tb_sort, ws.keys_in.as<uint16_t>(), ws.keys.as<uint16_t>(), ws.vals.as<uint32_t>(), N,
+                     kbits, s));
+    k_pip_bid0<<<nb_of(N), PTPB, 0, s>>>(ws.keys.as<uint16_t>(), ws.vals.as<uint32_t>(), N, fn, c,
                                          ws.start.as<uint32_t>(), ws.off[0].as<uint32_t>(), ws.bid[0].as<uint32_t>());
     // the worst-case step count (a bucket list is at most n long); steps past the depth of the
     // data exit on the device (pip_steps), so nothing here waits for the GPU
@@ -470,7 +543,7 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
                                                 ws.part.as<uint32_t>());
         k_pip_scan_fin<<<nparts, PTPB, 0, s>>>(t, ws.maxlen.as<unsigned>(), ws.pad[b].as<uint32_t>(),
                                                ws.part.as<uint32_t>(), nb, ws.off[b].as<uint32_t>());
-        k_pip_step<<<nb_of(lanes), PTPB, 0, s>>>(t, ws.maxlen.as<unsigned>(), P, (uint32_t)n, ws.vals.as<uint32_t>(),
+        k_pip_step<<<nb_of(lanes), PTPB, 0, s>>>(t, ws.maxlen.as<unsigned>(), P, fn, ws.vals.as<uint32_t>(),
                                                   ws.start.as<uint32_t>(), ws.Q[a].as<ge>(), ws.bid[a].as<uint32_t>(),
                                                   ws.off[a].as<uint32_t>(), ws.len[a].as<uint32_t>(),
                                                   ws.pad[a].as<uint32_t>(), ws.off[b].as<uint32_t>(), ws.Q[b].as<ge>(),

@@ -711,7 +711,8 @@ def test_sq_matches_mul(bp, oracle):
 
 
 # ----------------------------------------------------------------------------- Pippenger (labelled alternative)
-@pytest.mark.parametrize("n,c", [(1, 12), (2, 4), (17, 12), (300, 12), (1000, 8), (777, 4), (20000, 8), (4096, 12)])
+@pytest.mark.parametrize("n,c", [(1, 12), (2, 4), (17, 12), (300, 12), (1000, 8), (777, 4), (20000, 8), (4096, 12),
+                                 (70000, 8)])   # n > 65536: several histogram tiles per window
 def test_msm_pippenger_vs_oracle(bp, oracle, n, c):
     """hipbp_msm_pippenger == orc_msm_pippenger (the bucket algorithm restated in C): zero and short
     scalars (empty / crowded buckets), odd bucket sizes, every window width class."""
@@ -756,7 +757,8 @@ def test_msm_pippenger_concurrent_streams(bp, oracle):
             assert np.array_equal(got[r * len(cases) + k], want), (r, k)
 
 
-@pytest.mark.parametrize("n,count,c", [(300, 3, 12), (1000, 5, 8), (1, 4, 4), (4096, 2, 12), (777, 1, 4)])
+@pytest.mark.parametrize("n,count,c", [(300, 3, 12), (1000, 5, 8), (1, 4, 4), (4096, 2, 12), (777, 1, 4),
+                                       (70001, 2, 12), (1002, 3, 12)])   # odd n: one key per thread
 def test_msm_pippenger_batch_vs_oracle(bp, oracle, n, count, c):
     """hipbp_msm_pippenger_batch: count MSMs over the same points in one call, each equal to
     orc_msm_pippenger of its own scalars (shared sort / bucket trees / Horner launch)."""
