@@ -321,10 +321,16 @@ __device__ __forceinline__ fe fe_quad_bcast(const fe& a) {
     }
     return r;
 }
+// (bit masks, not a ternary chain: the compiler turned that into a private array indexed by q,
+// i.e. scratch stores and loads inside the dependent chains)
 __device__ __forceinline__ fe fe_sel4(int q, const fe& a, const fe& b, const fe& c, const fe& d) {
+    const uint64_t m0 = 0ull - (uint64_t)(q & 1), m1 = 0ull - (uint64_t)((q >> 1) & 1);
     fe r;
 #pragma unroll
-    for (int i = 0; i < 4; i++) r.v[i] = q == 0 ? a.v[i] : q == 1 ? b.v[i] : q == 2 ? c.v[i] : d.v[i];
+    for (int i = 0; i < 4; i++) {
+        const uint64_t ab = a.v[i] ^ ((a.v[i] ^ b.v[i]) & m0), cd = c.v[i] ^ ((c.v[i] ^ d.v[i]) & m0);
+        r.v[i] = ab ^ ((ab ^ cd) & m1);
+    }
     return r;
 }
 // DBL: add(p, p) (q ignored); else add(p, q).  p, q replicated over the quad; result replicated.
