@@ -25,6 +25,7 @@
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 
+#include <cstdlib>
 #include <map>
 #include <mutex>
 
@@ -59,15 +60,17 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t x, const FastDiv& f) {
 }
 
 // Sort input: element g = v n + i (virtual window v = m Wp + lw: MSM m of the batch, window
-// lw = w - w0 of the part, point i), generated window-major; its key is the c-bit digit alone (16
-// bits) and its value is g itself (a counting iterator, never stored), so after a STABLE sort on
-// the digit each bucket (v, d) is contiguous and in index order, and the bucket of a sorted element
-// is ((g / n) << c) | digit.  MSM m's scalars are s[m n .. m n + n); all share the points.  One
-// thread per scalar (m, i): it reads the scalar once and writes its Wp keys, each store coalesced
-// over consecutive i.
-template <int V>   // V consecutive scalars per thread (V > 1 needs n % V == 0: one V-key store per window)
+// lw = w - w0 of the part, point i), generated window-major, so a STABLE sort on the digit leaves
+// each bucket (v, d) contiguous and in index order (buckets in digit-major order).  Two key forms:
+//  * 32-bit keys (when c + ib <= 32, ib = bits of n - 1): key = digit << ib | i, sorted on bits
+//    [ib, ib + c) with no values; the sorted key itself names the point.
+//  * 16-bit keys otherwise: key = the digit, value = g (a counting iterator, never stored); the
+//    bucket of a sorted element is ((g / n) << c) | digit.
+// MSM m's scalars are s[m n .. m n + n); all share the points.  One thread per V scalars (m, i..):
+// it reads them once and writes their Wp keys, each store coalesced over consecutive i.
+template <int V, typename KT>   // V > 1 needs n % V == 0 (one V-key store per window)
 __global__ __launch_bounds__(PTPB) void k_pip_keys(const fe* __restrict__ s, FastDiv fn, uint32_t count, int c,
-                                                  int w0, int Wp, uint16_t* keys) {
+                                                  int ib, int w0, int Wp, KT* keys) {
     const uint32_t n = fn.d, g = (blockIdx.x * PTPB + threadIdx.x) * V;
     if (g >= count * n) return;
     const uint32_t m = fdiv(g, fn), i = g - m * n;
@@ -75,22 +78,25 @@ __global__ __launch_bounds__(PTPB) void k_pip_keys(const fe* __restrict__ s, Fas
 #pragma unroll
     for (int u = 0; u < V; u++) sc[u] = s[g + u];
     const uint64_t mask = (1ull << c) - 1;
-    uint16_t* out = keys + (size_t)m * Wp * n + i;
+    KT* out = keys + (size_t)m * Wp * n + i;
     for (int lw = 0; lw < Wp; lw++) {
         // bits [lo, lo + c) of the 256-bit scalar (a window may straddle two limbs or end past bit 255)
         const int lo = c * (w0 + lw), li = lo >> 6, sh = lo & 63;
-        uint16_t d[V];
+        uint32_t d[V];
 #pragma unroll
         for (int u = 0; u < V; u++) {
             uint64_t x = sc[u].v[li] >> sh;
             if (sh && li < 3) x |= sc[u].v[li + 1] << (64 - sh);
-            d[u] = (uint16_t)(x & mask);
+            d[u] = (uint32_t)(x & mask);
+            if constexpr (sizeof(KT) == 4) d[u] = (d[u] << ib) | (i + u);
         }
-        if constexpr (V == 4) {
-            *(uint64_t*)(out + (size_t)lw * n) =
-                (uint64_t)d[0] | ((uint64_t)d[1] << 16) | ((uint64_t)d[2] << 32) | ((uint64_t)d[3] << 48);
+        KT* o = out + (size_t)lw * n;
+        if constexpr (V == 4 && sizeof(KT) == 2) {
+            *(uint64_t*)o = (uint64_t)d[0] | ((uint64_t)d[1] << 16) | ((uint64_t)d[2] << 32) | ((uint64_t)d[3] << 48);
+        } else if constexpr (V == 4) {
+            *(uint4*)o = make_uint4(d[0], d[1], d[2], d[3]);
         } else {
-            out[(size_t)lw * n] = d[0];
+            o[0] = (KT)d[0];
         }
     }
 }
@@ -103,15 +109,16 @@ __device__ __forceinline__ uint32_t pip_bucket(const uint16_t* __restrict__ keys
 // Bucket sizes straight from the unsorted keys (the sort only orders them): a block takes a tile
 // of one virtual window's keys, counts the digits in LDS and adds its counts to cnt[(v << c) | d].
 constexpr uint32_t HIST_TILE = 65536;
-__global__ __launch_bounds__(PTPB) void k_pip_hist(const uint16_t* __restrict__ keys, uint32_t n, int c,
+template <typename KT>
+__global__ __launch_bounds__(PTPB) void k_pip_hist(const KT* __restrict__ keys, uint32_t n, int c, int ib,
                                                   uint32_t tpw, uint32_t* cnt) {
     extern __shared__ uint32_t h[];
     const uint32_t NB = 1u << c, v = blockIdx.x / tpw, t = blockIdx.x - v * tpw;
     for (uint32_t d = threadIdx.x; d < NB; d += PTPB) h[d] = 0;
     __syncthreads();
-    const uint16_t* __restrict__ k = keys + (size_t)v * n;
+    const KT* __restrict__ k = keys + (size_t)v * n;
     const uint32_t e = (t + 1) * HIST_TILE < n ? (t + 1) * HIST_TILE : n;
-    for (uint32_t j = t * HIST_TILE + threadIdx.x; j < e; j += PTPB) atomicAdd(&h[k[j]], 1u);
+    for (uint32_t j = t * HIST_TILE + threadIdx.x; j < e; j += PTPB) atomicAdd(&h[(uint32_t)k[j] >> ib], 1u);
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < NB; d += PTPB)
         if (h[d]) atomicAdd(&cnt[((size_t)v << c) | d], h[d]);
@@ -241,8 +248,18 @@ __global__ __launch_bounds__(PTPB) void k_pip_bid0(const uint16_t* __restrict__ 
     bid[off[b] + (p - start[b])] = b;
 }
 
+// 32-bit-key path: bid from the layout alone (no sorted value says which virtual window an element
+// is in): one wave per bucket writes its list's positions.
+__global__ __launch_bounds__(PTPB) void k_pip_bidfill(const uint32_t* __restrict__ len, const uint32_t* __restrict__ off,
+                                                     size_t nb, uint32_t* bid) {
+    const size_t b = ((size_t)blockIdx.x * PTPB + threadIdx.x) >> 6;
+    if (b >= nb) return;
+    const uint32_t L = len[b], o = off[b];
+    for (uint32_t j = threadIdx.x & 63; j < L; j += 64) bid[o + j] = (uint32_t)b;
+}
+
 __global__ __launch_bounds__(PTPB) void k_pip_step(int t, const unsigned* __restrict__ maxlen, const ge* __restrict__ P,
-                                                  FastDiv fn,
+                                                  FastDiv fn, const uint32_t* __restrict__ keys32, uint32_t imask,
                                                   const uint32_t* __restrict__ vals,
                                                   const uint32_t* __restrict__ start, const ge* __restrict__ Qin,
                                                   const uint32_t* __restrict__ bid, const uint32_t* __restrict__ off,
@@ -261,6 +278,7 @@ __global__ __launch_bounds__(PTPB) void k_pip_step(int t, const unsigned* __rest
     const size_t base = first ? (size_t)start[b] + j : (size_t)off[b] + j;
     auto load = [&](uint32_t t) -> ge {
         if (!first) return Qin[base + t];
+        if (keys32) return P[keys32[base + t] & imask];
         const uint32_t g = vals[base + t];
         return P[g - fdiv(g, fn) * fn.d];
     };
@@ -479,6 +497,16 @@ static hipError_t pip_sort(void* temp, size_t& tb, const uint16_t* kin, uint16_t
     return rocprim::radix_sort_pairs(temp, tb, kin, kout, rocprim::counting_iterator<uint32_t>(0u), vout,
                                      (unsigned)N, 0u, (unsigned)bits, s);
 }
+// stable sort of the 32-bit keys (digit << ib | i) on bits [ib, ib + c): keys only
+static hipError_t pip_sort32(void* temp, size_t& tb, const uint32_t* kin, uint32_t* kout, size_t N, int ib, int c,
+                             hipStream_t s) {
+    return rocprim::radix_sort_keys(temp, tb, kin, kout, (unsigned)N, (unsigned)ib, (unsigned)(ib + c), s);
+}
+// HIPBP_PIP_KEYS16=1 forces the 16-bit-key path (read per call: tests run both paths in one process)
+static bool pip_force16() {
+    const char* e = getenv("HIPBP_PIP_KEYS16");
+    return e && e[0] == '1';
+}
 
 // Bucket sums of windows [w0, w1) on stream s (they end on ping-pong side pip_steps & 1).
 static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, size_t count, int c, int w0, int w1,
@@ -486,12 +514,12 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
     const int Wp = w1 - w0;
     const size_t W = (size_t)Wp * count;   // virtual windows: the part's windows of every MSM
     const size_t NB = (size_t)1 << c, nb = W * NB, N = W * n, NC = NB / PM;
-    (void)P;
-    // keys are generated window-major, so a STABLE sort on the c digit bits alone leaves each
-    // (window, digit) bucket contiguous and in index order (buckets ordered digit-major)
-    const int kbits = c;
-    PIP_RET(ws.keys_in.need(N * 2));
-    PIP_RET(ws.keys.need(N * 2)); PIP_RET(ws.vals.need(N * 4));
+    int ib = 0;   // bits of the point index in a 32-bit key
+    while (ib < 32 && ((size_t)1 << ib) < n) ib++;
+    const bool k32 = c + ib <= 32 && !pip_force16();
+    PIP_RET(ws.keys_in.need(N * (k32 ? 4 : 2)));
+    PIP_RET(ws.keys.need(N * (k32 ? 4 : 2)));
+    if (!k32) PIP_RET(ws.vals.need(N * 4));
     PIP_RET(ws.start.need(nb * 4));
     for (int i = 0; i < 2; i++) {
         PIP_RET(ws.len[i].need(nb * 4)); PIP_RET(ws.pad[i].need(nb * 4)); PIP_RET(ws.off[i].need(nb * 4));
@@ -503,24 +531,36 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
     PIP_RET(ws.V.need((size_t)W * NC * sizeof(ge)));
     PIP_RET(ws.maxlen.need(sizeof(unsigned)));
     size_t tb_sort = 0, tb_scan = 0;
-    PIP_RET(pip_sort(nullptr, tb_sort, ws.keys_in.as<uint16_t>(), ws.keys.as<uint16_t>(), ws.vals.as<uint32_t>(), N,
-                     kbits, s));
+    if (k32)
+        PIP_RET(pip_sort32(nullptr, tb_sort, ws.keys_in.as<uint32_t>(), ws.keys.as<uint32_t>(), N, ib, c, s));
+    else
+        PIP_RET(pip_sort(nullptr, tb_sort, ws.keys_in.as<uint16_t>(), ws.keys.as<uint16_t>(), ws.vals.as<uint32_t>(),
+                         N, c, s));
     PIP_RET(hipcub::DeviceScan::ExclusiveSum(nullptr, tb_scan, ws.pad[0].as<uint32_t>(), ws.off[0].as<uint32_t>(),
                                              (int)nb, s));
     PIP_RET(ws.temp.need(tb_sort > tb_scan ? tb_sort : tb_scan));
 
     const FastDiv fn = fastdiv_make((uint32_t)n);
-    if (n % 4 == 0)   // keys_in rows start 8-byte aligned (DBuf memory, n % 4 == 0)
-        k_pip_keys<4><<<nb_of(count * n / 4), PTPB, 0, s>>>(scal, fn, (uint32_t)count, c, w0, Wp,
-                                                            ws.keys_in.as<uint16_t>());
+    // keys_in rows start 8-byte (16-byte) aligned when n % 4 == 0 (DBuf memory)
+    const bool v4 = n % 4 == 0;
+    const unsigned kgrid = nb_of(v4 ? count * n / 4 : count * n);
+    if (k32 && v4)
+        k_pip_keys<4, uint32_t><<<kgrid, PTPB, 0, s>>>(scal, fn, (uint32_t)count, c, ib, w0, Wp, ws.keys_in.as<uint32_t>());
+    else if (k32)
+        k_pip_keys<1, uint32_t><<<kgrid, PTPB, 0, s>>>(scal, fn, (uint32_t)count, c, ib, w0, Wp, ws.keys_in.as<uint32_t>());
+    else if (v4)
+        k_pip_keys<4, uint16_t><<<kgrid, PTPB, 0, s>>>(scal, fn, (uint32_t)count, c, 0, w0, Wp, ws.keys_in.as<uint16_t>());
     else
-        k_pip_keys<1><<<nb_of(count * n), PTPB, 0, s>>>(scal, fn, (uint32_t)count, c, w0, Wp,
-                                                        ws.keys_in.as<uint16_t>());
+        k_pip_keys<1, uint16_t><<<kgrid, PTPB, 0, s>>>(scal, fn, (uint32_t)count, c, 0, w0, Wp, ws.keys_in.as<uint16_t>());
     PIP_RET(hipMemsetAsync(ws.len[0].p, 0, nb * 4, s));
     PIP_RET(hipMemsetAsync(ws.maxlen.p, 0, sizeof(unsigned), s));
     const uint32_t tpw = (uint32_t)((n + HIST_TILE - 1) / HIST_TILE);
-    k_pip_hist<<<(unsigned)(W * tpw), PTPB, NB * 4, s>>>(ws.keys_in.as<uint16_t>(), (uint32_t)n, c, tpw,
-                                                          ws.len[0].as<uint32_t>());
+    if (k32)
+        k_pip_hist<uint32_t><<<(unsigned)(W * tpw), PTPB, NB * 4, s>>>(ws.keys_in.as<uint32_t>(), (uint32_t)n, c, ib,
+                                                                       tpw, ws.len[0].as<uint32_t>());
+    else
+        k_pip_hist<uint16_t><<<(unsigned)(W * tpw), PTPB, NB * 4, s>>>(ws.keys_in.as<uint16_t>(), (uint32_t)n, c, 0,
+                                                                       tpw, ws.len[0].as<uint32_t>());
     // len[1] / off[1] are free until step 0: the transposed counts and their scan
     k_pip_len0<<<nb_of(nb), PTPB, 0, s>>>(ws.len[0].as<uint32_t>(), ws.pad[0].as<uint32_t>(), ws.len[1].as<uint32_t>(),
                                           nb, c, (uint32_t)W, ws.maxlen.as<unsigned>());
@@ -529,10 +569,18 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
     k_pip_start<<<nb_of(nb), PTPB, 0, s>>>(ws.off[1].as<uint32_t>(), nb, c, (uint32_t)W, ws.start.as<uint32_t>());
     PIP_RET(hipcub::DeviceScan::ExclusiveSum(ws.temp.p, tb_scan, ws.pad[0].as<uint32_t>(), ws.off[0].as<uint32_t>(),
                                              (int)nb, s));
-    PIP_RET(pip_sort(ws.temp.p, tb_sort, ws.keys_in.as<uint16_t>(), ws.keys.as<uint16_t>(), ws.vals.as<uint32_t>(), N,
-                     kbits, s));
-    k_pip_bid0<<<nb_of(N), PTPB, 0, s>>>(ws.keys.as<uint16_t>(), ws.vals.as<uint32_t>(), N, fn, c,
-                                         ws.start.as<uint32_t>(), ws.off[0].as<uint32_t>(), ws.bid[0].as<uint32_t>());
+    if (k32) {
+        PIP_RET(pip_sort32(ws.temp.p, tb_sort, ws.keys_in.as<uint32_t>(), ws.keys.as<uint32_t>(), N, ib, c, s));
+        k_pip_bidfill<<<nb_of(nb * 64), PTPB, 0, s>>>(ws.len[0].as<uint32_t>(), ws.off[0].as<uint32_t>(), nb,
+                                                       ws.bid[0].as<uint32_t>());
+    } else {
+        PIP_RET(pip_sort(ws.temp.p, tb_sort, ws.keys_in.as<uint16_t>(), ws.keys.as<uint16_t>(), ws.vals.as<uint32_t>(),
+                         N, c, s));
+        k_pip_bid0<<<nb_of(N), PTPB, 0, s>>>(ws.keys.as<uint16_t>(), ws.vals.as<uint32_t>(), N, fn, c,
+                                             ws.start.as<uint32_t>(), ws.off[0].as<uint32_t>(), ws.bid[0].as<uint32_t>());
+    }
+    const uint32_t* keys32 = k32 ? ws.keys.as<uint32_t>() : nullptr;
+    const uint32_t imask = ib >= 32 ? 0xFFFFFFFFu : (uint32_t)((1ull << ib) - 1);
     // the worst-case step count (a bucket list is at most n long); steps past the depth of the
     // data exit on the device (pip_steps), so nothing here waits for the GPU
     int levels = 1;
@@ -549,7 +597,8 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
                                                 ws.part.as<uint32_t>());
         k_pip_scan_fin<<<nparts, PTPB, 0, s>>>(t, ws.maxlen.as<unsigned>(), ws.pad[b].as<uint32_t>(),
                                                ws.part.as<uint32_t>(), nb, ws.off[b].as<uint32_t>());
-        k_pip_step<<<nb_of(lanes), PTPB, 0, s>>>(t, ws.maxlen.as<unsigned>(), P, fn, ws.vals.as<uint32_t>(),
+        k_pip_step<<<nb_of(lanes), PTPB, 0, s>>>(t, ws.maxlen.as<unsigned>(), P, fn, keys32, imask,
+                                                  ws.vals.as<uint32_t>(),
                                                   ws.start.as<uint32_t>(), ws.Q[a].as<ge>(), ws.bid[a].as<uint32_t>(),
                                                   ws.off[a].as<uint32_t>(), ws.len[a].as<uint32_t>(),
                                                   ws.pad[a].as<uint32_t>(), ws.off[b].as<uint32_t>(), ws.Q[b].as<ge>(),

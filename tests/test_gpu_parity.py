@@ -779,6 +779,29 @@ def test_msm_pippenger_batch_vs_oracle(bp, oracle, n, count, c):
         assert np.array_equal(got[m], oracle.msm_pippenger(s[m * n:(m + 1) * n], P, c)), m
 
 
+def test_msm_pippenger_key_paths_agree(bp, oracle, monkeypatch):
+    """The 32-bit-key sort (digit << ib | i, c + ib <= 32) and the 16-bit-key sort with
+    counting-iterator values (forced by HIPBP_PIP_KEYS16=1; the path for larger n) give the same
+    bits: single and batched calls, n % 4 == 0 and not, a crowded bucket per window."""
+    import torch
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    for n, count, c in [(5000, 1, 12), (4097, 3, 8), (70000, 2, 12)]:
+        rng = np.random.default_rng(n + c)
+        P = oracle.base_points(n, 40)
+        s = rand_fe(rng, count * n)
+        s[::9] = s[0]
+        outs = []
+        for force in ("0", "1"):
+            monkeypatch.setenv("HIPBP_PIP_KEYS16", force)
+            out = torch.zeros(count, 16, dtype=torch.int64, device=dev)
+            bp.msm_pippenger_batch(out, T(s), T(P), c)
+            torch.cuda.synchronize()
+            outs.append(out.cpu().numpy().view(np.uint64))
+        assert np.array_equal(outs[0], outs[1]), (n, count, c)
+        assert np.array_equal(outs[0][0], oracle.msm_pippenger(s[:n], P, c)), (n, count, c)
+
+
 def test_msm_pippenger_rejects_bad_window(bp):
     import torch
     dev = torch.device("cuda:0")

@@ -5,7 +5,8 @@ import sqlite3
 import sys
 
 c = sqlite3.connect(sys.argv[1])
-rows = list(c.execute("select name, start, end, grid_x, stream_id, queue_id from kernels order by start"))
+rows = [(r[0].replace("(anonymous namespace)::", ""),) + tuple(r[1:]) for r in
+        c.execute("select name, start, end, grid_x, stream_id, queue_id from kernels order by start")]
 tot = {}
 for r in rows:
     k = r[0].split("(")[0]
