@@ -74,21 +74,30 @@ __global__ __launch_bounds__(PTPB) void k_pip_keys(const fe* __restrict__ s, Fas
     const uint32_t n = fn.d, g = (blockIdx.x * PTPB + threadIdx.x) * V;
     if (g >= count * n) return;
     const uint32_t m = fdiv(g, fn), i = g - m * n;
+    // each scalar as a 256-bit shift register, shifted right by c per window (a limb index that
+    // varies with the window would put the scalars in scratch)
     fe sc[V];
 #pragma unroll
     for (int u = 0; u < V; u++) sc[u] = s[g + u];
+    auto shr = [&](fe& x) {
+        x.v[0] = (x.v[0] >> c) | (x.v[1] << (64 - c));
+        x.v[1] = (x.v[1] >> c) | (x.v[2] << (64 - c));
+        x.v[2] = (x.v[2] >> c) | (x.v[3] << (64 - c));
+        x.v[3] >>= c;
+    };
+    for (int k = 0; k < w0; k++)
+#pragma unroll
+        for (int u = 0; u < V; u++) shr(sc[u]);
     const uint64_t mask = (1ull << c) - 1;
     KT* out = keys + (size_t)m * Wp * n + i;
     for (int lw = 0; lw < Wp; lw++) {
-        // bits [lo, lo + c) of the 256-bit scalar (a window may straddle two limbs or end past bit 255)
-        const int lo = c * (w0 + lw), li = lo >> 6, sh = lo & 63;
+        // bits [c (w0 + lw), + c) of the 256-bit scalar (zeros past bit 255)
         uint32_t d[V];
 #pragma unroll
         for (int u = 0; u < V; u++) {
-            uint64_t x = sc[u].v[li] >> sh;
-            if (sh && li < 3) x |= sc[u].v[li + 1] << (64 - sh);
-            d[u] = (uint32_t)(x & mask);
+            d[u] = (uint32_t)(sc[u].v[0] & mask);
             if constexpr (sizeof(KT) == 4) d[u] = (d[u] << ib) | (i + u);
+            shr(sc[u]);
         }
         KT* o = out + (size_t)lw * n;
         if constexpr (V == 4 && sizeof(KT) == 2) {
@@ -132,13 +141,14 @@ __global__ __launch_bounds__(PTPB) void k_pip_hist(const KT* __restrict__ keys, 
 // longest list (one atomic per wave), and the counts in sorted order — digit-major, virtual
 // window minor — whose exclusive scan is each bucket's start in the sorted array.
 __global__ __launch_bounds__(PTPB) void k_pip_len0(const uint32_t* __restrict__ len, uint32_t* pad, uint32_t* cnt_t,
-                                                  size_t nb, int c, uint32_t Wv, unsigned* maxlen) {
+                                                  size_t nb, int c, uint32_t Wv, unsigned* maxlen, ge* S) {
     const size_t b = (size_t)blockIdx.x * PTPB + threadIdx.x;
     uint32_t L = 0;
     if (b < nb) {
         L = len[b];
         pad[b] = (L + 3) & ~3u;
         cnt_t[(b & ((1u << c) - 1)) * Wv + (b >> c)] = L;
+        if (!L) S[b] = ge_zero();   // an empty bucket's sum (the steps write every other one)
     }
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) {
@@ -192,7 +202,8 @@ __global__ __launch_bounds__(PTPB) void k_pip_scan_part(int t, const unsigned* _
     for (int k = 0; k < SCAN_PER; k++) {
         const size_t b = b0 + k;
         if (b < nb) {
-            const uint32_t L = (len[b] + 3) >> 2, pd = (L + 3) & ~3u;
+            // a list of <= 4 is finished by this step (its sum goes to S[b]): no next-layout slots
+            const uint32_t L = len[b] <= 4 ? 0u : (len[b] + 3) >> 2, pd = (L + 3) & ~3u;
             len2[b] = L;
             pad2[b] = pd;
             sum += pd;
@@ -259,14 +270,15 @@ __global__ __launch_bounds__(PTPB) void k_pip_bidfill(const uint32_t* __restrict
     for (uint32_t j = threadIdx.x & 63; j < L; j += 64) bid[o + j] = (uint32_t)b;
 }
 
-__global__ __launch_bounds__(PTPB) void k_pip_step(int t, const unsigned* __restrict__ maxlen, const ge* __restrict__ P,
+// (min 4 waves per SIMD: the compiler keeps it at 128 VGPRs)
+__global__ __launch_bounds__(PTPB, 4) void k_pip_step(int t, const unsigned* __restrict__ maxlen, const ge* __restrict__ P,
                                                   FastDiv fn, const uint32_t* __restrict__ keys32, uint32_t imask,
                                                   const uint32_t* __restrict__ vals,
                                                   const uint32_t* __restrict__ start, const ge* __restrict__ Qin,
                                                   const uint32_t* __restrict__ bid, const uint32_t* __restrict__ off,
                                                   const uint32_t* __restrict__ len, const uint32_t* __restrict__ pad,
                                                   const uint32_t* __restrict__ off2, ge* Qout, uint32_t* bid2,
-                                                  size_t nb, size_t lanes) {
+                                                  ge* S, size_t nb, size_t lanes) {
     const size_t k = (size_t)blockIdx.x * PTPB + threadIdx.x;
     if (k >= lanes || t >= pip_steps(maxlen)) return;
     const bool first = t == 0;
@@ -296,15 +308,13 @@ __global__ __launch_bounds__(PTPB) void k_pip_step(int t, const unsigned* __rest
         if (r > 3) y1 = add_in(y1, load(3));
         y0 = ge_add(y0, y1);
     }
-    const uint32_t o = off2[b] + j / 4;
-    Qout[o] = y0;
-    bid2[o] = b;
+    // a group that is the whole list holds the bucket's sum (the bucket leaves the next layout)
+    const bool fin = L <= 4;
+    const uint32_t o = fin ? 0u : off2[b] + j / 4;
+    *(fin ? &S[b] : &Qout[o]) = y0;
+    if (!fin) bid2[o] = b;
 }
 
-__device__ __forceinline__ ge bucket_sum(const ge* __restrict__ Q, const uint32_t* __restrict__ off,
-                                         const uint32_t* __restrict__ cnt, size_t b) {
-    return cnt[b] ? Q[off[b]] : ge_zero();
-}
 
 // one block per (virtual) window v = m Wp + lw: pairwise tree over its NC <= PTPB chunk values, in
 // LDS, into Sw[m W + w0 + lw] (MSM m's window sums, absolute window index)
@@ -418,26 +428,19 @@ __device__ __forceinline__ ge ge_row_move(const ge& a) {
 // quad B walks S one step behind, fed each new R over DPP — both quads run the same point add in
 // lockstep on their own operands, 15 dependent adds instead of 29.  (kM) R is
 // ge25519_scalarmult's double-and-add on the scalar's raw bits, leading zeros from dtab.
-__global__ __launch_bounds__(PTPB) void k_pip_chunks(const ge* __restrict__ Q0, const ge* __restrict__ Q1,
-                                                    const uint32_t* __restrict__ off0, const uint32_t* __restrict__ off1,
-                                                    const uint32_t* __restrict__ cnt0, const uint32_t* __restrict__ cnt1,
-                                                    const unsigned* __restrict__ maxlen, int c, int W, ge* V,
+__global__ __launch_bounds__(PTPB) void k_pip_chunks(const ge* __restrict__ Sb, int c, int W, ge* V,
                                                     const ge* __restrict__ dtab) {
-    // after the last step every non-empty bucket holds its sum on side (steps & 1)
-    const bool f1 = (pip_steps(maxlen) & 1) != 0;
-    const ge* __restrict__ Q = f1 ? Q1 : Q0;
-    const uint32_t* __restrict__ off = f1 ? off1 : off0;
-    const uint32_t* __restrict__ cnt = f1 ? cnt1 : cnt0;
+    // Sb[b]: every bucket's sum (written by the step that finished it; empty buckets: ge25519_0)
     const size_t NB = (size_t)1 << c, NC = NB / PM;
     const size_t g = ((size_t)blockIdx.x * PTPB + threadIdx.x) >> 3;
     if (g >= (size_t)W * NC) return;   // whole octets leave together
     const bool qB = (threadIdx.x & 4) != 0;
     const size_t w = g / NC, k = g % NC, b0 = w * NB + k * PM;
-    ge X = bucket_sum(Q, off, cnt, b0 + PM - 1);   // A: R = B_{M-1}; B: S = B_{M-1}
+    ge X = Sb[b0 + PM - 1];   // A: R = B_{M-1}; B: S = B_{M-1}
     ge Rin = X;
     for (int j = PM - 2; j >= 0; j--) {
         // A: R_j = R_{j+1} + B_j (j = 0: the final R + B_0);  B: S = S + R_{j+1} (from j = M-3 on)
-        const ge y = qB ? Rin : bucket_sum(Q, off, cnt, b0 + j);
+        const ge y = qB ? Rin : Sb[b0 + j];
         const ge res = ge_op_quad<false>(X, y);
         if (!qB || j < PM - 2) X = res;
         Rin = ge_row_move<0x114>(X);   // quad B takes quad A's new R
@@ -474,7 +477,7 @@ struct DBuf {
     template <typename T> T* as() const { return (T*)p; }
 };
 struct PipWs {
-    DBuf keys_in, keys, vals, temp, start, len[2], pad[2], off[2], bid[2], Q[2], V, Sw, Tmid, maxlen, part;
+    DBuf keys_in, keys, vals, temp, start, len[2], pad[2], off[2], bid[2], Q[2], S, V, Sw, Tmid, maxlen, part;
     hipStream_t side = nullptr;           // the Horner chain's stream
     hipEvent_t ev[4] = {};   // [1] top half's buckets done, [2] bottom half done, [3] chain done
 };
@@ -509,7 +512,7 @@ static bool pip_force16() {
     return e && e[0] == '1';
 }
 
-// Bucket sums of windows [w0, w1) on stream s (they end on ping-pong side pip_steps & 1).
+// Bucket sums of windows [w0, w1) on stream s, into ws.S (the step that finishes a list writes it).
 static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, size_t count, int c, int w0, int w1,
                               hipStream_t s) {
     const int Wp = w1 - w0;
@@ -530,6 +533,7 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
     PIP_RET(ws.bid[0].need(tot0 * 4)); PIP_RET(ws.bid[1].need(qcap * 4));
     PIP_RET(ws.Q[0].need(qcap * sizeof(ge))); PIP_RET(ws.Q[1].need(qcap * sizeof(ge)));
     PIP_RET(ws.V.need((size_t)W * NC * sizeof(ge)));
+    PIP_RET(ws.S.need(nb * sizeof(ge)));
     PIP_RET(ws.maxlen.need(sizeof(unsigned)));
     size_t tb_sort = 0, tb_scan = 0;
     if (k32)
@@ -564,7 +568,7 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
                                                                        tpw, ws.len[0].as<uint32_t>());
     // len[1] / off[1] are free until step 0: the transposed counts and their scan
     k_pip_len0<<<nb_of(nb), PTPB, 0, s>>>(ws.len[0].as<uint32_t>(), ws.pad[0].as<uint32_t>(), ws.len[1].as<uint32_t>(),
-                                          nb, c, (uint32_t)W, ws.maxlen.as<unsigned>());
+                                          nb, c, (uint32_t)W, ws.maxlen.as<unsigned>(), ws.S.as<ge>());
     PIP_RET(hipcub::DeviceScan::ExclusiveSum(ws.temp.p, tb_scan, ws.len[1].as<uint32_t>(), ws.off[1].as<uint32_t>(),
                                              (int)nb, s));
     k_pip_start<<<nb_of(nb), PTPB, 0, s>>>(ws.off[1].as<uint32_t>(), nb, c, (uint32_t)W, ws.start.as<uint32_t>());
@@ -603,7 +607,7 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
                                                   ws.start.as<uint32_t>(), ws.Q[a].as<ge>(), ws.bid[a].as<uint32_t>(),
                                                   ws.off[a].as<uint32_t>(), ws.len[a].as<uint32_t>(),
                                                   ws.pad[a].as<uint32_t>(), ws.off[b].as<uint32_t>(), ws.Q[b].as<ge>(),
-                                                  ws.bid[b].as<uint32_t>(), nb, lanes);
+                                                  ws.bid[b].as<uint32_t>(), ws.S.as<ge>(), nb, lanes);
         lanes = lanes / 4 + nb;
     }
     return hipGetLastError();
@@ -614,10 +618,7 @@ static hipError_t pip_finish(PipWs& ws, size_t count, int c, int Wtot, int w0, i
                              hipStream_t s) {
     const int Wp = w1 - w0, W = Wp * (int)count;
     const size_t NC = ((size_t)1 << c) / PM;
-    k_pip_chunks<<<nb_of(8 * (size_t)W * NC), PTPB, 0, s>>>(ws.Q[0].as<ge>(), ws.Q[1].as<ge>(), ws.off[0].as<uint32_t>(),
-                                                         ws.off[1].as<uint32_t>(), ws.len[0].as<uint32_t>(),
-                                                         ws.len[1].as<uint32_t>(), ws.maxlen.as<unsigned>(), c, W,
-                                                         ws.V.as<ge>(), dtab);
+    k_pip_chunks<<<nb_of(8 * (size_t)W * NC), PTPB, 0, s>>>(ws.S.as<ge>(), c, W, ws.V.as<ge>(), dtab);
     k_pip_window<<<W, PTPB, 0, s>>>(ws.V.as<ge>(), (int)NC, Wp, Wtot, w0, Sw);
     return hipGetLastError();
 }
