@@ -712,7 +712,8 @@ def test_sq_matches_mul(bp, oracle):
 
 # ----------------------------------------------------------------------------- Pippenger (labelled alternative)
 @pytest.mark.parametrize("n,c", [(1, 12), (2, 4), (17, 12), (300, 12), (1000, 8), (777, 4), (20000, 8), (4096, 12),
-                                 (70000, 8)])   # n > 65536: several histogram tiles per window
+                                 (70000, 8),    # n > 65536: several histogram tiles per window
+                                 (999, 5), (2048, 7), (3001, 11)])   # odd widths: partial top windows
 def test_msm_pippenger_vs_oracle(bp, oracle, n, c):
     """hipbp_msm_pippenger == orc_msm_pippenger (the bucket algorithm restated in C): zero and short
     scalars (empty / crowded buckets), odd bucket sizes, every window width class."""
