@@ -109,8 +109,8 @@ EXPORTS = [
     "cuda_benchmark_multi_scalar_mul", "cuda_benchmark_inner_product", "cuda_benchmark_field_operations",
     "cuda_benchmark_range_proof", "hipbp_last_error", "hipbp_device_count", "hipbp_batch_range_proof_verify",
     "hipbp_batch_range_proof_verify_std", "hipbp_batch_inner_product_verify", "hipbp_batch_generate_range_proof", "hipbp_msm",
-    "hipbp_msm_pippenger", "hipbp_msm_pippenger_batch", "hipbp_msm_batch",
-    "hipbp_point_tree", "hipbp_field_op", "hipbp_sync", "hipbp_timing_enable",
+    "hipbp_msm_pippenger", "hipbp_msm_pippenger_batch", "hipbp_msm_pippenger_windows",
+    "hipbp_msm_pippenger_horner", "hipbp_msm_batch", "hipbp_point_tree", "hipbp_field_op", "hipbp_sync", "hipbp_timing_enable",
     "hipbp_timing_collect", "hipbp_kernel_count", "hipbp_kernel_name", "hipbp_pipeline_create",
     "hipbp_pipeline_push", "hipbp_pipeline_flush", "hipbp_pipeline_depth", "hipbp_pipeline_destroy",
 ]
@@ -136,8 +136,8 @@ def lib():
         for f in ("hipbp_batch_range_proof_verify", "hipbp_batch_range_proof_verify_host",
                   "hipbp_batch_range_proof_verify_std",
                   "hipbp_batch_inner_product_verify", "hipbp_batch_generate_range_proof", "hipbp_msm",
-                  "hipbp_msm_pippenger", "hipbp_msm_pippenger_batch", "hipbp_msm_batch",
-                  "hipbp_point_tree",
+                  "hipbp_msm_pippenger", "hipbp_msm_pippenger_batch", "hipbp_msm_pippenger_windows",
+                  "hipbp_msm_pippenger_horner", "hipbp_msm_batch", "hipbp_point_tree",
                   "hipbp_field_op", "hipbp_sync", "hipbp_device_count"):
             getattr(L, f).restype = ctypes.c_int
         _lib = L
@@ -489,6 +489,33 @@ def msm_pippenger_batch(results, scalars, points, window_bits=12, stream=None):
         raise BulletproofError("msm_pippenger_batch: scalars must hold count * n rows")
     _chk(lib().hipbp_msm_pippenger_batch(_c(results.data_ptr()), _c(scalars.data_ptr()), _c(points.data_ptr()),
                                          _sz(n), _sz(count), ctypes.c_int(window_bits), _stream_ptr(stream)))
+
+
+def pippenger_num_windows(window_bits=12):
+    return (256 + int(window_bits) - 1) // int(window_bits)
+
+
+def msm_pippenger_windows(window_sums, scalars, points, w_begin, w_end, window_bits=12, stream=None):
+    """Window sums S_w, w in [w_begin, w_end), of the Pippenger MSM into window_sums[w] (a (W,16)
+    device tensor, W = pippenger_num_windows; other rows untouched)."""
+    W = pippenger_num_windows(window_bits)
+    if window_sums.numel() != W * 16:
+        raise BulletproofError(f"msm_pippenger_windows: window_sums must be ({W}, 16)")
+    if scalars.numel() != points.shape[0] * 4:
+        raise BulletproofError("msm_pippenger_windows: one scalar per point")
+    _chk(lib().hipbp_msm_pippenger_windows(_c(window_sums.data_ptr()), _c(scalars.data_ptr()),
+                                           _c(points.data_ptr()), _sz(points.shape[0]), ctypes.c_int(window_bits),
+                                           ctypes.c_int(w_begin), ctypes.c_int(w_end), _stream_ptr(stream)))
+
+
+def msm_pippenger_horner(results, window_sums, window_bits=12, stream=None):
+    """Horner over all W window sums: results (count,16) or (16,), window_sums (count*W,16)."""
+    W = pippenger_num_windows(window_bits)
+    count = results.numel() // 16
+    if window_sums.numel() != count * W * 16:
+        raise BulletproofError(f"msm_pippenger_horner: window_sums must hold count * {W} rows")
+    _chk(lib().hipbp_msm_pippenger_horner(_c(results.data_ptr()), _c(window_sums.data_ptr()), _sz(count),
+                                          ctypes.c_int(window_bits), _stream_ptr(stream)))
 
 
 def point_tree(result, points, stream=None):

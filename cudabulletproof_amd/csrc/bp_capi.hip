@@ -832,6 +832,38 @@ int hipbp_msm_pippenger(ge25519* result, const fe25519* scalars, const ge25519* 
     return hipbp_msm_pippenger_batch(result, scalars, points, n, 1, window_bits, stream);
 }
 
+int hipbp_msm_pippenger_windows(ge25519* window_sums, const fe25519* scalars, const ge25519* points, size_t n,
+                                int window_bits, int w_begin, int w_end, void* stream) {
+    hipError_t err;
+    Engine* e = engine_or_null(&err);
+    BP_RET_ON(err);
+    if (window_bits < 4 || window_bits > 12) { g_err = "pippenger: window_bits must be 4..12"; return HIPBP_ERR_ARG; }
+    const int W = (256 + window_bits - 1) / window_bits;
+    if (w_begin < 0 || w_end > W || w_begin > w_end) { g_err = "pippenger_windows: need 0 <= w_begin <= w_end <= W"; return HIPBP_ERR_ARG; }
+    if (n == 0 || w_begin == w_end) return HIPBP_OK;
+    if (!window_sums || !scalars || !points) { g_err = "null argument"; return HIPBP_ERR_ARG; }
+    if (n * (size_t)(w_end - w_begin) > 0x7FFFFFFFull) { g_err = "pippenger: n * windows too large"; return HIPBP_ERR_ARG; }
+    std::lock_guard<std::mutex> lk(e->mu);
+    BP_RET_ON(bp::msm_pippenger_windows((bp::ge*)window_sums, (const bp::fe*)scalars, (const bp::ge*)points, n,
+                                        window_bits, w_begin, w_end, e->dtab, pick(stream, *e)));
+    return HIPBP_OK;
+}
+
+int hipbp_msm_pippenger_horner(ge25519* results, const ge25519* window_sums, size_t count, int window_bits,
+                               void* stream) {
+    hipError_t err;
+    Engine* e = engine_or_null(&err);
+    BP_RET_ON(err);
+    if (window_bits < 4 || window_bits > 12) { g_err = "pippenger: window_bits must be 4..12"; return HIPBP_ERR_ARG; }
+    if (count == 0) return HIPBP_OK;
+    if (!results || !window_sums) { g_err = "null argument"; return HIPBP_ERR_ARG; }
+    if (count > 0xFFFFu) { g_err = "pippenger_horner: count <= 65535"; return HIPBP_ERR_ARG; }
+    std::lock_guard<std::mutex> lk(e->mu);
+    BP_RET_ON(bp::pippenger_horner((bp::ge*)results, (const bp::ge*)window_sums, count, window_bits,
+                                   pick(stream, *e)));
+    return HIPBP_OK;
+}
+
 static int prove_run(const hipbp_prove_input* in, const ge25519* G, const ge25519* H, const ge25519* g,
                      const ge25519* h, const bp::ge* ptab, int pbits, hipbp_proof_out* out, void* stream) {
     hipError_t err;

@@ -186,6 +186,9 @@ void launch_ops_scan(unsigned* bins, int longest_first, hipStream_t s);   // bin
 // count MSMs over the same n points: results[m] = MSM(scal[m n .. m n + n), P)
 hipError_t msm_pippenger(ge* result, const fe* scal, const ge* P, size_t n, size_t count, int c, const ge* dtab,
                          hipStream_t s);
+hipError_t msm_pippenger_windows(ge* Sw, const fe* scal, const ge* P, size_t n, int c, int w0, int w1,
+                                 const ge* dtab, hipStream_t s);
+hipError_t pippenger_horner(ge* result, const ge* Sw, size_t count, int c, hipStream_t s);
 
 
 

@@ -688,4 +688,26 @@ hipError_t msm_pippenger(ge* result, const fe* scal, const ge* P, size_t n, size
     return hipSuccess;
 }
 
+// Window sums of windows [w0, w1) of one MSM into Sw[w0 .. w1) (entries outside untouched), all on
+// stream s: the same keys, sort, bucket trees, chunks and window trees as msm_pippenger's parts,
+// so each S_w has the bits the single call forms.  A multi-GPU MSM gives each rank a window range
+// and exchanges the 128-byte sums (cudabulletproof_amd/shard.py sharded_msm_pippenger).
+hipError_t msm_pippenger_windows(ge* Sw, const fe* scal, const ge* P, size_t n, int c, int w0, int w1,
+                                 const ge* dtab, hipStream_t s) {
+    const int W = (256 + c - 1) / c;
+    if (n == 0 || w0 >= w1 || w0 < 0 || w1 > W) return hipSuccess;
+    PipPair* pp = nullptr;
+    PIP_RET(pip_pair(&pp, s));
+    PIP_RET(pip_buckets(pp->lo, scal, P, n, 1, c, w0, w1, s));
+    return pip_finish(pp->lo, 1, c, W, w0, w1, Sw, dtab, s);
+}
+
+// Horner over all W window sums of `count` MSMs (Sw[m W .. m W + W)), on stream s.
+hipError_t pippenger_horner(ge* result, const ge* Sw, size_t count, int c, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    const int W = (256 + c - 1) / c;
+    k_pip_horner<<<(unsigned)count, 64, 0, s>>>(Sw, W, W - 1, 0, c, nullptr, result);
+    return hipGetLastError();
+}
+
 }  // namespace bp

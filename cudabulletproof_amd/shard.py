@@ -12,6 +12,12 @@ torch.distributed ("nccl" = RCCL on ROCm) for the few bytes that cross GPUs.
   rank is bit-exact with the single-GPU MSM.  RCCL has no point-add reduction op, hence
   all_gather + tree rather than all_reduce.
 
+* One large Pippenger MSM (the labelled alternative, BASELINE configs[2]'s window 12): its windows
+  are independent until the final Horner chain, so each rank forms the window sums S_w of a
+  contiguous window range over ALL points, the 128-byte sums meet in one all_gather (RCCL cannot
+  add points, so no all_reduce), and every rank runs the Horner over the W sums: bit-exact with
+  the single-GPU ``msm_pippenger``, whose windows are formed the same way.
+
 The compute callables default to the HIP kernels (``msm`` / ``point_tree`` of this package);
 the CPU gloo tests (tests/test_shard.py) pass CPU checkers in their place to test the host logic.
 """
@@ -97,3 +103,54 @@ def gather_verdicts(ok_local, total, group=None):
     dist.all_gather(allb, buf, group=group)
     parts = [allb[r][:shard_bounds(total, world, r)[1] - shard_bounds(total, world, r)[0]] for r in range(world)]
     return torch.cat(parts)
+
+
+def pippenger_window_bounds(window_bits, world, rank):
+    """Contiguous window range [w0, w1) of rank `rank` (W = ceil(256 / window_bits) windows)."""
+    return shard_bounds((256 + int(window_bits) - 1) // int(window_bits), world, rank)
+
+
+def _hip_windows(scalars, points, w0, w1, window_bits):
+    from . import msm_pippenger_windows, pippenger_num_windows
+    W = pippenger_num_windows(window_bits)
+    Sw = torch.zeros(W, 16, dtype=torch.int64, device=points.device)
+    msm_pippenger_windows(Sw, scalars, points, w0, w1, window_bits)
+    return Sw[w0:w1]
+
+
+def _hip_horner(Sw, window_bits):
+    from . import msm_pippenger_horner
+    out = torch.zeros(16, dtype=torch.int64, device=Sw.device)
+    msm_pippenger_horner(out, Sw.contiguous(), window_bits)
+    return out
+
+
+def sharded_msm_pippenger(scalars, points, window_bits=12, group=None, windows=None, horner=None):
+    """Pippenger MSM of all n points with its windows split over the ranks of `group`.
+
+    Every rank holds all scalars (n,4) and points (n,16).  Rank r forms the window sums of
+    pippenger_window_bounds(window_bits, world, r); one all_gather of (ceil(W / world), 16)
+    int64 rows per rank brings all W sums to every rank; each runs the Horner chain.  Returns
+    the (16,) int64 result on every rank, bit-exact with ``msm_pippenger`` on one GPU.
+    `windows(scalars, points, w0, w1, c) -> (w1 - w0, 16)` and `horner(Sw, c) -> (16,)` default
+    to the HIP kernels (the CPU tests pass their own checkers).
+    """
+    windows = windows or _hip_windows
+    horner = horner or _hip_horner
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    W = (256 + int(window_bits) - 1) // int(window_bits)
+    if points.shape[0] == 0 or scalars.shape[0] != points.shape[0]:
+        raise ValueError("sharded_msm_pippenger: need one scalar per point and n > 0")
+    w0, w1 = pippenger_window_bounds(window_bits, world, rank)
+    if world == 1:
+        return horner(windows(scalars, points, 0, W, window_bits), window_bits)
+    cap = pippenger_window_bounds(window_bits, world, 0)[1]
+    buf = torch.zeros(cap, 16, dtype=torch.int64, device=points.device)
+    if w1 > w0:
+        buf[:w1 - w0] = windows(scalars, points, w0, w1, window_bits)
+    parts = [torch.empty(cap, 16, dtype=torch.int64, device=points.device) for _ in range(world)]
+    dist.all_gather(parts, buf, group=group)
+    Sw = torch.cat([parts[r][:b - a] for r, (a, b) in
+                    enumerate(pippenger_window_bounds(window_bits, world, r) for r in range(world))])
+    return horner(Sw.contiguous(), window_bits)

@@ -260,6 +260,17 @@ int hipbp_msm_pippenger(ge25519* result, const fe25519* scalars, const ge25519* 
  * Horner launch serve all of them, so the latency-bound chains are shared.  count <= 65535. */
 int hipbp_msm_pippenger_batch(ge25519* results, const fe25519* scalars, const ge25519* points, size_t n,
                               size_t count, int window_bits, void* stream);
+/* The two halves of hipbp_msm_pippenger, for a multi-GPU MSM that splits the windows over the
+ * ranks (cudabulletproof_amd/shard.py sharded_msm_pippenger).  _windows writes the
+ * window sums S_w, w in [w_begin, w_end), into window_sums[w] (W = ceil(256 / window_bits)
+ * entries; the others are left untouched), each with the bits the single call forms; _horner
+ * runs the Horner chain over all W sums of each of count MSMs (window_sums[m W .. m W + W)), so
+ * every rank that holds all sums gets hipbp_msm_pippenger's result bit for bit.  Device buffers,
+ * asynchronous on `stream`. */
+int hipbp_msm_pippenger_windows(ge25519* window_sums, const fe25519* scalars, const ge25519* points, size_t n,
+                                int window_bits, int w_begin, int w_end, void* stream);
+int hipbp_msm_pippenger_horner(ge25519* results, const ge25519* window_sums, size_t count, int window_bits,
+                               void* stream);
 /* Canonical tree over n device points: for stride 1, 2, 4, ...: T[i] = Ndev(T[i] + T[i+stride])
  * for i % (2 stride) == 0 and i + stride < n; result = T[0] (the reduction half of
  * cuda_bulletproof_kernels.cu:45-115).  hipbp_msm = this tree over the per-point

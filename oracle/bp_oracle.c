@@ -328,17 +328,18 @@ static void tree_inplace(orc_ge* T, size_t n) {
     for (size_t st = 1; st < n; st *= 2)
         for (size_t i = 0; i + st < n; i += 2 * st) orc_ge_add(&T[i], &T[i], &T[i + st]);
 }
-void orc_msm_pippenger(orc_ge* r, const orc_fe* s, const orc_ge* P, size_t n, int c) {
-    const int W = (256 + c - 1) / c, M = 16;
+/* Window sums Sw[w0 .. w1) of the bucket MSM (a multi-GPU Pippenger splits the windows over the
+ * ranks: each rank forms its windows' sums, the ranks exchange them, every rank runs the Horner). */
+void orc_pippenger_windows(orc_ge* Sw, const orc_fe* s, const orc_ge* P, size_t n, int c, int w0, int w1) {
+    const int M = 16;
     const size_t NB = (size_t)1 << c, NC = NB / M;
     orc_ge* Bk = (orc_ge*)malloc(NB * sizeof(orc_ge));
     orc_ge* V = (orc_ge*)malloc(NC * sizeof(orc_ge));
-    orc_ge* Sw = (orc_ge*)malloc(W * sizeof(orc_ge));
     orc_ge* tmp = (orc_ge*)malloc((n ? n : 1) * sizeof(orc_ge));
     uint32_t* dig = (uint32_t*)malloc((n ? n : 1) * sizeof(uint32_t));
     size_t* cnt = (size_t*)malloc((NB + 1) * sizeof(size_t));
     size_t* pos = (size_t*)malloc(NB * sizeof(size_t));
-    for (int w = 0; w < W; w++) {
+    for (int w = w0; w < w1; w++) {
         for (size_t i = 0; i < n; i++) {
             int lo = c * w;
             uint32_t d = 0;
@@ -375,13 +376,26 @@ void orc_msm_pippenger(orc_ge* r, const orc_fe* s, const orc_ge* P, size_t n, in
         tree_inplace(V, NC);
         Sw[w] = V[0];
     }
+    free(Bk); free(V); free(tmp); free(dig); free(cnt); free(pos);
+}
+
+/* Horner over all W = ceil(256 / c) window sums, top window first: c doublings, then + S_w. */
+void orc_pippenger_horner(orc_ge* r, const orc_ge* Sw, int c) {
+    const int W = (256 + c - 1) / c;
     orc_ge T = Sw[W - 1];
     for (int w = W - 2; w >= 0; w--) {
         for (int d = 0; d < c; d++) orc_ge_add(&T, &T, &T);
         orc_ge_add(&T, &T, &Sw[w]);
     }
     *r = T;
-    free(Bk); free(V); free(Sw); free(tmp); free(dig); free(cnt); free(pos);
+}
+
+void orc_msm_pippenger(orc_ge* r, const orc_fe* s, const orc_ge* P, size_t n, int c) {
+    const int W = (256 + c - 1) / c;
+    orc_ge* Sw = (orc_ge*)malloc(W * sizeof(orc_ge));
+    orc_pippenger_windows(Sw, s, P, n, c, 0, W);
+    orc_pippenger_horner(r, Sw, c);
+    free(Sw);
 }
 
 /* bulletproof_vectors.cu:189-224 : sequential, host bytes and host normalize */

@@ -48,6 +48,8 @@ void orc_msm_cpu(orc_ge* r, const orc_fe* s, const orc_ge* P, size_t n);     /* 
  * double-and-add + the A9 tree, and this arithmetic is not associative).  The algorithm this
  * restates exactly (hipbp_msm_pippenger): see bp_oracle.c. */
 void orc_msm_pippenger(orc_ge* r, const orc_fe* s, const orc_ge* P, size_t n, int c);
+void orc_pippenger_windows(orc_ge* Sw, const orc_fe* s, const orc_ge* P, size_t n, int c, int w0, int w1);
+void orc_pippenger_horner(orc_ge* r, const orc_ge* Sw, int c);
 void orc_inner_product(orc_fe* r, const orc_fe* a, const orc_fe* b, size_t n); /* vectors.cu:101 */
 void orc_ip_gpu(orc_fe* r, const orc_fe* a, const orc_fe* b, size_t n);        /* cuda_inner_product.cu:97 */
 void orc_ip_gpu_shared(orc_fe* r, const orc_fe* a, const orc_fe* b, size_t n); /* cuda_inner_product.cu:185 */

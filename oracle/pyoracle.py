@@ -139,6 +139,23 @@ class Oracle(_Lib):
         self.f("msm_pippenger")(_p(r), _p(s), _p(P), _sz(len(P)), ctypes.c_int(c))
         return r
 
+    def pippenger_windows(self, s, P, c, w0, w1):
+        """Window sums S_w for w in [w0, w1) (rows 0 .. w1 - w0 - 1 of the result)."""
+        W = (256 + c - 1) // c
+        Sw = np.zeros((W, 16), np.uint64)
+        s = np.ascontiguousarray(s, np.uint64)
+        P = np.ascontiguousarray(P, np.uint64)
+        self.f("pippenger_windows")(_p(Sw), _p(s), _p(P), _sz(len(P)), ctypes.c_int(c), ctypes.c_int(w0),
+                                    ctypes.c_int(w1))
+        return Sw[w0:w1].copy()
+
+    def pippenger_horner(self, Sw, c):
+        r = ge()
+        Sw = np.ascontiguousarray(Sw, np.uint64).reshape(-1, 16)
+        assert len(Sw) == (256 + c - 1) // c
+        self.f("pippenger_horner")(_p(r), _p(Sw), ctypes.c_int(c))
+        return r
+
     def msm_cpu(self, s, P):
         r = ge()
         s = np.ascontiguousarray(s, np.uint64)

@@ -1,6 +1,7 @@
 """bench.py's N>1 path (torchrun, one process per rank) rehearsed on one GPU: every rank on cuda:0
 with gloo collectives (--rehearse).  The sharded MSM (shard roots + all_gather + canonical tree)
-must give the same point as the single-rank run, and the line must carry the N=2 fields."""
+and the window-sharded Pippenger (window sums + all_gather + Horner) must give the same points as
+the single-rank run, and the line must carry the N=2 fields."""
 import json
 import os
 import subprocess
@@ -36,6 +37,9 @@ def test_bench_two_ranks_rehearsal_matches_one_rank():
     assert l1["n_gpus"] == 1 and l2["n_gpus"] == 2
     assert l2["msm"]["scaling"] == "strong" and l2["scaling"] == "weak"
     assert l1["msm"]["result_sha256"] == l2["msm"]["result_sha256"]
+    # Pippenger with its windows split over the 2 ranks == the single-GPU Pippenger
+    ps = l2["msm"]["pippenger_sharded"]
+    assert ps["scaling"] == "strong" and ps["result_sha256"] == l1["msm"]["pippenger"]["result_sha256"]
     # configs[4]: the same proof set sharded over 1 or 2 ranks -> the same verdicts on every rank
     s1, s2 = l1["sharded_2p16"], l2["sharded_2p16"]
     assert s1["proofs"] == s2["proofs"] == 3000 and s2["scaling"] == "strong"

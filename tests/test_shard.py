@@ -145,3 +145,108 @@ def test_sharded_msm_emulated_ranks_match_single_gpu(bp, n, world):
     comb = shard._hip_tree(torch.stack(roots))
     torch.cuda.synchronize()
     assert np.array_equal(_np(comb), _np(full))
+
+
+# ---- window-sharded Pippenger (shard.sharded_msm_pippenger) ----
+
+@pytest.mark.parametrize("c", [4, 5, 8, 12])
+def test_pippenger_window_bounds_cover_every_window(c):
+    W = (256 + c - 1) // c
+    for world in (1, 2, 3, 8, W + 3):
+        spans = [shard.pippenger_window_bounds(c, world, r) for r in range(world)]
+        assert spans[0][0] == 0 and spans[-1][1] == W
+        assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+
+
+@pytest.mark.parametrize("n,c,splits", [(1, 4, [0, 64]), (37, 5, [0, 7, 30, 52]), (300, 8, [0, 1, 31, 32]),
+                                        (1000, 12, [0, 5, 11, 22])])
+def test_pippenger_windows_then_horner_is_the_msm(oracle, n, c, splits):
+    """Window sums formed in pieces + the Horner == orc_msm_pippenger (the split is exact)."""
+    s, P = _inputs(n, seed=21)
+    Sw = np.concatenate([oracle.pippenger_windows(s, P, c, a, b) for a, b in zip(splits, splits[1:])])
+    assert np.array_equal(oracle.pippenger_horner(Sw, c), oracle.msm_pippenger(s, P, c))
+
+
+def _oracle_pip_fns(O):
+    def windows(sc, P, w0, w1, c):
+        return torch.from_numpy(O.pippenger_windows(_np(sc), _np(P), c, w0, w1).view(np.int64))
+
+    def horner(Sw, c):
+        return torch.from_numpy(O.pippenger_horner(_np(Sw), c).view(np.int64))
+    return windows, horner
+
+
+def _pip_worker(rank, world, port, n, c, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import pyoracle
+        O = pyoracle.Oracle()
+        s, P = _inputs(n, seed=4)
+        windows, horner = _oracle_pip_fns(O)
+        r = shard.sharded_msm_pippenger(torch.from_numpy(s.view(np.int64)), torch.from_numpy(P.view(np.int64)), c,
+                                        windows=windows, horner=horner)
+        q.put((rank, _np(r).copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,c", [(2, 200, 8), (3, 64, 12), (2, 33, 5)])
+def test_gloo_sharded_pippenger(oracle, world, n, c):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pip_worker, args=(r, world, port, n, c, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    s, P = _inputs(n, seed=4)
+    want = oracle.msm_pippenger(s, P, c)
+    for rank, r in res:
+        assert np.array_equal(r, want), f"rank {rank}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,c,world", [(1, 12, 2), (1000, 8, 3), (5000, 12, 8), (70001, 12, 4), (4096, 5, 8)])
+def test_pippenger_windows_emulated_ranks_match_single_gpu(bp, oracle, n, c, world):
+    """Each emulated rank's window range (hipbp_msm_pippenger_windows) + one Horner launch ==
+    hipbp_msm_pippenger, and both == the oracle (small n)."""
+    dev = torch.device("cuda:0")
+    s, P = _inputs(n, seed=12)
+    sd, Pd = torch.from_numpy(s.view(np.int64)).to(dev), torch.from_numpy(P.view(np.int64)).to(dev)
+    full = torch.zeros(16, dtype=torch.int64, device=dev)
+    bp.msm_pippenger(full, sd, Pd, c)
+    W = bp.pippenger_num_windows(c)
+    Sw = torch.zeros(W, 16, dtype=torch.int64, device=dev)
+    for r in range(world):
+        w0, w1 = shard.pippenger_window_bounds(c, world, r)
+        bp.msm_pippenger_windows(Sw, sd, Pd, w0, w1, c)
+    out = torch.zeros(16, dtype=torch.int64, device=dev)
+    bp.msm_pippenger_horner(out, Sw, c)
+    one = shard.sharded_msm_pippenger(sd, Pd, c)   # world 1: all windows in one call
+    torch.cuda.synchronize()
+    assert np.array_equal(_np(out), _np(full)) and np.array_equal(_np(one), _np(full))
+    if n <= 5000:
+        assert np.array_equal(_np(out), oracle.msm_pippenger(s, P, c))
+        assert np.array_equal(_np(Sw)[2:4], oracle.pippenger_windows(s, P, c, 2, 4))
+
+
+@pytest.mark.gpu
+def test_pippenger_windows_argument_errors(bp):
+    dev = torch.device("cuda:0")
+    s, P = _inputs(8, seed=1)
+    sd, Pd = torch.from_numpy(s.view(np.int64)).to(dev), torch.from_numpy(P.view(np.int64)).to(dev)
+    Sw = torch.zeros(22, 16, dtype=torch.int64, device=dev)
+    for w0, w1 in ((-1, 3), (3, 23), (5, 4)):
+        with pytest.raises(bp.BulletproofError):
+            bp.msm_pippenger_windows(Sw, sd, Pd, w0, w1, 12)
+    with pytest.raises(bp.BulletproofError):
+        bp.msm_pippenger_windows(Sw, sd, Pd, 0, 3, 13)
+    with pytest.raises(bp.BulletproofError):
+        bp.msm_pippenger_horner(torch.zeros(16, dtype=torch.int64, device=dev), Sw[:21], 12)
+    bp.msm_pippenger_windows(Sw, sd, Pd, 4, 4, 12)   # empty range: nothing written
+    torch.cuda.synchronize()
+    assert int(Sw.abs().sum().item()) == 0
