@@ -316,7 +316,7 @@ def msm_leg(args, dev, world, rank, T):
                "unit": "points/s", "ms_per_msm": sdt * 1e3, "n_gpus": world, "scaling": "strong",
                "windows_rank0": [w0, w1], "result_sha256": sd,
                "matches_oracle_golden": (sd == gold["pippenger_w12"]["digest"]) if gold else None,
-               "collective": "one all_gather of ceil(W/N) x 128 B window sums per rank (RCCL), then the Horner "
+               "collective": "one all_gather of the largest window range x 128 B per rank (RCCL), then the Horner "
                              "chain on every rank (shard.sharded_msm_pippenger)"}
     return {"metric": "MSM points/sec", "value": nm / mdt, "unit": "points/s", "points": nm,
             "ms_per_msm": mdt * 1e3, "n_gpus": world, "scaling": "strong" if world > 1 else None,

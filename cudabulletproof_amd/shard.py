@@ -106,8 +106,27 @@ def gather_verdicts(ok_local, total, group=None):
 
 
 def pippenger_window_bounds(window_bits, world, rank):
-    """Contiguous window range [w0, w1) of rank `rank` (W = ceil(256 / window_bits) windows)."""
-    return shard_bounds((256 + int(window_bits) - 1) // int(window_bits), world, rank)
+    """Contiguous window range [w0, w1) of rank `rank` (W = ceil(256 / window_bits) windows).
+
+    Windows are split by cost, not count: a narrow top window (fewer than c/2 bits: 4 at c = 12,
+    3 for the 255-bit config-3 scalars) has few, deep buckets whose trees run latency-bound tail
+    steps, and costs about three ordinary windows (2^20 points, c = 12, one MI355X:
+    tools/pip_shard_probe.py).  Window w goes to rank floor(start_w * world / total), start_w =
+    the cost of the windows below it, so the ranges are contiguous and cover every window."""
+    c = int(window_bits)
+    W = (256 + c - 1) // c
+    top_bits = 256 - c * (W - 1)
+    cost = [1] * (W - 1) + [3 if 2 * top_bits < c else 1]
+    total = sum(cost)
+    owner, start = [], 0
+    for w in range(W):
+        owner.append(min(world - 1, start * world // total))
+        start += cost[w]
+    ws = [w for w in range(W) if owner[w] == rank]
+    if ws:
+        return ws[0], ws[-1] + 1
+    lo = next((w for w in range(W) if owner[w] > rank), W)   # empty range at its place in the order
+    return lo, lo
 
 
 def _hip_windows(scalars, points, w0, w1, window_bits):
@@ -129,7 +148,7 @@ def sharded_msm_pippenger(scalars, points, window_bits=12, group=None, windows=N
     """Pippenger MSM of all n points with its windows split over the ranks of `group`.
 
     Every rank holds all scalars (n,4) and points (n,16).  Rank r forms the window sums of
-    pippenger_window_bounds(window_bits, world, r); one all_gather of (ceil(W / world), 16)
+    pippenger_window_bounds(window_bits, world, r); one all_gather of (largest range, 16)
     int64 rows per rank brings all W sums to every rank; each runs the Horner chain.  Returns
     the (16,) int64 result on every rank, bit-exact with ``msm_pippenger`` on one GPU.
     `windows(scalars, points, w0, w1, c) -> (w1 - w0, 16)` and `horner(Sw, c) -> (16,)` default
@@ -145,12 +164,12 @@ def sharded_msm_pippenger(scalars, points, window_bits=12, group=None, windows=N
     w0, w1 = pippenger_window_bounds(window_bits, world, rank)
     if world == 1:
         return horner(windows(scalars, points, 0, W, window_bits), window_bits)
-    cap = pippenger_window_bounds(window_bits, world, 0)[1]
+    spans = [pippenger_window_bounds(window_bits, world, r) for r in range(world)]
+    cap = max(b - a for a, b in spans)
     buf = torch.zeros(cap, 16, dtype=torch.int64, device=points.device)
     if w1 > w0:
         buf[:w1 - w0] = windows(scalars, points, w0, w1, window_bits)
     parts = [torch.empty(cap, 16, dtype=torch.int64, device=points.device) for _ in range(world)]
     dist.all_gather(parts, buf, group=group)
-    Sw = torch.cat([parts[r][:b - a] for r, (a, b) in
-                    enumerate(pippenger_window_bounds(window_bits, world, r) for r in range(world))])
+    Sw = torch.cat([parts[r][:b - a] for r, (a, b) in enumerate(spans)])
     return horner(Sw.contiguous(), window_bits)
