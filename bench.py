@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--ipa-batch", type=int, default=64, help="IPA proofs per pipeline tick")
     ap.add_argument("--ipa-steps", type=int, default=4)
     ap.add_argument("--no-ipa", action="store_true")
+    ap.add_argument("--ipa-prefix-bits", type=int, default=14,
+                    help="configs[3]: fixed-base prefix tables of G/H for fold round 0 (0 = none)")
     ap.add_argument("--prove-batch", type=int, default=65536, help="proofs per generate_range_proof batch")
     ap.add_argument("--prove-steps", type=int, default=4)
     ap.add_argument("--prove-streams", type=int, default=2, help="HIP streams prover batches rotate over")
@@ -347,6 +349,15 @@ def ipa_leg(args, dev):
     streams = [torch.cuda.Stream(dev) for _ in range(npipe)]
     pipes = [bp.VerifyPipeline(B, n, Gd, Hd, Qd, range_mode=False, stream=st) for st in streams]
     pipe = pipes[0]
+    gens = None
+    if args.ipa_prefix_bits > 0:   # one table set shared by both pipelines (fold round 0 is on G, H)
+        t0 = time.perf_counter()
+        gens = bp.Generators(n, Gd, Hd, Qd, Qd, prefix_bits=args.ipa_prefix_bits)
+        for pp in pipes:
+            pp.use_gens(gens)
+        torch.cuda.synchronize(dev)
+        tables = {"bits": args.ipa_prefix_bits, "GB": gens.nbytes_tables() / 1e9,
+                  "build_s": time.perf_counter() - t0}
 
     def tick(k, with_P):   # P of batch k on its pipeline's stream (per-stream MSM workspaces), then the tick
         j = k % npipe
@@ -370,6 +381,8 @@ def ipa_leg(args, dev):
         torch.cuda.synchronize(dev)
     for pp in pipes:
         pp.close()
+    if gens is not None:
+        gens.close()
     sm = 4 * (n - 1) + 3   # fold rounds + a0*G', b0*H', c*Q (crv:160-296)
     dt = res[True]
     return {"metric": f"{n}-element inner-product-argument verifies/sec", "value": B * steps / dt,
@@ -377,7 +390,8 @@ def ipa_leg(args, dev):
             "scalar_mults_per_verify": sm + 2 * n, "scalar_mults_per_s": B * steps * (sm + 2 * n) / dt,
             "value_P_given": B * steps / res[False],
             "semantics": "P = canonical-tree MSM(a||b, G||H) (hipbp_msm_batch) + cuda_inner_product_verify "
-                         "(crv:130)", "pipeline_depth": pipe.depth}
+                         "(crv:130)", "pipeline_depth": pipe.depth,
+            "prefix_tables": tables if gens is not None else None}
 
 
 def shard_leg(args, dev, world, rank, pipes, gens, G, H, g, h):

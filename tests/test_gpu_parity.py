@@ -1135,3 +1135,35 @@ def test_gens_prover_and_pipeline_same_bits(bp, oracle, n, B, K):
     for a, b2 in zip(*res):
         assert torch.equal(a, b2)
     gens.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,B,K", [(64, 24, 6), (256, 8, 10), (4096, 4, 12)])
+def test_gens_inner_product_pipeline_same_bits(bp, oracle, n, B, K):
+    """Inner-product mode (cuda_inner_product_verify, bench configs[3]) on a generator set whose g and
+    h are both Q: fold round 0 on G/H starts from the prefix tables; verdicts and check points are
+    bit-identical to the table-free pipeline."""
+    import torch
+    from cudabulletproof_amd import synth
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+    _, h = oracle.gh()
+    Gd, Hd, Qd = T(G), T(H), T(h)
+    arrays = synth.proofs(B, n, seed=70 + K)
+    Pg = T(oracle.base_points(B, 9))
+    gens = bp.Generators(n, Gd, Hd, Qd, Qd, prefix_bits=K)
+    res = []
+    for use in (False, True):
+        pipe = bp.VerifyPipeline(B, n, Gd, Hd, Qd, range_mode=False)
+        if use:
+            pipe.use_gens(gens)
+        ok = torch.zeros(B, dtype=torch.uint8, device=dev)
+        chk = torch.zeros(B, 16, dtype=torch.int64, device=dev)
+        pipe.push(bp.RangeProofBatch.from_numpy(n, arrays, dev), ok, None, chk, P_in=Pg)
+        pipe.flush()
+        torch.cuda.synchronize()
+        res.append((ok.cpu(), chk.cpu()))
+        pipe.close()
+    gens.close()
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
