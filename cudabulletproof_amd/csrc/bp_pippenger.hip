@@ -316,16 +316,28 @@ __global__ __launch_bounds__(PTPB, 4) void k_pip_step(int t, const unsigned* __r
 }
 
 
+template <bool DBL>
+__device__ __forceinline__ ge ge_op_quad(const ge& p, const ge& q);
+
 // one block per (virtual) window v = m Wp + lw: pairwise tree over its NC <= PTPB chunk values, in
-// LDS, into Sw[m W + w0 + lw] (MSM m's window sums, absolute window index)
+// LDS, into Sw[m W + w0 + lw] (MSM m's window sums, absolute window index).  A latency-bound
+// chain of log2(NC) levels, so each add runs on a lane quad (ge_op_quad: the same products as
+// ge_add, 3 product latencies instead of 9); quad a of a level forms the pair a of that level.
 __global__ __launch_bounds__(PTPB) void k_pip_window(const ge* __restrict__ V, int NC, int Wp, int W, int w0, ge* Sw) {
     __shared__ ge sh[PTPB];
     const int t = threadIdx.x;
     if (t < NC) sh[t] = V[(size_t)blockIdx.x * NC + t];
     __syncthreads();
     for (int st = 1; st < NC; st <<= 1) {
-        if ((t % (2 * st)) == 0 && t + st < NC) sh[t] = ge_add(sh[t], sh[t + st]);
-        __syncthreads();
+        const int pairs = (NC - st + 2 * st - 1) / (2 * st);   // i = 2 st a with i + st < NC
+        for (int a0 = 0; a0 < pairs; a0 += PTPB / 4) {         // block-uniform trip count
+            const int a = a0 + (t >> 2);
+            if (a < pairs) {   // pairs of one level touch disjoint entries
+                const ge r = ge_op_quad<false>(sh[2 * st * a], sh[2 * st * a + st]);
+                if ((t & 3) == 0) sh[2 * st * a] = r;
+            }
+            __syncthreads();
+        }
     }
     if (t == 0) Sw[(size_t)(blockIdx.x / Wp) * W + w0 + blockIdx.x % Wp] = sh[0];
 }
