@@ -271,6 +271,16 @@ __global__ __launch_bounds__(PTPB) void k_pip_bidfill(const uint32_t* __restrict
 }
 
 // (min 4 waves per SIMD: the compiler keeps it at 128 VGPRs)
+template <bool DBL>
+__device__ __forceinline__ ge ge_op_quad(const ge& p, const ge& q);
+template <int CTRL>
+__device__ __forceinline__ ge ge_row_move(const ge& a);
+
+// Bucket-tree step: each lane reduces one aligned 4-element group of a bucket's list (2 levels).
+// When few groups remain (the deep buckets' tail steps, a wave-uniform test on the device-side
+// count), each group takes a lane octet instead: quads A and B add elements (0, 1) and (2, 3) side
+// by side on ge_op_quad, then A adds B's sum, moved over DPP: 2 point-op latencies instead of
+// 3 adds on one lane.  The same adds in the same order, so the same bits.
 __global__ __launch_bounds__(PTPB, 4) void k_pip_step(int t, const unsigned* __restrict__ maxlen, const ge* __restrict__ P,
                                                   FastDiv fn, const uint32_t* __restrict__ keys32, uint32_t imask,
                                                   const uint32_t* __restrict__ vals,
@@ -283,6 +293,38 @@ __global__ __launch_bounds__(PTPB, 4) void k_pip_step(int t, const unsigned* __r
     if (k >= lanes || t >= pip_steps(maxlen)) return;
     const bool first = t == 0;
     const uint32_t total = off[nb - 1] + pad[nb - 1];
+    const uint32_t groups = total >> 2;   // lists are padded to x4
+    const size_t oct_max = nb / 8 < 16384 ? nb / 8 : 16384;   // 8 groups' lanes <= nb <= grid lanes
+    if (groups <= oct_max) {
+        const uint32_t pos = (uint32_t)(4 * (k >> 3));
+        if (pos >= total) return;   // whole octets leave together
+        const uint32_t b = bid[pos];
+        const uint32_t j = pos - off[b], L = len[b];
+        const uint32_t r = L - j < 4 ? L - j : 4;
+        const size_t base = first ? (size_t)start[b] + j : (size_t)off[b] + j;
+        auto load = [&](uint32_t e) -> ge {
+            if (!first) return Qin[base + e];
+            if (keys32) return P[keys32[base + e] & imask];
+            const uint32_t g = vals[base + e];
+            return P[g - fdiv(g, fn) * fn.d];
+        };
+        const uint32_t e0 = (threadIdx.x & 4) ? 2u : 0u;   // quad A: elements 0, 1; quad B: 2, 3
+        const bool has0 = e0 < r, has1 = e0 + 1 < r;
+        const ge u = load(has0 ? e0 : 0u);
+        const ge v = has1 ? load(e0 + 1) : u;
+        ge sum = ge_op_quad<false>(u, v);   // computed on every quad; kept where the pair exists
+        if (!has1) sum = u;
+        const ge sB = ge_row_move<0x104>(sum);   // quad A takes quad B's sum
+        ge y = ge_op_quad<false>(sum, sB);
+        if (r <= 2) y = sum;
+        if ((threadIdx.x & 7) == 0) {
+            const bool fin = L <= 4;
+            const uint32_t o = fin ? 0u : off2[b] + j / 4;
+            *(fin ? &S[b] : &Qout[o]) = y;
+            if (!fin) bid2[o] = b;
+        }
+        return;
+    }
     const uint32_t pos = (uint32_t)(4 * k);
     if (pos >= total) return;
     const uint32_t b = bid[pos];
@@ -315,9 +357,6 @@ __global__ __launch_bounds__(PTPB, 4) void k_pip_step(int t, const unsigned* __r
     if (!fin) bid2[o] = b;
 }
 
-
-template <bool DBL>
-__device__ __forceinline__ ge ge_op_quad(const ge& p, const ge& q);
 
 // one block per (virtual) window v = m Wp + lw: pairwise tree over its NC <= PTPB chunk values, in
 // LDS, into Sw[m W + w0 + lw] (MSM m's window sums, absolute window index).  A latency-bound
