@@ -359,10 +359,21 @@ def ipa_leg(args, dev):
         tables = {"bits": args.ipa_prefix_bits, "GB": gens.nbytes_tables() / 1e9,
                   "build_s": time.perf_counter() - t0}
 
+    P_same = None
+    if gens is not None:   # the tables change no bits: P of batch 0 both ways, outside the timed region
+        pa, pb = torch.zeros_like(Ps[0]), torch.zeros_like(Ps[0])
+        bp.msm_batch(pa, wit[0], GH)
+        bp.msm_batch_gens(pb, wit[0], gens)
+        torch.cuda.synchronize(dev)
+        P_same = bool(torch.equal(pa, pb))
+
     def tick(k, with_P):   # P of batch k on its pipeline's stream (per-stream MSM workspaces), then the tick
         j = k % npipe
-        if with_P:
-            bp.msm_batch(Ps[k % nb], wit[k % nb], GH, stream=streams[j])
+        if with_P:   # over the generator set's G||H with its prefix tables when there is one (same bits)
+            if gens is not None:
+                bp.msm_batch_gens(Ps[k % nb], wit[k % nb], gens, stream=streams[j])
+            else:
+                bp.msm_batch(Ps[k % nb], wit[k % nb], GH, stream=streams[j])
         pipes[j].push(batches[k % nb], oks[k % nb], P_in=Ps[k % nb])
 
     res = {}
@@ -389,9 +400,9 @@ def ipa_leg(args, dev):
             "unit": "verifies/s", "batch": B, "n": n, "ms_per_tick": dt / steps * 1e3, "pipelines": npipe,
             "scalar_mults_per_verify": sm + 2 * n, "scalar_mults_per_s": B * steps * (sm + 2 * n) / dt,
             "value_P_given": B * steps / res[False],
-            "semantics": "P = canonical-tree MSM(a||b, G||H) (hipbp_msm_batch) + cuda_inner_product_verify "
+            "semantics": "P = canonical-tree MSM(a||b, G||H) (hipbp_msm_batch_gens) + cuda_inner_product_verify "
                          "(crv:130)", "pipeline_depth": pipe.depth,
-            "prefix_tables": tables if gens is not None else None}
+            "prefix_tables": tables if gens is not None else None, "P_tables_equal_plain": P_same}
 
 
 def shard_leg(args, dev, world, rank, pipes, gens, G, H, g, h):

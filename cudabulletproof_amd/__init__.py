@@ -110,7 +110,8 @@ EXPORTS = [
     "cuda_benchmark_range_proof", "hipbp_last_error", "hipbp_device_count", "hipbp_batch_range_proof_verify",
     "hipbp_batch_range_proof_verify_std", "hipbp_batch_inner_product_verify", "hipbp_batch_generate_range_proof", "hipbp_msm",
     "hipbp_msm_pippenger", "hipbp_msm_pippenger_batch", "hipbp_msm_pippenger_windows",
-    "hipbp_msm_pippenger_horner", "hipbp_msm_batch", "hipbp_point_tree", "hipbp_field_op", "hipbp_sync", "hipbp_timing_enable",
+    "hipbp_msm_pippenger_horner", "hipbp_msm_batch", "hipbp_msm_batch_gens", "hipbp_point_tree", "hipbp_field_op",
+    "hipbp_sync", "hipbp_timing_enable",
     "hipbp_timing_collect", "hipbp_kernel_count", "hipbp_kernel_name", "hipbp_pipeline_create",
     "hipbp_pipeline_push", "hipbp_pipeline_flush", "hipbp_pipeline_depth", "hipbp_pipeline_destroy",
 ]
@@ -137,7 +138,7 @@ def lib():
                   "hipbp_batch_range_proof_verify_std",
                   "hipbp_batch_inner_product_verify", "hipbp_batch_generate_range_proof", "hipbp_msm",
                   "hipbp_msm_pippenger", "hipbp_msm_pippenger_batch", "hipbp_msm_pippenger_windows",
-                  "hipbp_msm_pippenger_horner", "hipbp_msm_batch", "hipbp_point_tree",
+                  "hipbp_msm_pippenger_horner", "hipbp_msm_batch", "hipbp_msm_batch_gens", "hipbp_point_tree",
                   "hipbp_field_op", "hipbp_sync", "hipbp_device_count"):
             getattr(L, f).restype = ctypes.c_int
         _lib = L
@@ -472,6 +473,16 @@ def msm_batch(results, scalars, points, stream=None):
         raise BulletproofError("msm_batch: scalars must hold count * n rows")
     _chk(lib().hipbp_msm_batch(_c(results.data_ptr()), _c(scalars.data_ptr()), _c(points.data_ptr()), _sz(n),
                                _sz(count), _stream_ptr(stream)))
+
+
+def msm_batch_gens(results, scalars, gens, stream=None):
+    """msm_batch over a Generators set's G||H (2n points) with its prefix tables: results (count,16),
+    scalars (count*2n,4); the same bits as msm_batch(results, scalars, cat(G, H))."""
+    count, n2 = results.shape[0], 2 * gens.n
+    if scalars.numel() != count * n2 * 4:
+        raise BulletproofError("msm_batch_gens: scalars must hold count * 2n rows")
+    _chk(lib().hipbp_msm_batch_gens(_c(results.data_ptr()), _c(scalars.data_ptr()), _c(gens.h), _sz(count),
+                                    _stream_ptr(stream)))
 
 
 def msm_pippenger(result, scalars, points, window_bits=12, stream=None):

@@ -557,7 +557,7 @@ struct Pipeline {
 
 // `count` canonical-tree MSMs of n points each on stream s, in s's own workspace.
 hipError_t msm_run(Engine& e, bp::ge* results, const bp::fe* scalars, const bp::ge* points, size_t n, size_t count,
-                   hipStream_t s) {
+                   hipStream_t s, const bp::ge* ptab = nullptr, int K = 0) {
     const size_t tot = n * count, nb = count * ((n + 255) / 256);
     Buf* w = e.msm_bufs(s);
     hipError_t err;
@@ -567,7 +567,7 @@ hipError_t msm_run(Engine& e, bp::ge* results, const bp::fe* scalars, const bp::
     if ((err = w[5].need(tot * sizeof(uint32_t))) != hipSuccess) return err;
     if ((err = w[6].need(bp::MSM_BINS * sizeof(unsigned))) != hipSuccess) return err;
     bp::launch_msm_full(results, scalars, points, n, w[0].as<bp::ge>(), w[1].as<bp::ge>(), w[2].as<bp::ge>(),
-                        w[5].as<uint32_t>(), w[6].as<unsigned>(), e.dtab, s, count);
+                        w[5].as<uint32_t>(), w[6].as<unsigned>(), e.dtab, s, count, ptab, K);
     return hipGetLastError();
 }
 
@@ -805,6 +805,25 @@ int hipbp_msm_batch(ge25519* results, const fe25519* scalars, const ge25519* poi
     std::lock_guard<std::mutex> lk(e->mu);
     hipStream_t s = pick(stream, *e);
     BP_RET_ON(msm_run(*e, (bp::ge*)results, (const bp::fe*)scalars, (const bp::ge*)points, n, count, s));
+    BP_RET_ON(hipGetLastError());
+    return HIPBP_OK;
+}
+
+int hipbp_msm_batch_gens(ge25519* results, const fe25519* scalars, const void* gens, size_t count, void* stream) {
+    hipError_t err;
+    Engine* e = engine_or_null(&err);
+    BP_RET_ON(err);
+    const Gens* gs = (const Gens*)gens;
+    if (!gs) { g_err = "null gens"; return HIPBP_ERR_ARG; }
+    if (count == 0 || gs->n == 0) return HIPBP_OK;
+    if (!results || !scalars) { g_err = "null argument"; return HIPBP_ERR_ARG; }
+    if (gs->device != e->device) { g_err = "gens: created on another device"; return HIPBP_ERR_ARG; }
+    const size_t n = 2 * gs->n;
+    if (count > 0x7FFFFFFFull || n * count > 0xFFFFFFFFull) { g_err = "msm_batch_gens: too many items"; return HIPBP_ERR_ARG; }
+    std::lock_guard<std::mutex> lk(e->mu);
+    hipStream_t s = pick(stream, *e);
+    BP_RET_ON(msm_run(*e, (bp::ge*)results, (const bp::fe*)scalars, gs->G(), n, count, s,
+                      gs->bits ? gs->tab.as<bp::ge>() : nullptr, gs->bits));
     BP_RET_ON(hipGetLastError());
     return HIPBP_OK;
 }

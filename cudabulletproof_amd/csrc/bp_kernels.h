@@ -179,7 +179,7 @@ void launch_terms(const RegionList& rl, const SlotDev* slots, const ge* G, const
 // counting sort that groups items of equal chain length into the same waves (m >= MSM_SORT_MIN).
 constexpr size_t MSM_SORT_MIN = 4096;
 void launch_msm_points(ge* pts, const fe* scal, const ge* P, size_t m, uint32_t* perm, unsigned* bins,
-                       const ge* dtab, hipStream_t s, size_t pm = 0);
+                       const ge* dtab, hipStream_t s, size_t pm = 0, const ge* ptab = nullptr, int K = 0);
 void launch_tree(ge* out, const ge* in, int S, size_t m, hipStream_t s);
 void launch_ops_scan(unsigned* bins, int longest_first, hipStream_t s);   // bins -> start offsets
 // Pippenger bucket MSM (bp_pippenger.hip; hipbp_msm_pippenger), 4 <= c <= 12
@@ -252,5 +252,6 @@ void launch_ip_batch(fe* out, const fe* a, const fe* b, size_t n, size_t nvec, h
 void launch_invert(fe* r, const fe* a, size_t count, hipStream_t s);
 void launch_tree_full(ge* result, const ge* in, size_t n, ge* part0, ge* part1, hipStream_t s, int S = 1);
 void launch_msm_full(ge* result, const fe* scal, const ge* P, size_t n, ge* ptsbuf, ge* part0, ge* part1,
-                     uint32_t* perm, unsigned* bins, const ge* dtab, hipStream_t s, size_t count = 1);
+                     uint32_t* perm, unsigned* bins, const ge* dtab, hipStream_t s, size_t count = 1,
+                     const ge* ptab = nullptr, int K = 0);
 }  // namespace bp

@@ -81,15 +81,19 @@ void launch_prefix_tables(ge* tab, const ge* G, const ge* H, const ge* h, const 
 #define BP_MSM_TPB 256   // k_msm_points block size
 #endif
 constexpr int MSM_TPB = BP_MSM_TPB;
+// `ptab` / K (nullable / 0): prefix tables of the points as bases (point b's rows at b << K),
+// when the points are generators with tables (hipbp_msm_batch_gens).
 __global__ __launch_bounds__(MSM_TPB, 768 / MSM_TPB) void k_msm_points(ge* pts, const fe* __restrict__ scal,
                                                     const ge* __restrict__ P, size_t total, size_t pm,
                                                     const uint32_t* __restrict__ perm,
-                                                    const ge* __restrict__ dtab) {
+                                                    const ge* __restrict__ dtab, const ge* __restrict__ ptab,
+                                                    int K) {
     __shared__ geq qs[MSM_TPB];
     size_t i = gid();
     if (i >= total) return;
     if (perm) i = perm[i];
-    ge r = scalarmult<true>(scal[i], P[pm == total ? i : i % pm], &qs[threadIdx.x], dtab);
+    const size_t b = pm == total ? i : i % pm;
+    ge r = scalarmult<true>(scal[i], P[b], &qs[threadIdx.x], dtab, ptab ? ptab + (b << K) : nullptr, ptab ? K : 0);
     pts[i] = ge_norm_dev(r);
 }
 
@@ -99,12 +103,12 @@ __global__ void k_ops_zero(unsigned* bins) {
     for (int k = threadIdx.x; k < OPS_BINS; k += blockDim.x) bins[k] = 0;
 }
 
-__global__ __launch_bounds__(TPB) void k_ops_hist(unsigned* bins, const fe* __restrict__ scal, size_t n) {
+__global__ __launch_bounds__(TPB) void k_ops_hist(unsigned* bins, const fe* __restrict__ scal, size_t n, int K) {
     __shared__ unsigned h[OPS_BINS];
     for (int k = threadIdx.x; k < OPS_BINS; k += TPB) h[k] = 0;
     __syncthreads();
     size_t i = gid();
-    if (i < n) atomicAdd(&h[sm_ops(scal[i])], 1u);
+    if (i < n) atomicAdd(&h[sm_ops_prefix(scal[i], K)], 1u);
     __syncthreads();
     for (int k = threadIdx.x; k < OPS_BINS; k += TPB)
         if (h[k]) atomicAdd(&bins[k], h[k]);
@@ -134,7 +138,7 @@ __global__ __launch_bounds__(SCAN_T) void k_ops_scan(unsigned* bins, int longest
 // (block, bin) to reserve the block's range (per-item global atomics on ~100 hot bins
 // serialise: 1.7 ms for 2^20 items).
 __global__ __launch_bounds__(SCAN_T) void k_ops_scatter(uint32_t* perm, unsigned* offs, const fe* __restrict__ scal,
-                                                        size_t n) {
+                                                        size_t n, int K) {
     __shared__ unsigned cnt[OPS_BINS], base[OPS_BINS];
     for (int k = threadIdx.x; k < OPS_BINS; k += SCAN_T) cnt[k] = 0;
     __syncthreads();
@@ -142,7 +146,7 @@ __global__ __launch_bounds__(SCAN_T) void k_ops_scatter(uint32_t* perm, unsigned
     int key = 0;
     unsigned rank = 0;
     if (i < n) {
-        key = sm_ops(scal[i]);
+        key = sm_ops_prefix(scal[i], K);
         rank = atomicAdd(&cnt[key], 1u);
     }
     __syncthreads();
@@ -157,20 +161,21 @@ void launch_ops_scan(unsigned* bins, int longest_first, hipStream_t s) {
 }
 
 void launch_msm_points(ge* pts, const fe* scal, const ge* P, size_t m, uint32_t* perm, unsigned* bins,
-                       const ge* dtab, hipStream_t s, size_t pm) {
+                       const ge* dtab, hipStream_t s, size_t pm, const ge* ptab, int K) {
+    if (!ptab) K = 0;
     if (!pm) pm = m;
     size_t blocks = (m + TPB - 1) / TPB;
     static const int sort_mode = getenv("HIPBP_MSM_SORT") ? atoi(getenv("HIPBP_MSM_SORT")) : 1;
     if (!sort_mode) perm = nullptr;
     if (perm && bins && m >= MSM_SORT_MIN && m <= 0xFFFFFFFFull) {   // a counting sort of the items by chain length
         k_ops_zero<<<1, 64, 0, s>>>(bins);
-        k_ops_hist<<<blocks, TPB, 0, s>>>(bins, scal, m);
+        k_ops_hist<<<blocks, TPB, 0, s>>>(bins, scal, m, K);
         k_ops_scan<<<1, SCAN_T, 0, s>>>(bins, sort_mode == 1);
-        k_ops_scatter<<<(unsigned)((m + SCAN_T - 1) / SCAN_T), SCAN_T, 0, s>>>(perm, bins, scal, m);
+        k_ops_scatter<<<(unsigned)((m + SCAN_T - 1) / SCAN_T), SCAN_T, 0, s>>>(perm, bins, scal, m, K);
     } else {
         perm = nullptr;
     }
-    k_msm_points<<<(unsigned)((m + MSM_TPB - 1) / MSM_TPB), MSM_TPB, 0, s>>>(pts, scal, P, m, pm, perm, dtab);
+    k_msm_points<<<(unsigned)((m + MSM_TPB - 1) / MSM_TPB), MSM_TPB, 0, s>>>(pts, scal, P, m, pm, perm, dtab, ptab, K);
 }
 
 // Canonical pairwise tree over S segments of m points: for stride 1,2,4,..:
@@ -999,10 +1004,11 @@ void launch_tree_full(ge* result, const ge* in, size_t n, ge* part0, ge* part1, 
 }
 
 void launch_msm_full(ge* result, const fe* scal, const ge* P, size_t n, ge* ptsbuf, ge* part0, ge* part1,
-                     uint32_t* perm, unsigned* bins, const ge* dtab, hipStream_t s, size_t count) {
+                     uint32_t* perm, unsigned* bins, const ge* dtab, hipStream_t s, size_t count, const ge* ptab,
+                     int K) {
     // count MSMs of n points each over the same points: one per-point launch over all count*n
     // items (chain-length sorted together), then the canonical tree per segment
-    launch_msm_points(ptsbuf, scal, P, n * count, perm, bins, dtab, s, n);
+    launch_msm_points(ptsbuf, scal, P, n * count, perm, bins, dtab, s, n, ptab, K);
     launch_tree_full(result, ptsbuf, n, part0, part1, s, (int)count);
 }
 

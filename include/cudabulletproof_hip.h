@@ -243,6 +243,12 @@ int hipbp_msm(ge25519* result, const fe25519* scalars, const ge25519* points, si
 int hipbp_msm_batch(ge25519* results, const fe25519* scalars, const ge25519* points, size_t n, size_t count,
                     void* stream);
 
+/* hipbp_msm_batch over a generator set's G||H (2n points, hipbp_gens_create) with its fixed-base
+ * prefix tables: each point's scalar multiplication starts from the table entry of its scalar's
+ * top K bits, so every result has hipbp_msm_batch's bits with fewer point operations.  scalars
+ * [count*2n] (MSM k = rows k*2n .. k*2n+2n-1, the a||b of an IPA commitment P), results [count]. */
+int hipbp_msm_batch_gens(ge25519* results, const fe25519* scalars, const void* gens, size_t count, void* stream);
+
 /* Pippenger bucket MSM with window_bits-bit windows (4..12; BASELINE configs[2] names 12), over
  * the same fe25519/ge25519 arithmetic, on device buffers.  A LABELLED ALTERNATIVE, not a drop-in
  * for cuda_point_vector_multi_scalar_mul: the reference's MSM bits come from per-point

@@ -1167,3 +1167,35 @@ def test_gens_inner_product_pipeline_same_bits(bp, oracle, n, B, K):
         pipe.close()
     gens.close()
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,count,K", [(64, 3, 6), (256, 2, 10), (4096, 2, 12)])
+def test_msm_batch_gens_same_bits(bp, oracle, n, count, K):
+    """hipbp_msm_batch_gens (canonical MSMs over a generator set's G||H, prefix-table starts) ==
+    hipbp_msm_batch over cat(G, H), bit for bit, including zero scalars and scalars with exactly
+    K and K - 1 leading zeros; one small case also equals the oracle."""
+    import torch
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+    g, h = oracle.gh()
+    rng = np.random.default_rng(n + K)
+    s = rand_fe(rng, count * 2 * n)
+    s[0] = 0
+    s[1, :3] = 0
+    s[1, 3] = np.uint64(1) << np.uint64(63 - K)          # exactly K leading zeros
+    s[2, 3] = (np.uint64(1) << np.uint64(64 - K)) | np.uint64(5)   # K - 1 leading zeros
+    Gd, Hd = T(G), T(H)
+    gens = bp.Generators(n, Gd, Hd, T(g), T(h), prefix_bits=K)
+    sd = T(s)
+    r0 = torch.zeros(count, 16, dtype=torch.int64, device=dev)
+    r1 = torch.zeros(count, 16, dtype=torch.int64, device=dev)
+    bp.msm_batch(r0, sd, torch.cat([Gd, Hd]).contiguous())
+    bp.msm_batch_gens(r1, sd, gens)
+    torch.cuda.synchronize()
+    assert torch.equal(r0, r1)
+    if n == 64:
+        GH = np.concatenate([G, H])
+        assert np.array_equal(r1[0].cpu().numpy().view(np.uint64), oracle.msm_canon(s[:2 * n], GH))
+    gens.close()
