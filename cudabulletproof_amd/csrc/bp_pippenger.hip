@@ -434,10 +434,100 @@ __device__ __forceinline__ ge ge_op_quad(const ge& p, const ge& q) {
     return ge{fe_quad_bcast<0>(r3), fe_quad_bcast<1>(r3), fe_quad_bcast<2>(r3), fe_quad_bcast<3>(r3)};
 }
 
+// ---- the Horner chain: one point operation per 16-lane row, one product per lane quad.
+// fe_mul_q4: the product's 64 word products split over the quad by rows — lane rb forms
+// (x_{2rb+1} 2^32 + x_{2rb}) * y as an exact 320-bit partial (mul2x8_asm) — and two DPP levels of
+// shifted adds sum the partials (the exact 512-bit product) on lane rb = 0, which folds it.
+// Valid on the quad's lane 0 only; the same 512 bits as mul512, so the same result bits.
+__device__ __forceinline__ uint32_t dpp_qperm_1133(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xF5, 0xF, 0xF, true);   // lane l <- l | 1
+}
+__device__ __forceinline__ uint32_t dpp_qperm_2222(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xAA, 0xF, 0xF, true);   // lane l <- quad lane 2
+}
+__device__ __forceinline__ fe fe_mul_q4(const fe& x, const fe& y) {
+    const int rb = threadIdx.x & 3;
+    const uint64_t m0 = 0ull - (uint64_t)(rb & 1), m1 = 0ull - (uint64_t)((rb >> 1) & 1);
+    const uint64_t x01 = x.v[0] ^ ((x.v[0] ^ x.v[1]) & m0), x23 = x.v[2] ^ ((x.v[2] ^ x.v[3]) & m0);
+    const uint64_t xr = x01 ^ ((x01 ^ x23) & m1);
+    const uint32_t a[2] = {(uint32_t)xr, (uint32_t)(xr >> 32)};
+    uint32_t b[8], w[10], q[12], r[16];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        b[2 * i] = (uint32_t)y.v[i];
+        b[2 * i + 1] = (uint32_t)(y.v[i] >> 32);
+    }
+    mul2x8_asm(w, a, b);
+    // lanes 0, 2: q = own partial + the next lane's partial at +2 words (12 words)
+    uint32_t n1[10];
+#pragma unroll
+    for (int i = 0; i < 10; i++) n1[i] = dpp_qperm_1133(w[i]);
+    unsigned c = 0;
+    q[0] = w[0];
+    q[1] = w[1];
+#pragma unroll
+    for (int i = 2; i < 10; i++) q[i] = __builtin_addc(w[i], n1[i - 2], c, &c);
+    q[10] = __builtin_addc(n1[8], 0u, c, &c);
+    q[11] = n1[9] + c;   // < 2^(32*12) in total: no carry out
+    // lane 0: r = q + lane 2's q at +4 words (16 words, the exact 512-bit product)
+    uint32_t n2[12];
+#pragma unroll
+    for (int i = 0; i < 12; i++) n2[i] = dpp_qperm_2222(q[i]);
+    c = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) r[i] = q[i];
+#pragma unroll
+    for (int i = 4; i < 12; i++) r[i] = __builtin_addc(q[i], n2[i - 4], c, &c);
+#pragma unroll
+    for (int i = 12; i < 15; i++) r[i] = __builtin_addc(n2[i - 4], 0u, c, &c);
+    r[15] = n2[11] + c;
+    uint64_t t[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) t[i] = (uint64_t)r[2 * i] | ((uint64_t)r[2 * i + 1] << 32);
+    return fe_fold512(t);
+}
+template <int SRC>   // lane SRC of each 16-lane row to the whole row
+__device__ __forceinline__ fe fe_row_bcast(const fe& a) {
+    fe r;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)a.v[i], 0x150 + SRC, 0xF, 0xF, true);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(a.v[i] >> 32), 0x150 + SRC, 0xF, 0xF, true);
+        r.v[i] = (uint64_t)lo | ((uint64_t)hi << 32);
+    }
+    return r;
+}
+// DBL: add(p, p) (q ignored); else add(p, q).  p, q replicated over the row; result replicated.
+// Quad qi of the row forms product qi of each stage (A, B, T1 T2, Z1 Z2 / X3, Y3, Z3, T3).
+template <bool DBL>
+__device__ __forceinline__ ge ge_op16(const ge& p, const ge& q) {
+    const int qi = (threadIdx.x >> 2) & 3;
+    const fe ymx = fe_sub(p.Y, p.X), ypx = fe_add(p.Y, p.X);
+    const fe x1 = fe_sel4(qi, ymx, ypx, p.T, p.Z);
+    fe r1;
+    if (DBL) {
+        r1 = fe_mul_q4(x1, x1);   // the squares: mul(f, f) == fe25519_sq's product
+    } else {
+        const fe qymx = fe_sub(q.Y, q.X), qypx = fe_add(q.Y, q.X);
+        r1 = fe_mul_q4(x1, fe_sel4(qi, qymx, qypx, q.T, q.Z));
+    }
+    const fe A = fe_row_bcast<0>(r1), B = fe_row_bcast<4>(r1), CT = fe_row_bcast<8>(r1);
+    fe D = fe_row_bcast<12>(r1);
+    const fe C = fe_quad_bcast<0>(fe_mul_q4(CT, k_const()));
+    D = fe_add(D, D);
+    const fe E = fe_sub(B, A), F = fe_sub(D, C), G = fe_add(D, C), H = fe_add(B, A);
+    const fe r3 = fe_mul_q4(fe_sel4(qi, E, G, F, E), fe_sel4(qi, F, H, G, H));
+    return ge{fe_row_bcast<0>(r3), fe_row_bcast<4>(r3), fe_row_bcast<8>(r3), fe_row_bcast<12>(r3)};
+}
+
+#ifndef BP_HORNER16
+#define BP_HORNER16 1
+#endif
 // Horner over windows w_top .. w_end (descending): T = Tin ? *Tin : S_{w_top} (then from
-// w_top - 1); per window c doublings, then + S_w.  One quad per MSM (a block per MSM of the
-// batch; its wave runs 16 identical quads; lane 0 stores).  Split at any window, two calls give
-// the single chain's bits.
+// w_top - 1); per window c doublings, then + S_w.  A block (one wave) per MSM of the batch; each
+// 16-lane row of the wave runs the chain (ge_op16: a product per lane quad, 4 identical rows;
+// BP_HORNER16=0: ge_op_quad, 16 identical quads); lane 0 stores.  Split at any window, two calls
+// give the single chain's bits.
 __global__ __launch_bounds__(64) void k_pip_horner(const ge* __restrict__ Sw, int W, int w_top, int w_end, int c,
                                                   const ge* __restrict__ Tin, ge* out) {
     Sw += (size_t)blockIdx.x * W;   // block m: MSM m of the batch
@@ -451,8 +541,13 @@ __global__ __launch_bounds__(64) void k_pip_horner(const ge* __restrict__ Sw, in
         w--;
     }
     for (; w >= w_end; w--) {
-        for (int d = 0; d < c; d++) T = ge_op_quad<true>(T, T);
-        T = ge_op_quad<false>(T, Sw[w]);
+        if (BP_HORNER16) {
+            for (int d = 0; d < c; d++) T = ge_op16<true>(T, T);
+            T = ge_op16<false>(T, Sw[w]);
+        } else {
+            for (int d = 0; d < c; d++) T = ge_op_quad<true>(T, T);
+            T = ge_op_quad<false>(T, Sw[w]);
+        }
     }
     if (threadIdx.x == 0) *out = T;
 }
