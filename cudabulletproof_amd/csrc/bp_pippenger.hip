@@ -117,19 +117,45 @@ __device__ __forceinline__ uint32_t pip_bucket(const uint16_t* __restrict__ keys
 
 // Bucket sizes straight from the unsorted keys (the sort only orders them): a block takes a tile
 // of one virtual window's keys, counts the digits in LDS and adds its counts to cnt[(v << c) | d].
+// 1024 threads per block and four 16-byte loads in flight per thread: the loop is bound by load
+// latency, not by the LDS atomics.
 constexpr uint32_t HIST_TILE = 65536;
+constexpr int HIST_TPB = 1024;
 template <typename KT>
-__global__ __launch_bounds__(PTPB) void k_pip_hist(const KT* __restrict__ keys, uint32_t n, int c, int ib,
-                                                  uint32_t tpw, uint32_t* cnt) {
+__global__ __launch_bounds__(HIST_TPB) void k_pip_hist(const KT* __restrict__ keys, uint32_t n, int c, int ib,
+                                                      uint32_t tpw, uint32_t* cnt) {
     extern __shared__ uint32_t h[];
     const uint32_t NB = 1u << c, v = blockIdx.x / tpw, t = blockIdx.x - v * tpw;
-    for (uint32_t d = threadIdx.x; d < NB; d += PTPB) h[d] = 0;
+    for (uint32_t d = threadIdx.x; d < NB; d += HIST_TPB) h[d] = 0;
     __syncthreads();
     const KT* __restrict__ k = keys + (size_t)v * n;
-    const uint32_t e = (t + 1) * HIST_TILE < n ? (t + 1) * HIST_TILE : n;
-    for (uint32_t j = t * HIST_TILE + threadIdx.x; j < e; j += PTPB) atomicAdd(&h[(uint32_t)k[j] >> ib], 1u);
+    const uint32_t s0 = t * HIST_TILE, e = (t + 1) * HIST_TILE < n ? (t + 1) * HIST_TILE : n;
+    bool vec = false;
+    if constexpr (sizeof(KT) == 4) {
+        vec = (n & 3) == 0;
+        if (vec) {   // rows and tiles start 16-byte aligned; e - s0 is a multiple of 4
+            const uint4* __restrict__ k4 = (const uint4*)(k + s0);
+            const uint32_t n4 = (e - s0) >> 2;
+            for (uint32_t j = threadIdx.x; j < n4; j += 4 * HIST_TPB) {
+                uint4 a[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    if (j + u * HIST_TPB < n4) a[u] = k4[j + u * HIST_TPB];
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    if (j + u * HIST_TPB < n4) {
+                        atomicAdd(&h[a[u].x >> ib], 1u);
+                        atomicAdd(&h[a[u].y >> ib], 1u);
+                        atomicAdd(&h[a[u].z >> ib], 1u);
+                        atomicAdd(&h[a[u].w >> ib], 1u);
+                    }
+            }
+        }
+    }
+    if (!vec)
+        for (uint32_t j = s0 + threadIdx.x; j < e; j += HIST_TPB) atomicAdd(&h[(uint32_t)k[j] >> ib], 1u);
     __syncthreads();
-    for (uint32_t d = threadIdx.x; d < NB; d += PTPB)
+    for (uint32_t d = threadIdx.x; d < NB; d += HIST_TPB)
         if (h[d]) atomicAdd(&cnt[((size_t)v << c) | d], h[d]);
 }
 
@@ -137,16 +163,14 @@ __global__ __launch_bounds__(PTPB) void k_pip_hist(const KT* __restrict__ keys, 
 // aligned group of 4 consecutive elements of one bucket's current list and reduces it exactly as
 // levels s and 2s of the pairwise tree do (x0+x1, x2+x3, then their sum; a short last group
 // carries), so lists are padded to a multiple of 4.  bid[pos] = the bucket of element pos (every
-// group head is a real element, so no search is needed).  k_pip_len0: the padded lengths, the
-// longest list (one atomic per wave), and the counts in sorted order — digit-major, virtual
+// group head is a real element, so no search is needed).  k_pip_len0: the longest list (one atomic per wave), and the counts in sorted order — digit-major, virtual
 // window minor — whose exclusive scan is each bucket's start in the sorted array.
-__global__ __launch_bounds__(PTPB) void k_pip_len0(const uint32_t* __restrict__ len, uint32_t* pad, uint32_t* cnt_t,
+__global__ __launch_bounds__(PTPB) void k_pip_len0(const uint32_t* __restrict__ len, uint32_t* cnt_t,
                                                   size_t nb, int c, uint32_t Wv, unsigned* maxlen, ge* S) {
     const size_t b = (size_t)blockIdx.x * PTPB + threadIdx.x;
     uint32_t L = 0;
     if (b < nb) {
         L = len[b];
-        pad[b] = (L + 3) & ~3u;
         cnt_t[(b & ((1u << c) - 1)) * Wv + (b >> c)] = L;
         if (!L) S[b] = ge_zero();   // an empty bucket's sum (the steps write every other one)
     }
@@ -175,9 +199,13 @@ __device__ __forceinline__ int pip_steps(const unsigned* maxlen) {
     return (levels + 1) / 2;
 }
 
-// Next layout (len, pad)[b] of step t and its exclusive scan off[b], in two launches:
-// k_pip_scan_part forms len/pad for SCAN_PER consecutive buckets per thread and one partial sum
-// per block; k_pip_scan_fin adds the partial sums of the blocks before it and scans its own.
+// Every step's layout at once.  A list of length L is finished by its step when L <= 4 (its sum
+// goes to S[b]); otherwise the step leaves ceil(L / 4) elements.  So layout t of every bucket
+// follows from the bucket sizes alone: LEN_t[b], PAD_t[b] = LEN_t[b] padded to x4, and
+// OFF_t = the exclusive scan of PAD_t over the buckets.  Two launches form all T layers (the
+// per-step scans were two launches per step on the bucket trees' critical path):
+// k_pip_lay_part writes LEN/PAD for SCAN_PER consecutive buckets per thread and one partial sum
+// per block and layer; k_pip_lay_fin adds the partial sums of the blocks before it and scans.
 constexpr int SCAN_PER = 8;
 constexpr int SCAN_BLK = PTPB * SCAN_PER;
 
@@ -191,63 +219,67 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     return v;
 }
 
-__global__ __launch_bounds__(PTPB) void k_pip_scan_part(int t, const unsigned* __restrict__ maxlen,
-                                                       const uint32_t* __restrict__ len, uint32_t* len2,
-                                                       uint32_t* pad2, size_t nb, uint32_t* part) {
-    if (t >= pip_steps(maxlen)) return;
+__global__ __launch_bounds__(PTPB) void k_pip_lay_part(const uint32_t* __restrict__ len0, int T, size_t nb,
+                                                      uint32_t* LEN, uint32_t* PAD, uint32_t* part, unsigned nparts) {
     __shared__ uint32_t wsum[PTPB / 64];
     const size_t b0 = (size_t)blockIdx.x * SCAN_BLK + (size_t)threadIdx.x * SCAN_PER;
-    uint32_t sum = 0;
+    uint32_t L[SCAN_PER];
 #pragma unroll
-    for (int k = 0; k < SCAN_PER; k++) {
-        const size_t b = b0 + k;
-        if (b < nb) {
-            // a list of <= 4 is finished by this step (its sum goes to S[b]): no next-layout slots
-            const uint32_t L = len[b] <= 4 ? 0u : (len[b] + 3) >> 2, pd = (L + 3) & ~3u;
-            len2[b] = L;
-            pad2[b] = pd;
+    for (int k = 0; k < SCAN_PER; k++) L[k] = b0 + k < nb ? len0[b0 + k] : 0u;
+    for (int t = 0; t < T; t++) {
+        uint32_t sum = 0;
+#pragma unroll
+        for (int k = 0; k < SCAN_PER; k++) {
+            const uint32_t pd = (L[k] + 3) & ~3u;
+            if (b0 + k < nb) {
+                LEN[(size_t)t * nb + b0 + k] = L[k];
+                PAD[(size_t)t * nb + b0 + k] = pd;
+            }
             sum += pd;
+            L[k] = L[k] <= 4 ? 0u : (L[k] + 3) >> 2;
         }
-    }
-    const uint32_t inc = wave_incl_scan(sum);
-    if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = inc;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t tot = 0;
+        const uint32_t inc = wave_incl_scan(sum);
+        if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = inc;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t tot = 0;
 #pragma unroll
-        for (int w = 0; w < PTPB / 64; w++) tot += wsum[w];
-        part[blockIdx.x] = tot;
+            for (int w = 0; w < PTPB / 64; w++) tot += wsum[w];
+            part[(size_t)t * nparts + blockIdx.x] = tot;
+        }
+        __syncthreads();
     }
 }
 
-__global__ __launch_bounds__(PTPB) void k_pip_scan_fin(int t, const unsigned* __restrict__ maxlen,
-                                                      const uint32_t* __restrict__ pad2,
-                                                      const uint32_t* __restrict__ part, size_t nb, uint32_t* off2) {
-    if (t >= pip_steps(maxlen)) return;
+__global__ __launch_bounds__(PTPB) void k_pip_lay_fin(const uint32_t* __restrict__ PAD, const uint32_t* __restrict__ part,
+                                                     unsigned nparts, int T, size_t nb, uint32_t* OFF) {
     __shared__ uint32_t wsum[PTPB / 64];
     __shared__ uint32_t pre;
-    if (threadIdx.x < 64) {   // sum of the partial sums of the blocks before this one
-        uint32_t v = 0;
-        for (unsigned i = threadIdx.x; i < blockIdx.x; i += 64) v += part[i];
-        v = wave_incl_scan(v);
-        if (threadIdx.x == 63) pre = v;
-    }
     const size_t b0 = (size_t)blockIdx.x * SCAN_BLK + (size_t)threadIdx.x * SCAN_PER;
-    uint32_t p[SCAN_PER], sum = 0;
+    for (int t = 0; t < T; t++) {
+        if (threadIdx.x < 64) {   // sum of layer t's partial sums of the blocks before this one
+            uint32_t v = 0;
+            for (unsigned i = threadIdx.x; i < blockIdx.x; i += 64) v += part[(size_t)t * nparts + i];
+            v = wave_incl_scan(v);
+            if (threadIdx.x == 63) pre = v;
+        }
+        uint32_t p[SCAN_PER], sum = 0;
 #pragma unroll
-    for (int k = 0; k < SCAN_PER; k++) {
-        p[k] = b0 + k < nb ? pad2[b0 + k] : 0u;
-        sum += p[k];
-    }
-    const uint32_t inc = wave_incl_scan(sum);
-    if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = inc;
-    __syncthreads();
-    uint32_t run = pre + inc - sum;
-    for (int w = 0; w < (int)(threadIdx.x >> 6); w++) run += wsum[w];
+        for (int k = 0; k < SCAN_PER; k++) {
+            p[k] = b0 + k < nb ? PAD[(size_t)t * nb + b0 + k] : 0u;
+            sum += p[k];
+        }
+        const uint32_t inc = wave_incl_scan(sum);
+        if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = inc;
+        __syncthreads();
+        uint32_t run = pre + inc - sum;
+        for (int w = 0; w < (int)(threadIdx.x >> 6); w++) run += wsum[w];
 #pragma unroll
-    for (int k = 0; k < SCAN_PER; k++) {
-        if (b0 + k < nb) off2[b0 + k] = run;
-        run += p[k];
+        for (int k = 0; k < SCAN_PER; k++) {
+            if (b0 + k < nb) OFF[(size_t)t * nb + b0 + k] = run;
+            run += p[k];
+        }
+        __syncthreads();   // wsum / pre are rewritten by the next layer
     }
 }
 
@@ -261,13 +293,14 @@ __global__ __launch_bounds__(PTPB) void k_pip_bid0(const uint16_t* __restrict__ 
 }
 
 // 32-bit-key path: bid from the layout alone (no sorted value says which virtual window an element
-// is in): one wave per bucket writes its list's positions.
+// is in): one wave per bucket writes its list's group heads (step 0 reads bid only there: every
+// head is a multiple of 4), a quarter of the positions.
 __global__ __launch_bounds__(PTPB) void k_pip_bidfill(const uint32_t* __restrict__ len, const uint32_t* __restrict__ off,
                                                      size_t nb, uint32_t* bid) {
     const size_t b = ((size_t)blockIdx.x * PTPB + threadIdx.x) >> 6;
     if (b >= nb) return;
     const uint32_t L = len[b], o = off[b];
-    for (uint32_t j = threadIdx.x & 63; j < L; j += 64) bid[o + j] = (uint32_t)b;
+    for (uint32_t j = 4 * (threadIdx.x & 63); j < L; j += 256) bid[o + j] = (uint32_t)b;
 }
 
 // (min 4 waves per SIMD: the compiler keeps it at 128 VGPRs)
@@ -623,7 +656,7 @@ struct DBuf {
     template <typename T> T* as() const { return (T*)p; }
 };
 struct PipWs {
-    DBuf keys_in, keys, vals, temp, start, len[2], pad[2], off[2], bid[2], Q[2], S, V, Sw, Tmid, maxlen, part;
+    DBuf keys_in, keys, vals, temp, start, len[2], off[2], lay, bid[2], Q[2], S, V, Sw, Tmid, maxlen, part;
     hipStream_t side = nullptr;           // the Horner chain's stream
     hipEvent_t ev[4] = {};   // [1] top half's buckets done, [2] bottom half done, [3] chain done
 };
@@ -672,8 +705,19 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
     if (!k32) PIP_RET(ws.vals.need(N * 4));
     PIP_RET(ws.start.need(nb * 4));
     for (int i = 0; i < 2; i++) {
-        PIP_RET(ws.len[i].need(nb * 4)); PIP_RET(ws.pad[i].need(nb * 4)); PIP_RET(ws.off[i].need(nb * 4));
+        PIP_RET(ws.len[i].need(nb * 4)); PIP_RET(ws.off[i].need(nb * 4));
     }
+    // the worst-case step count (a bucket list is at most n long); steps past the depth of the
+    // data exit on the device (pip_steps), so nothing here waits for the GPU
+    int levels = 1;
+    while (levels < 31 && ((size_t)1 << levels) < n) levels++;
+    const int steps = (levels + 1) / 2, T = steps + 1;   // layouts 0 .. steps
+    const unsigned nparts = (unsigned)((nb + SCAN_BLK - 1) / SCAN_BLK);
+    PIP_RET(ws.lay.need((size_t)3 * T * nb * 4));
+    PIP_RET(ws.part.need((size_t)T * nparts * 4));
+    uint32_t* LEN = ws.lay.as<uint32_t>();
+    uint32_t* PAD = LEN + (size_t)T * nb;
+    uint32_t* OFF = PAD + (size_t)T * nb;
     // step 0 reads <= N + 3 nb padded positions and writes a quarter of them (+ padding)
     const size_t tot0 = N + 3 * nb, qcap = tot0 / 4 + 4 * nb;
     PIP_RET(ws.bid[0].need(tot0 * 4)); PIP_RET(ws.bid[1].need(qcap * 4));
@@ -687,7 +731,7 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
     else
         PIP_RET(pip_sort(nullptr, tb_sort, ws.keys_in.as<uint16_t>(), ws.keys.as<uint16_t>(), ws.vals.as<uint32_t>(),
                          N, c, s));
-    PIP_RET(hipcub::DeviceScan::ExclusiveSum(nullptr, tb_scan, ws.pad[0].as<uint32_t>(), ws.off[0].as<uint32_t>(),
+    PIP_RET(hipcub::DeviceScan::ExclusiveSum(nullptr, tb_scan, ws.len[1].as<uint32_t>(), ws.off[1].as<uint32_t>(),
                                              (int)nb, s));
     PIP_RET(ws.temp.need(tb_sort > tb_scan ? tb_sort : tb_scan));
 
@@ -707,52 +751,40 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
     PIP_RET(hipMemsetAsync(ws.maxlen.p, 0, sizeof(unsigned), s));
     const uint32_t tpw = (uint32_t)((n + HIST_TILE - 1) / HIST_TILE);
     if (k32)
-        k_pip_hist<uint32_t><<<(unsigned)(W * tpw), PTPB, NB * 4, s>>>(ws.keys_in.as<uint32_t>(), (uint32_t)n, c, ib,
-                                                                       tpw, ws.len[0].as<uint32_t>());
+        k_pip_hist<uint32_t><<<(unsigned)(W * tpw), HIST_TPB, NB * 4, s>>>(ws.keys_in.as<uint32_t>(), (uint32_t)n, c,
+                                                                           ib, tpw, ws.len[0].as<uint32_t>());
     else
-        k_pip_hist<uint16_t><<<(unsigned)(W * tpw), PTPB, NB * 4, s>>>(ws.keys_in.as<uint16_t>(), (uint32_t)n, c, 0,
-                                                                       tpw, ws.len[0].as<uint32_t>());
-    // len[1] / off[1] are free until step 0: the transposed counts and their scan
-    k_pip_len0<<<nb_of(nb), PTPB, 0, s>>>(ws.len[0].as<uint32_t>(), ws.pad[0].as<uint32_t>(), ws.len[1].as<uint32_t>(),
-                                          nb, c, (uint32_t)W, ws.maxlen.as<unsigned>(), ws.S.as<ge>());
+        k_pip_hist<uint16_t><<<(unsigned)(W * tpw), HIST_TPB, NB * 4, s>>>(ws.keys_in.as<uint16_t>(), (uint32_t)n, c,
+                                                                           0, tpw, ws.len[0].as<uint32_t>());
+    // the transposed counts and their scan: each bucket's start in the sorted array
+    k_pip_len0<<<nb_of(nb), PTPB, 0, s>>>(ws.len[0].as<uint32_t>(), ws.len[1].as<uint32_t>(), nb, c, (uint32_t)W,
+                                          ws.maxlen.as<unsigned>(), ws.S.as<ge>());
     PIP_RET(hipcub::DeviceScan::ExclusiveSum(ws.temp.p, tb_scan, ws.len[1].as<uint32_t>(), ws.off[1].as<uint32_t>(),
                                              (int)nb, s));
     k_pip_start<<<nb_of(nb), PTPB, 0, s>>>(ws.off[1].as<uint32_t>(), nb, c, (uint32_t)W, ws.start.as<uint32_t>());
-    PIP_RET(hipcub::DeviceScan::ExclusiveSum(ws.temp.p, tb_scan, ws.pad[0].as<uint32_t>(), ws.off[0].as<uint32_t>(),
-                                             (int)nb, s));
+    // every step's layout (LEN, PAD, OFF)[t], t = 0 .. steps
+    k_pip_lay_part<<<nparts, PTPB, 0, s>>>(ws.len[0].as<uint32_t>(), T, nb, LEN, PAD, ws.part.as<uint32_t>(), nparts);
+    k_pip_lay_fin<<<nparts, PTPB, 0, s>>>(PAD, ws.part.as<uint32_t>(), nparts, T, nb, OFF);
     if (k32) {
         PIP_RET(pip_sort32(ws.temp.p, tb_sort, ws.keys_in.as<uint32_t>(), ws.keys.as<uint32_t>(), N, ib, c, s));
-        k_pip_bidfill<<<nb_of(nb * 64), PTPB, 0, s>>>(ws.len[0].as<uint32_t>(), ws.off[0].as<uint32_t>(), nb,
-                                                       ws.bid[0].as<uint32_t>());
+        k_pip_bidfill<<<nb_of(nb * 64), PTPB, 0, s>>>(LEN, OFF, nb, ws.bid[0].as<uint32_t>());
     } else {
         PIP_RET(pip_sort(ws.temp.p, tb_sort, ws.keys_in.as<uint16_t>(), ws.keys.as<uint16_t>(), ws.vals.as<uint32_t>(),
                          N, c, s));
         k_pip_bid0<<<nb_of(N), PTPB, 0, s>>>(ws.keys.as<uint16_t>(), ws.vals.as<uint32_t>(), N, fn, c,
-                                             ws.start.as<uint32_t>(), ws.off[0].as<uint32_t>(), ws.bid[0].as<uint32_t>());
+                                             ws.start.as<uint32_t>(), OFF, ws.bid[0].as<uint32_t>());
     }
     const uint32_t* keys32 = k32 ? ws.keys.as<uint32_t>() : nullptr;
     const uint32_t imask = ib >= 32 ? 0xFFFFFFFFu : (uint32_t)((1ull << ib) - 1);
-    // the worst-case step count (a bucket list is at most n long); steps past the depth of the
-    // data exit on the device (pip_steps), so nothing here waits for the GPU
-    int levels = 1;
-    while (levels < 31 && ((size_t)1 << levels) < n) levels++;
-    const int steps = (levels + 1) / 2;
-    const unsigned nparts = (unsigned)((nb + SCAN_BLK - 1) / SCAN_BLK);
-    PIP_RET(ws.part.need((size_t)nparts * 4));
-    // step t: layout (off, len, pad, bid)[t & 1] -> [(t + 1) & 1], data -> Q[(t + 1) & 1]
+    // step t: layout t -> t + 1, (bid, data)[t & 1] -> [(t + 1) & 1]
     size_t lanes = (tot0 + 3) / 4;
     for (int t = 0; t < steps; t++) {
         const int a = t & 1, b = a ^ 1;
-        k_pip_scan_part<<<nparts, PTPB, 0, s>>>(t, ws.maxlen.as<unsigned>(), ws.len[a].as<uint32_t>(),
-                                                ws.len[b].as<uint32_t>(), ws.pad[b].as<uint32_t>(), nb,
-                                                ws.part.as<uint32_t>());
-        k_pip_scan_fin<<<nparts, PTPB, 0, s>>>(t, ws.maxlen.as<unsigned>(), ws.pad[b].as<uint32_t>(),
-                                               ws.part.as<uint32_t>(), nb, ws.off[b].as<uint32_t>());
+        const size_t l0 = (size_t)t * nb, l1 = l0 + nb;
         k_pip_step<<<nb_of(lanes), PTPB, 0, s>>>(t, ws.maxlen.as<unsigned>(), P, fn, keys32, imask,
                                                   ws.vals.as<uint32_t>(),
                                                   ws.start.as<uint32_t>(), ws.Q[a].as<ge>(), ws.bid[a].as<uint32_t>(),
-                                                  ws.off[a].as<uint32_t>(), ws.len[a].as<uint32_t>(),
-                                                  ws.pad[a].as<uint32_t>(), ws.off[b].as<uint32_t>(), ws.Q[b].as<ge>(),
+                                                  OFF + l0, LEN + l0, PAD + l0, OFF + l1, ws.Q[b].as<ge>(),
                                                   ws.bid[b].as<uint32_t>(), ws.S.as<ge>(), nb, lanes);
         lanes = lanes / 4 + nb;
     }
