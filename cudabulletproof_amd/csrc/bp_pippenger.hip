@@ -68,10 +68,16 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t x, const FastDiv& f) {
 //    bucket of a sorted element is ((g / n) << c) | digit.
 // MSM m's scalars are s[m n .. m n + n); all share the points.  One thread per V scalars (m, i..):
 // it reads them once and writes their Wp keys, each store coalesced over consecutive i.
+// It also zeroes the bucket counts cnt[0 .. nb) and the longest-list word that the histogram and
+// k_pip_len0 accumulate into (two memset launches less on the serial path).
 template <int V, typename KT>   // V > 1 needs n % V == 0 (one V-key store per window)
 __global__ __launch_bounds__(PTPB) void k_pip_keys(const fe* __restrict__ s, FastDiv fn, uint32_t count, int c,
-                                                  int ib, int w0, int Wp, KT* keys) {
-    const uint32_t n = fn.d, g = (blockIdx.x * PTPB + threadIdx.x) * V;
+                                                  int ib, int w0, int Wp, KT* keys, uint32_t* cnt, size_t nb,
+                                                  unsigned* maxlen) {
+    const size_t tid = (size_t)blockIdx.x * PTPB + threadIdx.x;
+    for (size_t b = tid; b < nb; b += (size_t)gridDim.x * PTPB) cnt[b] = 0;
+    if (tid == 0) *maxlen = 0;
+    const uint32_t n = fn.d, g = (uint32_t)tid * V;
     if (g >= count * n) return;
     const uint32_t m = fdiv(g, fn), i = g - m * n;
     // each scalar as a 256-bit shift register, shifted right by c per window (a limb index that
@@ -740,15 +746,17 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
     const bool v4 = n % 4 == 0;
     const unsigned kgrid = nb_of(v4 ? count * n / 4 : count * n);
     if (k32 && v4)
-        k_pip_keys<4, uint32_t><<<kgrid, PTPB, 0, s>>>(scal, fn, (uint32_t)count, c, ib, w0, Wp, ws.keys_in.as<uint32_t>());
+        k_pip_keys<4, uint32_t><<<kgrid, PTPB, 0, s>>>(scal, fn, (uint32_t)count, c, ib, w0, Wp, ws.keys_in.as<uint32_t>(),
+                                                        ws.len[0].as<uint32_t>(), nb, ws.maxlen.as<unsigned>());
     else if (k32)
-        k_pip_keys<1, uint32_t><<<kgrid, PTPB, 0, s>>>(scal, fn, (uint32_t)count, c, ib, w0, Wp, ws.keys_in.as<uint32_t>());
+        k_pip_keys<1, uint32_t><<<kgrid, PTPB, 0, s>>>(scal, fn, (uint32_t)count, c, ib, w0, Wp, ws.keys_in.as<uint32_t>(),
+                                                        ws.len[0].as<uint32_t>(), nb, ws.maxlen.as<unsigned>());
     else if (v4)
-        k_pip_keys<4, uint16_t><<<kgrid, PTPB, 0, s>>>(scal, fn, (uint32_t)count, c, 0, w0, Wp, ws.keys_in.as<uint16_t>());
+        k_pip_keys<4, uint16_t><<<kgrid, PTPB, 0, s>>>(scal, fn, (uint32_t)count, c, 0, w0, Wp, ws.keys_in.as<uint16_t>(),
+                                                        ws.len[0].as<uint32_t>(), nb, ws.maxlen.as<unsigned>());
     else
-        k_pip_keys<1, uint16_t><<<kgrid, PTPB, 0, s>>>(scal, fn, (uint32_t)count, c, 0, w0, Wp, ws.keys_in.as<uint16_t>());
-    PIP_RET(hipMemsetAsync(ws.len[0].p, 0, nb * 4, s));
-    PIP_RET(hipMemsetAsync(ws.maxlen.p, 0, sizeof(unsigned), s));
+        k_pip_keys<1, uint16_t><<<kgrid, PTPB, 0, s>>>(scal, fn, (uint32_t)count, c, 0, w0, Wp, ws.keys_in.as<uint16_t>(),
+                                                        ws.len[0].as<uint32_t>(), nb, ws.maxlen.as<unsigned>());
     const uint32_t tpw = (uint32_t)((n + HIST_TILE - 1) / HIST_TILE);
     if (k32)
         k_pip_hist<uint32_t><<<(unsigned)(W * tpw), HIST_TPB, NB * 4, s>>>(ws.keys_in.as<uint32_t>(), (uint32_t)n, c,
