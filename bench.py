@@ -37,7 +37,7 @@ FE_B, GE_B = 32, 128
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=1024, help="proofs per step per GPU")
     ap.add_argument("--n", type=int, default=64, help="range bits")

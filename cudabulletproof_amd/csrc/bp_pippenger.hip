@@ -68,15 +68,15 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t x, const FastDiv& f) {
 //    bucket of a sorted element is ((g / n) << c) | digit.
 // MSM m's scalars are s[m n .. m n + n); all share the points.  One thread per V scalars (m, i..):
 // it reads them once and writes their Wp keys, each store coalesced over consecutive i.
-// It also zeroes the bucket counts cnt[0 .. nb) and the longest-list word that the histogram and
-// k_pip_len0 accumulate into (two memset launches less on the serial path).
+// It also zeroes the bucket counts cnt[0 .. nb) and the two words (longest list, bidfill queue
+// length) that the histogram and k_pip_len0 accumulate into (two memset launches less on the serial path).
 template <int V, typename KT>   // V > 1 needs n % V == 0 (one V-key store per window)
 __global__ __launch_bounds__(PTPB) void k_pip_keys(const fe* __restrict__ s, FastDiv fn, uint32_t count, int c,
                                                   int ib, int w0, int Wp, KT* keys, uint32_t* cnt, size_t nb,
                                                   unsigned* maxlen) {
     const size_t tid = (size_t)blockIdx.x * PTPB + threadIdx.x;
     for (size_t b = tid; b < nb; b += (size_t)gridDim.x * PTPB) cnt[b] = 0;
-    if (tid == 0) *maxlen = 0;
+    if (tid < 2) maxlen[tid] = 0;   // [0] the longest list, [1] k_pip_bidfill's queue length
     const uint32_t n = fn.d, g = (uint32_t)tid * V;
     if (g >= count * n) return;
     const uint32_t m = fdiv(g, fn), i = g - m * n;
@@ -171,14 +171,22 @@ __global__ __launch_bounds__(HIST_TPB) void k_pip_hist(const KT* __restrict__ ke
 // carries), so lists are padded to a multiple of 4.  bid[pos] = the bucket of element pos (every
 // group head is a real element, so no search is needed).  k_pip_len0: the longest list (one atomic per wave), and the counts in sorted order — digit-major, virtual
 // window minor — whose exclusive scan is each bucket's start in the sorted array.
+constexpr uint32_t BID_PIECE = 4096;   // list elements per k_pip_bidfill wave
 __global__ __launch_bounds__(PTPB) void k_pip_len0(const uint32_t* __restrict__ len, uint32_t* cnt_t,
-                                                  size_t nb, int c, uint32_t Wv, unsigned* maxlen, ge* S) {
+                                                  size_t nb, int c, uint32_t Wv, unsigned* maxlen, ge* S,
+                                                  uint2* bq) {
     const size_t b = (size_t)blockIdx.x * PTPB + threadIdx.x;
     uint32_t L = 0;
     if (b < nb) {
         L = len[b];
         cnt_t[(b & ((1u << c) - 1)) * Wv + (b >> c)] = L;
         if (!L) S[b] = ge_zero();   // an empty bucket's sum (the steps write every other one)
+        // a long list's pieces past the first go to k_pip_bidfill's extra waves (maxlen[1]
+        // counts them; at most N / BID_PIECE in all)
+        if (L > BID_PIECE) {
+            const uint32_t np = (L - 1) / BID_PIECE, q = atomicAdd(&maxlen[1], np);
+            for (uint32_t u = 0; u < np; u++) bq[q + u] = make_uint2((uint32_t)b, u + 1);
+        }
     }
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) {
@@ -209,10 +217,11 @@ __device__ __forceinline__ int pip_steps(const unsigned* maxlen) {
 // goes to S[b]); otherwise the step leaves ceil(L / 4) elements.  So layout t of every bucket
 // follows from the bucket sizes alone: LEN_t[b], PAD_t[b] = LEN_t[b] padded to x4, and
 // OFF_t = the exclusive scan of PAD_t over the buckets.  Two launches form all T layers (the
-// per-step scans were two launches per step on the bucket trees' critical path):
-// k_pip_lay_part writes LEN/PAD for SCAN_PER consecutive buckets per thread and one partial sum
-// per block and layer; k_pip_lay_fin adds the partial sums of the blocks before it and scans.
-constexpr int SCAN_PER = 8;
+// per-step scans were two launches per step on the bucket trees' critical path), one block row
+// per layer (blockIdx.y): k_pip_lay_part writes LEN/PAD for SCAN_PER consecutive buckets per
+// thread and one partial sum per block; k_pip_lay_fin adds the partial sums of the blocks before
+// it and scans.
+constexpr int SCAN_PER = 4;
 constexpr int SCAN_BLK = PTPB * SCAN_PER;
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
@@ -225,67 +234,61 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     return v;
 }
 
-__global__ __launch_bounds__(PTPB) void k_pip_lay_part(const uint32_t* __restrict__ len0, int T, size_t nb,
-                                                      uint32_t* LEN, uint32_t* PAD, uint32_t* part, unsigned nparts) {
+__global__ __launch_bounds__(PTPB) void k_pip_lay_part(const uint32_t* __restrict__ len0, size_t nb, uint32_t* LEN,
+                                                      uint32_t* PAD, uint32_t* part, unsigned nparts) {
     __shared__ uint32_t wsum[PTPB / 64];
+    const int t = blockIdx.y;   // layer
     const size_t b0 = (size_t)blockIdx.x * SCAN_BLK + (size_t)threadIdx.x * SCAN_PER;
-    uint32_t L[SCAN_PER];
+    uint32_t sum = 0;
 #pragma unroll
-    for (int k = 0; k < SCAN_PER; k++) L[k] = b0 + k < nb ? len0[b0 + k] : 0u;
-    for (int t = 0; t < T; t++) {
-        uint32_t sum = 0;
-#pragma unroll
-        for (int k = 0; k < SCAN_PER; k++) {
-            const uint32_t pd = (L[k] + 3) & ~3u;
-            if (b0 + k < nb) {
-                LEN[(size_t)t * nb + b0 + k] = L[k];
-                PAD[(size_t)t * nb + b0 + k] = pd;
-            }
+    for (int k = 0; k < SCAN_PER; k++) {
+        if (b0 + k < nb) {
+            uint32_t L = len0[b0 + k];
+            for (int u = 0; u < t; u++) L = L <= 4 ? 0u : (L + 3) >> 2;
+            const uint32_t pd = (L + 3) & ~3u;
+            LEN[(size_t)t * nb + b0 + k] = L;
+            PAD[(size_t)t * nb + b0 + k] = pd;
             sum += pd;
-            L[k] = L[k] <= 4 ? 0u : (L[k] + 3) >> 2;
         }
-        const uint32_t inc = wave_incl_scan(sum);
-        if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = inc;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t tot = 0;
+    }
+    const uint32_t inc = wave_incl_scan(sum);
+    if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
 #pragma unroll
-            for (int w = 0; w < PTPB / 64; w++) tot += wsum[w];
-            part[(size_t)t * nparts + blockIdx.x] = tot;
-        }
-        __syncthreads();
+        for (int w = 0; w < PTPB / 64; w++) tot += wsum[w];
+        part[(size_t)t * nparts + blockIdx.x] = tot;
     }
 }
 
 __global__ __launch_bounds__(PTPB) void k_pip_lay_fin(const uint32_t* __restrict__ PAD, const uint32_t* __restrict__ part,
-                                                     unsigned nparts, int T, size_t nb, uint32_t* OFF) {
+                                                     unsigned nparts, size_t nb, uint32_t* OFF) {
     __shared__ uint32_t wsum[PTPB / 64];
     __shared__ uint32_t pre;
+    const int t = blockIdx.y;   // layer
     const size_t b0 = (size_t)blockIdx.x * SCAN_BLK + (size_t)threadIdx.x * SCAN_PER;
-    for (int t = 0; t < T; t++) {
-        if (threadIdx.x < 64) {   // sum of layer t's partial sums of the blocks before this one
-            uint32_t v = 0;
-            for (unsigned i = threadIdx.x; i < blockIdx.x; i += 64) v += part[(size_t)t * nparts + i];
-            v = wave_incl_scan(v);
-            if (threadIdx.x == 63) pre = v;
-        }
-        uint32_t p[SCAN_PER], sum = 0;
+    if (threadIdx.x < 64) {   // sum of layer t's partial sums of the blocks before this one
+        uint32_t v = 0;
+        for (unsigned i = threadIdx.x; i < blockIdx.x; i += 64) v += part[(size_t)t * nparts + i];
+        v = wave_incl_scan(v);
+        if (threadIdx.x == 63) pre = v;
+    }
+    uint32_t p[SCAN_PER], sum = 0;
 #pragma unroll
-        for (int k = 0; k < SCAN_PER; k++) {
-            p[k] = b0 + k < nb ? PAD[(size_t)t * nb + b0 + k] : 0u;
-            sum += p[k];
-        }
-        const uint32_t inc = wave_incl_scan(sum);
-        if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = inc;
-        __syncthreads();
-        uint32_t run = pre + inc - sum;
-        for (int w = 0; w < (int)(threadIdx.x >> 6); w++) run += wsum[w];
+    for (int k = 0; k < SCAN_PER; k++) {
+        p[k] = b0 + k < nb ? PAD[(size_t)t * nb + b0 + k] : 0u;
+        sum += p[k];
+    }
+    const uint32_t inc = wave_incl_scan(sum);
+    if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = inc;
+    __syncthreads();
+    uint32_t run = pre + inc - sum;
+    for (int w = 0; w < (int)(threadIdx.x >> 6); w++) run += wsum[w];
 #pragma unroll
-        for (int k = 0; k < SCAN_PER; k++) {
-            if (b0 + k < nb) OFF[(size_t)t * nb + b0 + k] = run;
-            run += p[k];
-        }
-        __syncthreads();   // wsum / pre are rewritten by the next layer
+    for (int k = 0; k < SCAN_PER; k++) {
+        if (b0 + k < nb) OFF[(size_t)t * nb + b0 + k] = run;
+        run += p[k];
     }
 }
 
@@ -299,14 +302,26 @@ __global__ __launch_bounds__(PTPB) void k_pip_bid0(const uint16_t* __restrict__ 
 }
 
 // 32-bit-key path: bid from the layout alone (no sorted value says which virtual window an element
-// is in): one wave per bucket writes its list's group heads (step 0 reads bid only there: every
-// head is a multiple of 4), a quarter of the positions.
+// is in).  A wave writes one BID_PIECE-element piece of one bucket's list, at its group heads
+// only (step 0 reads bid only there: every head is a multiple of 4): wave w < nb takes bucket w's
+// first piece, wave nb + q the q-th entry of k_pip_len0's queue of further pieces, so the deep
+// buckets (the top window's few digits) do not leave one wave looping over a whole list.
 __global__ __launch_bounds__(PTPB) void k_pip_bidfill(const uint32_t* __restrict__ len, const uint32_t* __restrict__ off,
-                                                     size_t nb, uint32_t* bid) {
-    const size_t b = ((size_t)blockIdx.x * PTPB + threadIdx.x) >> 6;
-    if (b >= nb) return;
+                                                     size_t nb, const unsigned* __restrict__ maxlen,
+                                                     const uint2* __restrict__ bq, uint32_t* bid) {
+    const size_t w = ((size_t)blockIdx.x * PTPB + threadIdx.x) >> 6;
+    uint32_t b, pc = 0;
+    if (w < nb) {
+        b = (uint32_t)w;
+    } else {
+        if (w - nb >= maxlen[1]) return;
+        const uint2 e = bq[w - nb];
+        b = e.x;
+        pc = e.y;
+    }
     const uint32_t L = len[b], o = off[b];
-    for (uint32_t j = 4 * (threadIdx.x & 63); j < L; j += 256) bid[o + j] = (uint32_t)b;
+    const uint32_t e = L < (pc + 1) * BID_PIECE ? L : (pc + 1) * BID_PIECE;
+    for (uint32_t j = pc * BID_PIECE + 4 * (threadIdx.x & 63); j < e; j += 256) bid[o + j] = b;
 }
 
 // (min 4 waves per SIMD: the compiler keeps it at 128 VGPRs)
@@ -662,7 +677,7 @@ struct DBuf {
     template <typename T> T* as() const { return (T*)p; }
 };
 struct PipWs {
-    DBuf keys_in, keys, vals, temp, start, len[2], off[2], lay, bid[2], Q[2], S, V, Sw, Tmid, maxlen, part;
+    DBuf keys_in, keys, vals, temp, start, len[2], off[2], lay, bq, bid[2], Q[2], S, V, Sw, Tmid, maxlen, part;
     hipStream_t side = nullptr;           // the Horner chain's stream
     hipEvent_t ev[4] = {};   // [1] top half's buckets done, [2] bottom half done, [3] chain done
 };
@@ -730,7 +745,9 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
     PIP_RET(ws.Q[0].need(qcap * sizeof(ge))); PIP_RET(ws.Q[1].need(qcap * sizeof(ge)));
     PIP_RET(ws.V.need((size_t)W * NC * sizeof(ge)));
     PIP_RET(ws.S.need(nb * sizeof(ge)));
-    PIP_RET(ws.maxlen.need(sizeof(unsigned)));
+    PIP_RET(ws.maxlen.need(2 * sizeof(unsigned)));
+    const size_t nbq = N / BID_PIECE + 1;   // bidfill queue capacity (further pieces of long lists)
+    PIP_RET(ws.bq.need(nbq * sizeof(uint2)));
     size_t tb_sort = 0, tb_scan = 0;
     if (k32)
         PIP_RET(pip_sort32(nullptr, tb_sort, ws.keys_in.as<uint32_t>(), ws.keys.as<uint32_t>(), N, ib, c, s));
@@ -766,16 +783,18 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
                                                                            0, tpw, ws.len[0].as<uint32_t>());
     // the transposed counts and their scan: each bucket's start in the sorted array
     k_pip_len0<<<nb_of(nb), PTPB, 0, s>>>(ws.len[0].as<uint32_t>(), ws.len[1].as<uint32_t>(), nb, c, (uint32_t)W,
-                                          ws.maxlen.as<unsigned>(), ws.S.as<ge>());
+                                          ws.maxlen.as<unsigned>(), ws.S.as<ge>(), ws.bq.as<uint2>());
     PIP_RET(hipcub::DeviceScan::ExclusiveSum(ws.temp.p, tb_scan, ws.len[1].as<uint32_t>(), ws.off[1].as<uint32_t>(),
                                              (int)nb, s));
     k_pip_start<<<nb_of(nb), PTPB, 0, s>>>(ws.off[1].as<uint32_t>(), nb, c, (uint32_t)W, ws.start.as<uint32_t>());
     // every step's layout (LEN, PAD, OFF)[t], t = 0 .. steps
-    k_pip_lay_part<<<nparts, PTPB, 0, s>>>(ws.len[0].as<uint32_t>(), T, nb, LEN, PAD, ws.part.as<uint32_t>(), nparts);
-    k_pip_lay_fin<<<nparts, PTPB, 0, s>>>(PAD, ws.part.as<uint32_t>(), nparts, T, nb, OFF);
+    k_pip_lay_part<<<dim3(nparts, T), PTPB, 0, s>>>(ws.len[0].as<uint32_t>(), nb, LEN, PAD, ws.part.as<uint32_t>(),
+                                                    nparts);
+    k_pip_lay_fin<<<dim3(nparts, T), PTPB, 0, s>>>(PAD, ws.part.as<uint32_t>(), nparts, nb, OFF);
     if (k32) {
         PIP_RET(pip_sort32(ws.temp.p, tb_sort, ws.keys_in.as<uint32_t>(), ws.keys.as<uint32_t>(), N, ib, c, s));
-        k_pip_bidfill<<<nb_of(nb * 64), PTPB, 0, s>>>(LEN, OFF, nb, ws.bid[0].as<uint32_t>());
+        k_pip_bidfill<<<nb_of((nb + nbq) * 64), PTPB, 0, s>>>(LEN, OFF, nb, ws.maxlen.as<unsigned>(),
+                                                               ws.bq.as<uint2>(), ws.bid[0].as<uint32_t>());
     } else {
         PIP_RET(pip_sort(ws.temp.p, tb_sort, ws.keys_in.as<uint16_t>(), ws.keys.as<uint16_t>(), ws.vals.as<uint32_t>(),
                          N, c, s));
