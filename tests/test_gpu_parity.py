@@ -812,11 +812,13 @@ def test_msm_pippenger_rejects_bad_window(bp):
                                                                                       device=dev), z, 13)
 
 
-@pytest.mark.parametrize("kind", ["same", "zero", "one_bit"])
-def test_msm_pippenger_degenerate_scalars(bp, oracle, kind):
-    """Every point in one bucket per window (deep bucket trees, many empty buckets)."""
+@pytest.mark.parametrize("kind,n", [("same", 3000), ("zero", 3000), ("one_bit", 3000), ("same", 10000),
+                                    ("one_bit", 9001)])
+def test_msm_pippenger_degenerate_scalars(bp, oracle, kind, n):
+    """Every point in one bucket per window (deep bucket trees, many empty buckets).  n > 4096: the
+    lists are longer than one k_pip_bidfill piece (BID_PIECE), so the extra-piece queue runs."""
     import torch
-    n, c = 3000, 8
+    c = 8
     P = oracle.base_points(n, 12)
     s = np.zeros((n, 4), np.uint64)
     if kind == "same":

@@ -1,0 +1,45 @@
+"""Summarize a tools/profile_pip.sh run (gpurun_out/prof_<tag>_pip/) into profiles/.
+
+    python tools/pip_prof_summary.py <tag>
+      -> profiles/rocprof_<tag>_pip_summary.md   per-kernel totals and per-MSM times
+      -> profiles/raw_<tag>_pip/kernel_stats.csv  rocprofv3's own --stats table
+"""
+import csv
+import os
+import shutil
+import sys
+
+tag = sys.argv[1]
+root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+src = os.path.join(root, "gpurun_out", f"prof_{tag}_pip")
+rows = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv"))))
+probe = open(os.path.join(src, "probe.txt")).read().strip()
+tot = {}
+for r in rows:
+    k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
+    if "rocprim" in k:
+        k = "rocprim " + ("histogram" if "histogram" in r["Kernel_Name"] else
+                          "onesweep" if "onesweep" in r["Kernel_Name"] else
+                          "scan/lookback" if ("lookback" in r["Kernel_Name"] or "scan" in r["Kernel_Name"]) else "other")
+    n, t = tot.get(k, (0, 0))
+    tot[k] = (n + 1, t + int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+nmsm = sum(n for k, (n, _) in tot.items() if k.endswith("k_pip_horner")) // 2
+all_ns = sum(t for _, t in tot.values())
+out = [f"# rocprofv3 summary — {tag}, Pippenger MSM alone", "",
+       f"Command: `tools/profile_pip.sh {tag}` on one MI355X: `rocprofv3 --kernel-trace --stats -- python3 "
+       "tools/pip_probe.py 20 12 12 2` (2^20 config-3 points, window 12: one warm-up + 12 single-stream MSMs, then one "
+       "warm-up per stream + 12 MSMs alternating over two streams, each checked equal). "
+       f"{nmsm} MSMs under the profiler (k_pip_horner: 2 launches per MSM). Probe output (under the profiler, which "
+       "serialises part of the two-stream overlap):", "", "```", probe, "```", "",
+       "| kernel | calls | total ms | avg ms | per MSM ms | % GPU time |", "|---|---|---|---|---|---|"]
+for k, (n, t) in sorted(tot.items(), key=lambda x: -x[1][1]):
+    out.append(f"| {k} | {n} | {t / 1e6:.3f} | {t / n / 1e6:.4f} | {t / nmsm / 1e6:.4f} | {100 * t / all_ns:.1f} |")
+out.append(f"| **all kernels** |  | {all_ns / 1e6:.3f} |  | {all_ns / nmsm / 1e6:.3f} | 100 |")
+out += ["", "Per MSM, the kernel time adds to more than the wall time of one call because the top part's chunks, "
+        "window trees and Horner run on the side stream beside the bottom part's bucket trees (DESIGN §7c)."]
+dst = os.path.join(root, "profiles", f"rocprof_{tag}_pip_summary.md")
+open(dst, "w").write("\n".join(out) + "\n")
+os.makedirs(os.path.join(root, "profiles", f"raw_{tag}_pip"), exist_ok=True)
+shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
+            os.path.join(root, "profiles", f"raw_{tag}_pip", "kernel_stats.csv"))
+print(dst)
