@@ -70,6 +70,8 @@ def parse():
                     help="fixed-base prefix tables of the generators (hipbp_pipeline_prefix_tables; "
                          "0 = off): one-time setup, same bits")
     ap.add_argument("--shard-total", type=int, default=1 << 16, help="configs[4]: proofs in the sharded batch")
+    ap.add_argument("--shard-batch", type=int, default=0,
+                    help="configs[4]: proofs per pipeline push (0: auto from the rank's shard size)")
     ap.add_argument("--no-shard", action="store_true")
     ap.add_argument("--host-count", type=int, default=32768, help="proofs per host-struct API call")
     ap.add_argument("--no-host", action="store_true")
@@ -405,7 +407,21 @@ def ipa_leg(args, dev):
             "prefix_tables": tables if gens is not None else None, "P_tables_equal_plain": P_same}
 
 
-def shard_leg(args, dev, world, rank, pipes, gens, G, H, g, h):
+def shard_push_batch(args, shard_size, npipe):
+    """Proofs per push for a rank's shard.  A pushed batch completes depth - 1 ticks after its push,
+    and the drain ticks (fold rounds 3..5, final terms of the last batches) are latency-bound, so a
+    small shard (8192 proofs per rank at N = 8) goes through in fewer, larger pushes: ≈2 per
+    pipeline, at most 4096 proofs each; a large one keeps the bench's B (measured)."""
+    if args.shard_batch > 0:
+        return args.shard_batch
+    per = -(-shard_size // (2 * npipe))
+    Bs = args.batch
+    while Bs < per and Bs < 4096:
+        Bs *= 2
+    return Bs
+
+
+def shard_leg(args, dev, world, rank, pipes, gens, G, H, g, h, streams=None):
     """configs[4]: ONE batch of 2^16 64-bit proofs (1024 x 4 distinct proofs, tiled: the kernels do
     not dedupe) split into equal contiguous shards over the ranks (shard.shard_bounds).  Each rank
     verifies its shard through its pipelines; the pass counts meet in one all_reduce(SUM) and the
@@ -426,15 +442,30 @@ def shard_leg(args, dev, world, rank, pipes, gens, G, H, g, h):
                                             gens=gens)
         tiles.append({k: out[k] for k in bp.RangeProofBatch.FIELDS})
     torch.cuda.synchronize(dev)
-    jobs = []   # (tile, first row, rows) per push; proof j of the global set is tile (j // B) % 4, row j % B
-    j = lo
+    Bs = shard_push_batch(args, hi - lo, len(pipes))
+    own = []
+    if Bs != B:   # pipelines sized for the larger pushes, on the same streams
+        own = [bp.VerifyPipeline(Bs, n, G, H, h, stream=streams[i] if streams else None)
+               for i in range(len(pipes))]
+        if gens is not None:
+            for pp in own:
+                pp.use_gens(gens)
+        pipes = own
+    def rows(j0, m):   # proofs [j0, j0 + m) of the global set: proof j is tile (j // B) % 4, row j % B
+        parts, j = [], j0
+        while j < j0 + m:
+            k = min(B - j % B, j0 + m - j)
+            parts.append(((j // B) % 4, j % B, k))
+            j += k
+        return {f: torch.cat([tiles[t][f][r0:r0 + k] for t, r0, k in parts]) for f in bp.RangeProofBatch.FIELDS}
+    jobs, j = [], lo
     while j < hi:
-        m = min(B - j % B, hi - j)
-        jobs.append(((j // B) % 4, j % B, m))
+        m = min(Bs, hi - j)
+        jobs.append((j, m))
         j += m
-    batches = [bp.RangeProofBatch(n, **{k: v[r0:r0 + m] for k, v in tiles[t].items()}) for t, r0, m in jobs]
+    batches = [bp.RangeProofBatch(n, **rows(j0, m)) for j0, m in jobs]
     ok = torch.zeros(hi - lo, dtype=torch.uint8, device=dev)
-    offs = np.cumsum([0] + [m for _, _, m in jobs])
+    offs = np.cumsum([0] + [m for _, m in jobs])
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -457,7 +488,10 @@ def shard_leg(args, dev, world, rank, pipes, gens, G, H, g, h):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     import hashlib as _h
+    for pp in own:
+        pp.close()
     return {"metric": "2^16-proof 64-bit range-proof batch verify (BASELINE configs[4])", "value": total / dt,
+            "push_batch": Bs,
             "unit": "verifies/s", "proofs": total, "n_gpus": world, "scaling": "strong", "ms": dt * 1e3,
             "passes": int(passes.item()), "verdicts_sha256": _h.sha256(allv.cpu().numpy().tobytes()).hexdigest()[:16],
             "collectives": "all_reduce(SUM) of pass counts + all_gather of the verdict bytes (RCCL at N > 1)",
@@ -654,7 +688,7 @@ def main():
     torch.cuda.synchronize(dev)
     sharded = None
     if pipes and not args.no_shard:   # configs[4] on the same pipelines (all ranks take part)
-        sharded = shard_leg(args, dev, world, rank, pipes, gens, Gd, Hd, gd, hd)
+        sharded = shard_leg(args, dev, world, rank, pipes, gens, Gd, Hd, gd, hd, streams)
     for pp in pipes:
         pp.close()
     if world > 1:
