@@ -702,9 +702,18 @@ static hipError_t pip_sort(void* temp, size_t& tb, const uint16_t* kin, uint16_t
                                      (unsigned)N, 0u, (unsigned)bits, s);
 }
 // stable sort of the 32-bit keys (digit << ib | i) on bits [ib, ib + c): keys only
+#ifdef BP_PIP_SORT_IPT   // A/B builds: onesweep tile (items per thread) and radix bits per pass
+using PipSortCfg = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, BP_PIP_SORT_IPT>,
+                                        rocprim::kernel_config<1024, BP_PIP_SORT_IPT>, BP_PIP_SORT_BITS,
+                                        rocprim::block_radix_rank_algorithm::match>>;
+#else
+using PipSortCfg = rocprim::default_config;
+#endif
 static hipError_t pip_sort32(void* temp, size_t& tb, const uint32_t* kin, uint32_t* kout, size_t N, int ib, int c,
                              hipStream_t s) {
-    return rocprim::radix_sort_keys(temp, tb, kin, kout, (unsigned)N, (unsigned)ib, (unsigned)(ib + c), s);
+    return rocprim::radix_sort_keys<PipSortCfg>(temp, tb, kin, kout, (unsigned)N, (unsigned)ib, (unsigned)(ib + c), s);
 }
 // HIPBP_PIP_KEYS16=1 forces the 16-bit-key path (read per call: tests run both paths in one process)
 static bool pip_force16() {
