@@ -21,7 +21,6 @@
 // latency-bound), on a side stream so its top-half part overlaps the bottom half's buckets.
 // The host never waits: the tree depth is read on the device (pip_steps), so independent MSMs
 // on different streams overlap one's latency-bound chains with another's bucket trees.
-#include <hipcub/hipcub.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 
@@ -234,15 +233,22 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     return v;
 }
 
-__global__ __launch_bounds__(PTPB) void k_pip_lay_part(const uint32_t* __restrict__ len0, size_t nb, uint32_t* LEN,
-                                                      uint32_t* PAD, uint32_t* part, unsigned nparts) {
+// The extra layer T (the last block row) scans the bucket sizes in sorted order instead (cnt_t:
+// digit-major, virtual window minor, unpadded): OFF_T is each bucket's start in the sorted array.
+__global__ __launch_bounds__(PTPB) void k_pip_lay_part(const uint32_t* __restrict__ len0,
+                                                      const uint32_t* __restrict__ cnt_t, int T, size_t nb,
+                                                      uint32_t* LEN, uint32_t* PAD, uint32_t* part, unsigned nparts) {
     __shared__ uint32_t wsum[PTPB / 64];
     const int t = blockIdx.y;   // layer
     const size_t b0 = (size_t)blockIdx.x * SCAN_BLK + (size_t)threadIdx.x * SCAN_PER;
     uint32_t sum = 0;
 #pragma unroll
     for (int k = 0; k < SCAN_PER; k++) {
-        if (b0 + k < nb) {
+        if (b0 + k < nb && t == T) {
+            const uint32_t L = cnt_t[b0 + k];
+            PAD[(size_t)t * nb + b0 + k] = L;
+            sum += L;
+        } else if (b0 + k < nb) {
             uint32_t L = len0[b0 + k];
             for (int u = 0; u < t; u++) L = L <= 4 ? 0u : (L + 3) >> 2;
             const uint32_t pd = (L + 3) & ~3u;
@@ -677,7 +683,7 @@ struct DBuf {
     template <typename T> T* as() const { return (T*)p; }
 };
 struct PipWs {
-    DBuf keys_in, keys, vals, temp, start, len[2], off[2], lay, bq, bid[2], Q[2], S, V, Sw, Tmid, maxlen, part;
+    DBuf keys_in, keys, vals, temp, start, len[2], lay, bq, bid[2], Q[2], S, V, Sw, Tmid, maxlen, part;
     hipStream_t side = nullptr;           // the Horner chain's stream
     hipEvent_t ev[4] = {};   // [1] top half's buckets done, [2] bottom half done, [3] chain done
 };
@@ -735,19 +741,19 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
     if (!k32) PIP_RET(ws.vals.need(N * 4));
     PIP_RET(ws.start.need(nb * 4));
     for (int i = 0; i < 2; i++) {
-        PIP_RET(ws.len[i].need(nb * 4)); PIP_RET(ws.off[i].need(nb * 4));
+        PIP_RET(ws.len[i].need(nb * 4));
     }
     // the worst-case step count (a bucket list is at most n long); steps past the depth of the
     // data exit on the device (pip_steps), so nothing here waits for the GPU
     int levels = 1;
     while (levels < 31 && ((size_t)1 << levels) < n) levels++;
-    const int steps = (levels + 1) / 2, T = steps + 1;   // layouts 0 .. steps
+    const int steps = (levels + 1) / 2, T = steps + 1;   // layouts 0 .. steps, then the start layer T
     const unsigned nparts = (unsigned)((nb + SCAN_BLK - 1) / SCAN_BLK);
-    PIP_RET(ws.lay.need((size_t)3 * T * nb * 4));
-    PIP_RET(ws.part.need((size_t)T * nparts * 4));
+    PIP_RET(ws.lay.need((size_t)3 * (T + 1) * nb * 4));
+    PIP_RET(ws.part.need((size_t)(T + 1) * nparts * 4));
     uint32_t* LEN = ws.lay.as<uint32_t>();
-    uint32_t* PAD = LEN + (size_t)T * nb;
-    uint32_t* OFF = PAD + (size_t)T * nb;
+    uint32_t* PAD = LEN + (size_t)(T + 1) * nb;
+    uint32_t* OFF = PAD + (size_t)(T + 1) * nb;
     // step 0 reads <= N + 3 nb padded positions and writes a quarter of them (+ padding)
     const size_t tot0 = N + 3 * nb, qcap = tot0 / 4 + 4 * nb;
     PIP_RET(ws.bid[0].need(tot0 * 4)); PIP_RET(ws.bid[1].need(qcap * 4));
@@ -757,15 +763,13 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
     PIP_RET(ws.maxlen.need(2 * sizeof(unsigned)));
     const size_t nbq = N / BID_PIECE + 1;   // bidfill queue capacity (further pieces of long lists)
     PIP_RET(ws.bq.need(nbq * sizeof(uint2)));
-    size_t tb_sort = 0, tb_scan = 0;
+    size_t tb_sort = 0;
     if (k32)
         PIP_RET(pip_sort32(nullptr, tb_sort, ws.keys_in.as<uint32_t>(), ws.keys.as<uint32_t>(), N, ib, c, s));
     else
         PIP_RET(pip_sort(nullptr, tb_sort, ws.keys_in.as<uint16_t>(), ws.keys.as<uint16_t>(), ws.vals.as<uint32_t>(),
                          N, c, s));
-    PIP_RET(hipcub::DeviceScan::ExclusiveSum(nullptr, tb_scan, ws.len[1].as<uint32_t>(), ws.off[1].as<uint32_t>(),
-                                             (int)nb, s));
-    PIP_RET(ws.temp.need(tb_sort > tb_scan ? tb_sort : tb_scan));
+    PIP_RET(ws.temp.need(tb_sort));
 
     const FastDiv fn = fastdiv_make((uint32_t)n);
     // keys_in rows start 8-byte (16-byte) aligned when n % 4 == 0 (DBuf memory)
@@ -790,16 +794,14 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
     else
         k_pip_hist<uint16_t><<<(unsigned)(W * tpw), HIST_TPB, NB * 4, s>>>(ws.keys_in.as<uint16_t>(), (uint32_t)n, c,
                                                                            0, tpw, ws.len[0].as<uint32_t>());
-    // the transposed counts and their scan: each bucket's start in the sorted array
+    // the counts in sorted order (transposed), for the start layer
     k_pip_len0<<<nb_of(nb), PTPB, 0, s>>>(ws.len[0].as<uint32_t>(), ws.len[1].as<uint32_t>(), nb, c, (uint32_t)W,
                                           ws.maxlen.as<unsigned>(), ws.S.as<ge>(), ws.bq.as<uint2>());
-    PIP_RET(hipcub::DeviceScan::ExclusiveSum(ws.temp.p, tb_scan, ws.len[1].as<uint32_t>(), ws.off[1].as<uint32_t>(),
-                                             (int)nb, s));
-    k_pip_start<<<nb_of(nb), PTPB, 0, s>>>(ws.off[1].as<uint32_t>(), nb, c, (uint32_t)W, ws.start.as<uint32_t>());
-    // every step's layout (LEN, PAD, OFF)[t], t = 0 .. steps
-    k_pip_lay_part<<<dim3(nparts, T), PTPB, 0, s>>>(ws.len[0].as<uint32_t>(), nb, LEN, PAD, ws.part.as<uint32_t>(),
-                                                    nparts);
-    k_pip_lay_fin<<<dim3(nparts, T), PTPB, 0, s>>>(PAD, ws.part.as<uint32_t>(), nparts, nb, OFF);
+    // every step's layout (LEN, PAD, OFF)[t], t = 0 .. steps, and OFF[T] = the sorted-order starts
+    k_pip_lay_part<<<dim3(nparts, T + 1), PTPB, 0, s>>>(ws.len[0].as<uint32_t>(), ws.len[1].as<uint32_t>(), T, nb,
+                                                        LEN, PAD, ws.part.as<uint32_t>(), nparts);
+    k_pip_lay_fin<<<dim3(nparts, T + 1), PTPB, 0, s>>>(PAD, ws.part.as<uint32_t>(), nparts, nb, OFF);
+    k_pip_start<<<nb_of(nb), PTPB, 0, s>>>(OFF + (size_t)T * nb, nb, c, (uint32_t)W, ws.start.as<uint32_t>());
     if (k32) {
         PIP_RET(pip_sort32(ws.temp.p, tb_sort, ws.keys_in.as<uint32_t>(), ws.keys.as<uint32_t>(), N, ib, c, s));
         k_pip_bidfill<<<nb_of((nb + nbq) * 64), PTPB, 0, s>>>(LEN, OFF, nb, ws.maxlen.as<unsigned>(),
