@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--msm-log2", type=int, default=20)
     ap.add_argument("--ipa-n", type=int, default=4096, help="configs[3]: inner-product-argument size")
     ap.add_argument("--ipa-batch", type=int, default=64, help="IPA proofs per pipeline tick")
-    ap.add_argument("--ipa-steps", type=int, default=4)
+    ap.add_argument("--ipa-steps", type=int, default=16)
     ap.add_argument("--no-ipa", action="store_true")
     ap.add_argument("--ipa-prefix-bits", type=int, default=14,
                     help="configs[3]: fixed-base prefix tables of G/H for fold round 0 (0 = none)")
