@@ -192,8 +192,16 @@ __global__ __launch_bounds__(PTPB) void k_pip_len0(const uint32_t* __restrict__ 
         const uint32_t o = __shfl_xor(L, d, 64);
         L = o > L ? o : L;
     }
-    // same-address atomics serialize: skip the ones a plain read already shows cannot raise it
-    if ((threadIdx.x & 63) == 0 && L > __atomic_load_n(maxlen, __ATOMIC_RELAXED)) atomicMax(maxlen, L);
+    // same-address atomics serialize: one per block (the block's waves meet in LDS), and none
+    // where a plain read already shows it cannot raise the maximum
+    __shared__ uint32_t wmax[PTPB / 64];
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = L;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int w = 1; w < PTPB / 64; w++) L = wmax[w] > L ? wmax[w] : L;
+        if (L > __atomic_load_n(maxlen, __ATOMIC_RELAXED)) atomicMax(maxlen, L);
+    }
 }
 __global__ __launch_bounds__(PTPB) void k_pip_start(const uint32_t* __restrict__ start_t, size_t nb, int c, uint32_t Wv,
                                                    uint32_t* start) {
