@@ -114,6 +114,7 @@ EXPORTS = [
     "hipbp_sync", "hipbp_timing_enable",
     "hipbp_timing_collect", "hipbp_kernel_count", "hipbp_kernel_name", "hipbp_pipeline_create",
     "hipbp_pipeline_push", "hipbp_pipeline_flush", "hipbp_pipeline_depth", "hipbp_pipeline_destroy",
+    "hipbp_release_stream_workspaces",
 ]
 
 
@@ -139,7 +140,7 @@ def lib():
                   "hipbp_batch_inner_product_verify", "hipbp_batch_generate_range_proof", "hipbp_msm",
                   "hipbp_msm_pippenger", "hipbp_msm_pippenger_batch", "hipbp_msm_pippenger_windows",
                   "hipbp_msm_pippenger_horner", "hipbp_msm_batch", "hipbp_msm_batch_gens", "hipbp_point_tree",
-                  "hipbp_field_op", "hipbp_sync", "hipbp_device_count"):
+                  "hipbp_field_op", "hipbp_sync", "hipbp_device_count", "hipbp_release_stream_workspaces"):
             getattr(L, f).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -169,15 +170,17 @@ def _u64(a, last):
 
 
 # ====================================================================== reference-named host API
-def cuda_point_vector_multi_scalar_mul(scalars, points):
-    """cuda_bulletproof.h:13 — canonical-tree MSM of device-normalized terms."""
+def cuda_point_vector_multi_scalar_mul(scalars, points, shared=False):
+    """cuda_bulletproof.h:13 (shared: :17, cuda_point_vector_multi_scalar_mul_shared) — canonical-tree
+    MSM of device-normalized terms; both entry points compute the same tree."""
     require_gpu()
     s, P = _u64(scalars, 4), _u64(points, 16)
     if len(s) != len(P):
         raise ValueError("Vector lengths must match for multi-scalar multiplication")
     out = np.zeros(16, np.uint64)
     sv, pv = FieldVector(_p(s).value, len(s)), PointVector(_p(P).value, len(P))
-    lib().cuda_point_vector_multi_scalar_mul(_p(out), ctypes.byref(sv), ctypes.byref(pv))
+    f = lib().cuda_point_vector_multi_scalar_mul_shared if shared else lib().cuda_point_vector_multi_scalar_mul
+    f(_p(out), ctypes.byref(sv), ctypes.byref(pv))
     return out
 
 
@@ -529,6 +532,12 @@ def msm_pippenger_horner(results, window_sums, window_bits=12, stream=None):
                                           ctypes.c_int(window_bits), _stream_ptr(stream)))
 
 
+def release_stream_workspaces(stream=None):
+    """hipbp_release_stream_workspaces: free every workspace cached for `stream` on the current
+    device (MSM, prover, one-shot pipelines, Pippenger pair); call before dropping a stream."""
+    _chk(lib().hipbp_release_stream_workspaces(_stream_ptr(stream)))
+
+
 def point_tree(result, points, stream=None):
     """Canonical tree over device points (the MSM's reduction half): result (16,), points (n,16)."""
     _chk(lib().hipbp_point_tree(_c(result.data_ptr()), _c(points.data_ptr()), _sz(points.shape[0]),
@@ -576,6 +585,7 @@ class VerifyPipeline:
         L.hipbp_pipeline_flush.restype = ctypes.c_int
         L.hipbp_pipeline_depth.restype = ctypes.c_int
         self._keep = (G, H, h, g)
+        self.stream = stream   # the torch stream the ticks run on (None: the null stream)
         self.mode = int(range_mode)
         self.h = L.hipbp_pipeline_create(_sz(max_batch), _sz(n), self.mode, _c(G.data_ptr()), _c(H.data_ptr()),
                                          _c(g.data_ptr()) if g is not None else None, _c(h.data_ptr()),

@@ -868,6 +868,43 @@ int hipbp_msm_pippenger_windows(ge25519* window_sums, const fe25519* scalars, co
     return HIPBP_OK;
 }
 
+// Frees every per-stream workspace the engine keeps for `stream` on the current device (canonical
+// MSM / point-tree buffers, prover buffers, one-shot verify pipelines, Pippenger workspace pair),
+// after waiting for the stream.  A later call on that stream builds them again.
+int hipbp_release_stream_workspaces(void* stream) {
+    hipError_t err;
+    Engine* e = engine_or_null(&err);
+    BP_RET_ON(err);
+    hipStream_t s = (hipStream_t)stream;
+    std::lock_guard<std::mutex> lk(e->mu);
+    BP_RET_ON(hipStreamSynchronize(s));
+    auto mi = e->msm_ws.find(s);
+    if (mi != e->msm_ws.end()) {
+        for (auto& b : mi->second->b)
+            if (b.p) BP_RET_ON(hipFree(b.p));
+        delete mi->second;
+        e->msm_ws.erase(mi);
+    }
+    auto pi = e->provers.find(s);
+    if (pi != e->provers.end()) {
+        for (auto& b : pi->second->b)
+            if (b.p) BP_RET_ON(hipFree(b.p));
+        delete pi->second;
+        e->provers.erase(pi);
+    }
+    for (auto it = e->pipes.begin(); it != e->pipes.end();) {
+        if (std::get<0>(it->first) == s) {
+            it->second->release();
+            delete it->second;
+            it = e->pipes.erase(it);
+        } else {
+            ++it;
+        }
+    }
+    BP_RET_ON(bp::pippenger_release(s));
+    return HIPBP_OK;
+}
+
 int hipbp_msm_pippenger_horner(ge25519* results, const ge25519* window_sums, size_t count, int window_bits,
                                void* stream) {
     hipError_t err;
@@ -1508,6 +1545,7 @@ void cuda_benchmark_multi_scalar_mul(int iterations, size_t vector_size) {
     double dt = (now_s() - t0) / (iterations > 0 ? iterations : 1);
     printf("cuda_benchmark_multi_scalar_mul: n=%zu  %.3f ms/call  %.1f points/s\n", vector_size, dt * 1e3,
            vector_size / dt);
+    fflush(stdout);
 }
 
 void cuda_benchmark_inner_product(int iterations, size_t vector_size) {
@@ -1524,6 +1562,7 @@ void cuda_benchmark_inner_product(int iterations, size_t vector_size) {
     for (int i = 0; i < iterations; i++) cuda_field_vector_inner_product(&r, &av, &bv);
     double dt = (now_s() - t0) / (iterations > 0 ? iterations : 1);
     printf("cuda_benchmark_inner_product: n=%zu  %.3f ms/call\n", vector_size, dt * 1e3);
+    fflush(stdout);
 }
 
 void cuda_benchmark_field_operations(int iterations, size_t batch_size) {
@@ -1544,12 +1583,147 @@ void cuda_benchmark_field_operations(int iterations, size_t batch_size) {
         }
         double dt = (now_s() - t0) / (iterations > 0 ? iterations : 1);
         printf("cuda_benchmark_field_operations: %s x %zu  %.3f ms/call\n", names[op], batch_size, dt * 1e3);
+        fflush(stdout);
     }
 }
 
+static uint64_t bench_mix(uint64_t x) {   // splitmix64: deterministic benchmark inputs
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+// max(iterations, 1) real bit_size-bit range proofs (values < 2^bit_size, random scalars shaped as
+// generate_random_scalar, rp.cu:153-159) made by the GPU prover (hipbp_batch_generate_range_proof,
+// same bits as generate_range_proof), then verified as the reference's host RangeProof structs:
+// one cuda_range_proof_verify call per proof (the reference's per-proof entry point), and once
+// more through hipbp_batch_range_proof_verify_host.  One line: per-call latency, batched rate,
+// pass count, and whether the two verdict sets agree.
 void cuda_benchmark_range_proof(int iterations, size_t bit_size) {
-    printf("cuda_benchmark_range_proof: use bench.py (batched verifies/s) for n=%zu, %d iterations\n", bit_size,
-           iterations);
+    const size_t n = bit_size;
+    if (!is_pow2(n) || n > 64) {
+        fprintf(stderr, "cuda_benchmark_range_proof: bit_size must be a power of two <= 64\n");
+        return;
+    }
+    const size_t count = iterations > 0 ? std::min<size_t>((size_t)iterations, 65536) : 1;
+    const size_t Lr = (size_t)log2i(n), ng = 2 * n + 2;
+    uint64_t st = 0x5EEDull * 1000003 + n;
+    auto rnd = [&]() { return bench_mix(st++); };
+    // generators G[n] | H[n] | g | h: random X, Y < 2^255, Z = 1, T = X Y (the engine's fe25519_mul)
+    std::vector<fe25519> X(ng), Y(ng), T(ng);
+    for (size_t i = 0; i < ng; i++)
+        for (int k = 0; k < 4; k++) {
+            X[i].limbs[k] = rnd() & (k == 3 ? 0x7FFFFFFFFFFFFFFFull : ~0ull);
+            Y[i].limbs[k] = rnd() & (k == 3 ? 0x7FFFFFFFFFFFFFFFull : ~0ull);
+        }
+    cuda_batch_field_mul(T.data(), X.data(), Y.data(), ng);
+    std::vector<ge25519> gen(ng);
+    for (size_t i = 0; i < ng; i++) {
+        memset(&gen[i], 0, sizeof(ge25519));
+        gen[i].X = X[i]; gen[i].Y = Y[i]; gen[i].Z.limbs[0] = 1; gen[i].T = T[i];
+    }
+    auto scalar = [&](fe25519& f) {   // generate_random_scalar's masks: byte 0 &= 0xF8, byte 31 &= 0x7F | 0x40
+        for (int k = 0; k < 4; k++) f.limbs[k] = rnd();
+        f.limbs[0] &= ~7ull;
+        f.limbs[3] = (f.limbs[3] & 0x7FFFFFFFFFFFFFFFull) | 0x4000000000000000ull;
+    };
+    const size_t FE = sizeof(fe25519), GE = sizeof(ge25519);
+    std::vector<fe25519> v(count), gamma(count), sL(count * n), sR(count * n), r4(count * 4);
+    for (size_t p = 0; p < count; p++) {
+        memset(&v[p], 0, FE);
+        v[p].limbs[0] = n == 64 ? rnd() : rnd() & ((1ull << n) - 1);
+        scalar(gamma[p]);
+        for (size_t i = 0; i < n; i++) { scalar(sL[p * n + i]); scalar(sR[p * n + i]); }
+        for (int i = 0; i < 4; i++) scalar(r4[p * 4 + i]);
+    }
+    Engine& e = engine_or_exit();
+    const size_t Lc = Lr ? Lr : 1;
+    // device: inputs | generators | outputs (V A S T1 T2 [count], taux mu t c x a b [count], L R [count Lr], valid)
+    const size_t in_b = (count * (2 + 2 * n + 4)) * FE, gen_b = ng * GE;
+    const size_t out_b = count * (5 * GE + 7 * FE + 2 * Lc * GE) + count;
+    uint8_t* d = nullptr;
+    BP_EXIT_ON(hipMalloc(&d, in_b + gen_b + out_b));
+    fe25519* dv = (fe25519*)d;
+    fe25519* dgam = dv + count;
+    fe25519* dsL = dgam + count;
+    fe25519* dsR = dsL + count * n;
+    fe25519* dr4 = dsR + count * n;
+    ge25519* dgen = (ge25519*)(d + in_b);
+    uint8_t* o = d + in_b + gen_b;
+    BP_EXIT_ON(hipMemcpy(dv, v.data(), count * FE, hipMemcpyHostToDevice));
+    BP_EXIT_ON(hipMemcpy(dgam, gamma.data(), count * FE, hipMemcpyHostToDevice));
+    BP_EXIT_ON(hipMemcpy(dsL, sL.data(), count * n * FE, hipMemcpyHostToDevice));
+    BP_EXIT_ON(hipMemcpy(dsR, sR.data(), count * n * FE, hipMemcpyHostToDevice));
+    BP_EXIT_ON(hipMemcpy(dr4, r4.data(), count * 4 * FE, hipMemcpyHostToDevice));
+    BP_EXIT_ON(hipMemcpy(dgen, gen.data(), gen_b, hipMemcpyHostToDevice));
+    hipbp_proof_out po;
+    ge25519* og = (ge25519*)o;
+    po.V = og; po.A = og + count; po.S = og + 2 * count; po.T1 = og + 3 * count; po.T2 = og + 4 * count;
+    fe25519* of = (fe25519*)(og + 5 * count);
+    po.taux = of; po.mu = of + count; po.t = of + 2 * count; po.c = of + 3 * count; po.x = of + 4 * count;
+    po.a = of + 5 * count; po.b = of + 6 * count;
+    ge25519* olr = (ge25519*)(of + 7 * count);
+    po.L = olr; po.R = olr + count * Lc;
+    po.valid = (uint8_t*)(olr + 2 * count * Lc);
+    hipbp_prove_input pin{count, n, dv, dgam, dsL, dsR, dr4};
+    if (hipbp_batch_generate_range_proof(&pin, dgen, dgen + n, dgen + 2 * n, dgen + 2 * n + 1, &po, nullptr) !=
+        HIPBP_OK) {
+        fprintf(stderr, "HIP error - %s\n", g_err.c_str());
+        exit(EXIT_FAILURE);
+    }
+    BP_EXIT_ON(hipDeviceSynchronize());
+    std::vector<uint8_t> host(out_b);
+    BP_EXIT_ON(hipMemcpy(host.data(), o, out_b, hipMemcpyDeviceToHost));
+    BP_EXIT_ON(hipFree(d));
+    const ge25519* hg = (const ge25519*)host.data();
+    const fe25519* hf = (const fe25519*)(hg + 5 * count);
+    const ge25519* hlr = (const ge25519*)(hf + 7 * count);
+    std::vector<fe25519> ha(hf + 5 * count, hf + 6 * count), hb(hf + 6 * count, hf + 7 * count);
+    std::vector<ge25519> hL(hlr, hlr + count * Lc), hR(hlr + count * Lc, hlr + 2 * count * Lc);
+    std::vector<RangeProof> proofs(count);
+    std::vector<ge25519> V(hg, hg + count);
+    for (size_t p = 0; p < count; p++) {
+        RangeProof& rp = proofs[p];
+        memset(&rp, 0, sizeof rp);
+        rp.V = hg[p]; rp.A = hg[count + p]; rp.S = hg[2 * count + p]; rp.T1 = hg[3 * count + p];
+        rp.T2 = hg[4 * count + p];
+        rp.taux = hf[p]; rp.mu = hf[count + p]; rp.t = hf[2 * count + p];
+        InnerProductProof& ip = rp.ip_proof;
+        ip.n = n;
+        ip.a.elements = &ha[p]; ip.a.length = 1;
+        ip.b.elements = &hb[p]; ip.b.length = 1;
+        ip.c = hf[3 * count + p];
+        ip.x = hf[4 * count + p];
+        ip.L.elements = Lr ? &hL[p * Lr] : nullptr; ip.L.length = Lr;
+        ip.R.elements = Lr ? &hR[p * Lr] : nullptr; ip.R.length = Lr;
+        ip.L_len = Lr;
+    }
+    PointVector Gv = {gen.data(), n}, Hv = {gen.data() + n, n};
+    const ge25519 *g = &gen[2 * n], *h = &gen[2 * n + 1];
+    std::vector<uint8_t> ok1(count), ok2(count);
+    (void)cuda_range_proof_verify(&proofs[0], &V[0], n, &Gv, &Hv, g, h);   // warm-up (pipeline, tables)
+    double t0 = now_s();
+    for (size_t p = 0; p < count; p++) ok1[p] = cuda_range_proof_verify(&proofs[p], &V[p], n, &Gv, &Hv, g, h) ? 1 : 0;
+    const double dt1 = now_s() - t0;
+    if (hipbp_batch_range_proof_verify_host(proofs.data(), V.data(), count, n, &Gv, &Hv, g, h, 1, ok2.data()) !=
+        HIPBP_OK) {
+        fprintf(stderr, "HIP error - %s\n", g_err.c_str());
+        exit(EXIT_FAILURE);
+    }
+    t0 = now_s();
+    BP_EXIT_ON(hipbp_batch_range_proof_verify_host(proofs.data(), V.data(), count, n, &Gv, &Hv, g, h, 1, ok2.data())
+                   == HIPBP_OK ? hipSuccess : hipErrorUnknown);
+    const double dt2 = now_s() - t0;
+    size_t pass = 0, agree = 0;
+    for (size_t p = 0; p < count; p++) {
+        pass += ok1[p];
+        agree += ok1[p] == ok2[p];
+    }
+    printf("cuda_benchmark_range_proof: n=%zu  %zu proofs  cuda_range_proof_verify %.3f ms/call  "
+           "batched (hipbp_batch_range_proof_verify_host) %.1f verifies/s  passes %zu/%zu  verdicts agree %zu/%zu\n",
+           n, count, dt1 / count * 1e3, count / dt2, pass, count, agree, count);
+    fflush(stdout);
 }
 
 }  // extern "C"

@@ -189,6 +189,8 @@ hipError_t msm_pippenger(ge* result, const fe* scal, const ge* P, size_t n, size
 hipError_t msm_pippenger_windows(ge* Sw, const fe* scal, const ge* P, size_t n, int c, int w0, int w1,
                                  const ge* dtab, hipStream_t s);
 hipError_t pippenger_horner(ge* result, const ge* Sw, size_t count, int c, hipStream_t s);
+// Frees the (device, stream) Pippenger workspaces of stream s (after waiting for its work).
+hipError_t pippenger_release(hipStream_t s);
 
 
 

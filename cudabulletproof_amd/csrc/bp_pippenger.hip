@@ -24,6 +24,7 @@
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 
+#include <algorithm>
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -362,8 +363,10 @@ __global__ __launch_bounds__(PTPB, 4) void k_pip_step(int t, const unsigned* __r
     const bool first = t == 0;
     const uint32_t total = off[nb - 1] + pad[nb - 1];
     const uint32_t groups = total >> 2;   // lists are padded to x4
-    const size_t oct_max = nb / 8 < 16384 ? nb / 8 : 16384;   // 8 groups' lanes <= nb <= grid lanes
-    if (groups <= oct_max) {
+    // the octet path needs 8 lanes per group: every launch has lanes >= nb (pip_buckets), and the
+    // grid-uniform test below keeps 8 groups' lanes within this launch's lanes
+    const size_t oct_max = nb / 8 < 16384 ? nb / 8 : 16384;
+    if (groups <= oct_max && 8 * (size_t)groups <= lanes) {
         const uint32_t pos = (uint32_t)(4 * (k >> 3));
         if (pos >= total) return;   // whole octets leave together
         const uint32_t b = bid[pos];
@@ -823,7 +826,9 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
     const uint32_t* keys32 = k32 ? ws.keys.as<uint32_t>() : nullptr;
     const uint32_t imask = ib >= 32 ? 0xFFFFFFFFu : (uint32_t)((1ull << ib) - 1);
     // step t: layout t -> t + 1, (bid, data)[t & 1] -> [(t + 1) & 1]
-    size_t lanes = (tot0 + 3) / 4;
+    // at least nb lanes in every step (step 0 too: when n < 2^c / 4 the padded total is below
+    // 4 nb), so the octet tail path, which takes up to nb / 8 groups, always has its 8 lanes each
+    size_t lanes = std::max((tot0 + 3) / 4, nb);
     for (int t = 0; t < steps; t++) {
         const int a = t & 1, b = a ^ 1;
         const size_t l0 = (size_t)t * nb, l1 = l0 + nb;
@@ -924,6 +929,34 @@ hipError_t msm_pippenger_windows(ge* Sw, const fe* scal, const ge* P, size_t n, 
     PIP_RET(pip_pair(&pp, s));
     PIP_RET(pip_buckets(pp->lo, scal, P, n, 1, c, w0, w1, s));
     return pip_finish(pp->lo, 1, c, W, w0, w1, Sw, dtab, s);
+}
+
+// Frees stream s's workspace pair on the current device (hipbp_release_stream_workspaces): waits
+// for s and the pair's side stream, frees every buffer, destroys the side stream and events.
+hipError_t pippenger_release(hipStream_t s) {
+    int dev = 0;
+    PIP_RET(hipGetDevice(&dev));
+    PipPair* pp = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_pip_mu);
+        auto it = g_pip.find(std::make_pair(dev, s));
+        if (it == g_pip.end()) return hipSuccess;
+        pp = it->second;
+        g_pip.erase(it);
+    }
+    PIP_RET(hipStreamSynchronize(s));
+    if (pp->hi.side) PIP_RET(hipStreamSynchronize(pp->hi.side));
+    for (PipWs* w : {&pp->hi, &pp->lo}) {
+        for (DBuf* b : {&w->keys_in, &w->keys, &w->vals, &w->temp, &w->start, &w->len[0], &w->len[1], &w->lay,
+                        &w->bq, &w->bid[0], &w->bid[1], &w->Q[0], &w->Q[1], &w->S, &w->V, &w->Sw, &w->Tmid,
+                        &w->maxlen, &w->part})
+            if (b->p) PIP_RET(hipFree(b->p));
+        for (auto& ev : w->ev)
+            if (ev) PIP_RET(hipEventDestroy(ev));
+        if (w->side) PIP_RET(hipStreamDestroy(w->side));
+    }
+    delete pp;
+    return hipSuccess;
 }
 
 // Horner over all W window sums of `count` MSMs (Sw[m W .. m W + W)), on stream s.

@@ -286,6 +286,12 @@ int hipbp_point_tree(ge25519* result, const ge25519* points, size_t n, void* str
  * 4 SoA add (limbwise, no carry), 5 invert (host chain), 6 the product fold alone on the
  * 512-bit t = a || b (fe25519_mul's reduction, curve25519_ops.cu:114-145), 7 fe25519_sq. */
 int hipbp_field_op(int op, fe25519* r, const fe25519* a, const fe25519* b, size_t count, void* stream);
+/* Frees every workspace the library caches for `stream` on the current device (canonical MSM /
+ * point-tree, prover, one-shot verify pipelines, the Pippenger workspace pair with its side stream
+ * and events), after waiting for the stream.  Workspaces otherwise live as long as the process;
+ * a caller that makes short-lived streams calls this before destroying one.  No reference
+ * counterpart. */
+int hipbp_release_stream_workspaces(void* stream);
 /* Wait for `stream`. */
 int hipbp_sync(void* stream);
 

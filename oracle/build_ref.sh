@@ -48,14 +48,39 @@ g++ -O2 -w -fPIC -I"$REF" -D__device__= -c "$HERE/ref/ref_harness.cc" -o ref_har
 g++ -shared -Wl,-Bsymbolic -o "$OUT/libbpref.so" *.o -lcrypto
 echo "built $OUT/libbpref.so"
 
-# Drop-in demonstration: the reference's own test driver and host code,
-# unchanged, linked against OUR libcudabulletproof_hip.so instead of the CUDA objects.
+# The reference's own test driver (complete_bulletproof_test.cu, main() unchanged), three ways.
+# Built with clang's -ftrivial-auto-var-init=pattern so that the driver's own undefined behaviour
+# at its end — complete_bulletproof_test.cu:305 range_proof_free(&large_proof) frees the
+# never-initialised ip_proof of the refused out-of-range proof (generate_range_proof returns early
+# at bulletproof_range_proof.cu:1176-1187 before range_proof_init) — ends the same way on every run:
+# free(0xaaaaaaaaaaaaaaaa) -> SIGSEGV, after all of its output.  (g++ builds leave stack garbage
+# there: the run exits 0, SIGSEGVs or aborts in glibc depending on what the stack held.)
+#   complete_bulletproof_test_cpu   GPU symbols host-emulated by ref_harness.cc (the CPU twin)
+#   complete_bulletproof_test_asan  the same under AddressSanitizer + UBSan (tests/test_dropin.py
+#                                   asserts the report: field_vector_free <- inner_product_proof_free
+#                                   <- main at complete_bulletproof_test.cu:305, no UBSan finding)
+#   complete_bulletproof_test_hip   linked against OUR libcudabulletproof_hip.so (the drop-in)
+CXX=${CXX_PATTERN:-/opt/rocm/llvm/bin/clang++}
+P="-O2 -w -x c++ -fPIC -I$REF -ftrivial-auto-var-init=pattern"
+A="-O1 -g -w -x c++ -fPIC -I$REF -ftrivial-auto-var-init=pattern -fsanitize=address,undefined -fno-omit-frame-pointer"
+for v in p a; do
+    FL=$P; [ $v = a ] && FL=$A
+    for f in curve25519_ops bulletproof_vectors bulletproof_challenge complete_bulletproof_test; do
+        $CXX $FL -c "$REF/$f.cu" -o "${v}_$f.o"
+    done
+    $CXX $FL -include cuda_bulletproof.h -c "$REF/bulletproof_range_proof.cu" -o "${v}_bulletproof_range_proof.o"
+    $CXX $FL -D__device__= -c "$TMP/cuda_range_proof_verify.cu" -o "${v}_crv.o"
+    $CXX ${FL/-x c++/} -D__device__= -c "$HERE/ref/ref_harness.cc" -o "${v}_harness.o"
+done
+DRV="curve25519_ops bulletproof_vectors bulletproof_challenge bulletproof_range_proof complete_bulletproof_test"
+$CXX -o "$OUT/complete_bulletproof_test_cpu" $(for f in $DRV crv harness; do echo p_$f.o; done) -lcrypto
+$CXX -fsanitize=address,undefined -o "$OUT/complete_bulletproof_test_asan" \
+    $(for f in $DRV crv harness; do echo a_$f.o; done) -lcrypto
+echo "built $OUT/complete_bulletproof_test_cpu, $OUT/complete_bulletproof_test_asan"
 LIB="$(cd "$HERE/.." && pwd)/cudabulletproof_amd"
 if [ -f "$LIB/libcudabulletproof_hip.so" ]; then
-    g++ $F -c "$REF/complete_bulletproof_test.cu" -o test_main.o
     gcc -O2 -fPIC -c "$HERE/ref/det_rand.c" -o det_rand.o
-    g++ -o "$OUT/complete_bulletproof_test_hip" curve25519_ops.o bulletproof_vectors.o bulletproof_challenge.o \
-        bulletproof_range_proof.o test_main.o det_rand.o -L"$LIB" -lcudabulletproof_hip \
-        -Wl,-rpath,'$ORIGIN/../../cudabulletproof_amd' -lcrypto
+    $CXX -o "$OUT/complete_bulletproof_test_hip" $(for f in $DRV; do echo p_$f.o; done) det_rand.o \
+        -L"$LIB" -lcudabulletproof_hip -Wl,-rpath,'$ORIGIN/../../cudabulletproof_amd' -lcrypto
     echo "built $OUT/complete_bulletproof_test_hip"
 fi

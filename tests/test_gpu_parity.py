@@ -78,6 +78,73 @@ def test_msm_4096_survey_digest(bp, oracle):
     assert d8(bp.cuda_point_vector_multi_scalar_mul(s, P)) == "17b524ff179c621d"
 
 
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 16, 17, 64])
+def test_msm_shared_matches_reference(bp, golden, n):
+    """cuda_point_vector_multi_scalar_mul_shared (cuda_bulletproof.h:17): for n <= 64 the reference's
+    shared-memory kernel defines the canonical tree (kernels.cu:141-168) — the golden results."""
+    d = golden("msm")
+    assert np.array_equal(bp.cuda_point_vector_multi_scalar_mul(d[f"s{n}"], d[f"P{n}"], shared=True), d[f"canon{n}"])
+
+
+@pytest.mark.parametrize("n", [65, 257])
+def test_msm_shared_large_n_vs_oracle(bp, oracle, n):
+    """n > 64: the reference's _shared delegates to the standard path (kernels.cu:122-126)."""
+    rng = np.random.default_rng(3 * n)
+    P = oracle.base_points(n, 13)
+    s = rand_fe(rng, n)
+    s[::6] = 0
+    want = oracle.msm_canon(s, P)
+    assert np.array_equal(bp.cuda_point_vector_multi_scalar_mul(s, P, shared=True), want)
+    assert np.array_equal(bp.cuda_point_vector_multi_scalar_mul(s, P), want)
+
+
+def test_cuda_benchmark_hooks_run(bp, capfd):
+    """The four cuda_benchmark_* hooks the reference declares (cuda_bulletproof.h:81-84) run on the
+    GPU and print one line each; the range-proof one verifies real GPU-prover proofs through the
+    reference's per-proof entry point and the batched host-struct one, whose verdicts must agree."""
+    import ctypes
+    L = bp.lib()
+    L.cuda_benchmark_multi_scalar_mul(ctypes.c_int(2), ctypes.c_size_t(64))
+    L.cuda_benchmark_inner_product(ctypes.c_int(2), ctypes.c_size_t(1000))
+    L.cuda_benchmark_field_operations(ctypes.c_int(2), ctypes.c_size_t(4096))
+    L.cuda_benchmark_range_proof(ctypes.c_int(8), ctypes.c_size_t(16))
+    L.cuda_benchmark_range_proof(ctypes.c_int(4), ctypes.c_size_t(64))
+    out = capfd.readouterr().out.splitlines()
+    assert sum(l.startswith("cuda_benchmark_multi_scalar_mul: n=64") for l in out) == 1
+    assert sum(l.startswith("cuda_benchmark_inner_product: n=1000") for l in out) == 1
+    assert sum(l.startswith("cuda_benchmark_field_operations:") for l in out) == 3
+    rp = [l for l in out if l.startswith("cuda_benchmark_range_proof:")]
+    assert len(rp) == 2, out
+    assert "n=16  8 proofs" in rp[0] and "verdicts agree 8/8" in rp[0], rp[0]
+    assert "n=64  4 proofs" in rp[1] and "verdicts agree 4/4" in rp[1], rp[1]
+
+
+def test_release_stream_workspaces(bp, oracle):
+    """hipbp_release_stream_workspaces frees a stream's cached workspaces; the next call on that
+    stream rebuilds them and gives the same bits (workspaces per short-lived stream)."""
+    import torch
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    n = 3000
+    rng = np.random.default_rng(77)
+    P = oracle.base_points(n, 21)
+    s = rand_fe(rng, n)
+    want_p = oracle.msm_pippenger(s, P, 12)
+    want_c = oracle.msm_canon(s[:300], P[:300])
+    sd, Pd = T(s), T(P)
+    for _ in range(3):
+        st = torch.cuda.Stream(dev)
+        out = torch.zeros(2, 16, dtype=torch.int64, device=dev)
+        torch.cuda.synchronize()
+        bp.msm_pippenger(out[0], sd, Pd, 12, stream=st)
+        bp.msm(out[1], sd[:300], Pd[:300], stream=st)
+        bp.release_stream_workspaces(st)   # waits for st first
+        got = out.cpu().numpy().view(np.uint64)
+        assert np.array_equal(got[0], want_p) and np.array_equal(got[1], want_c)
+        del st
+    bp.release_stream_workspaces(None)   # the null stream's workspaces (rebuilt by the next call on it)
+
+
 def test_msm_length_mismatch_leaves_result(bp, capfd):
     import ctypes
     s = np.zeros((3, 4), np.uint64)
@@ -831,6 +898,39 @@ def test_msm_pippenger_degenerate_scalars(bp, oracle, kind, n):
     bp.msm_pippenger(out, T(s), T(P), c)
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy().view(np.uint64), oracle.msm_pippenger(s, P, c))
+
+
+@pytest.mark.parametrize("n,c", [(512, 12), (450, 12), (550, 12), (30, 8), (7, 5)])
+def test_msm_pippenger_sparse_buckets_all_apis(bp, oracle, n, c):
+    """n ~ 0.1-0.13 * 2^c: most buckets hold 0 or 1 point, so the padded step-0 layout has fewer
+    than nb / 4 groups of lanes but up to nb / 8 groups — the octet tail path's lane count at step
+    0.  Single call, a batch of 3 and a window split against the oracle."""
+    import torch
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    rng = np.random.default_rng(n * 13 + c)
+    P = oracle.base_points(n, 17)
+    count = 3
+    s = rand_fe(rng, count * n)
+    want = [oracle.msm_pippenger(s[m * n:(m + 1) * n], P, c) for m in range(count)]
+    out = torch.zeros(16, dtype=torch.int64, device=dev)
+    bp.msm_pippenger(out, T(s[:n]), T(P), c)
+    bo = torch.zeros(count, 16, dtype=torch.int64, device=dev)
+    bp.msm_pippenger_batch(bo, T(s), T(P), c)
+    W = (256 + c - 1) // c
+    Sw = torch.zeros(W, 16, dtype=torch.int64, device=dev)
+    h = W // 2
+    bp.msm_pippenger_windows(Sw, T(s[:n]), T(P), 0, h, c)
+    bp.msm_pippenger_windows(Sw, T(s[:n]), T(P), h, W, c)
+    wo = torch.zeros(1, 16, dtype=torch.int64, device=dev)
+    bp.msm_pippenger_horner(wo, Sw, c)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint64), want[0])
+    got = bo.cpu().numpy().view(np.uint64)
+    for m in range(count):
+        assert np.array_equal(got[m], want[m]), m
+    assert np.array_equal(wo.cpu().numpy().view(np.uint64)[0], want[0])
+    assert np.array_equal(Sw.cpu().numpy().view(np.uint64), oracle.pippenger_windows(s[:n], P, c, 0, W))
 
 
 # ----------------------------------------------------------------------------- batched MSM

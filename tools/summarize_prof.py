@@ -86,7 +86,9 @@ def main():
     stats = list(csv.DictReader(open(os.path.join(base, "trace", "run_kernel_stats.csv"))))
     lines = [f"# rocprofv3 summary — {tag}", "",
              "Command: `tools/profile.sh " + tag + "` on one MI355X "
-             "(bench.py --steps 6 --warmup 2 --no-cpu --no-ipa --no-prove --msm-log2 $MSM_LOG2 under rocprofv3, defaults otherwise).", "",
+             "(bench.py --steps 20 --warmup 5 --no-cpu --no-ipa --no-prove --no-shard --no-host --no-check --no-h2d "
+             "--msm-log2 $MSM_LOG2 under rocprofv3: the headline configuration — B = 1024, n = 64, K = 22 prefix "
+             "tables, two pipelines — otherwise defaults).", "",
              "## Kernel trace (`rocprofv3 --kernel-trace --stats`)", "",
              "| kernel | calls | avg ms | min ms | max ms | % time |", "|---|---|---|---|---|---|"]
     for r in stats:
@@ -103,6 +105,7 @@ def main():
     lines += ["", "## Steady-state launches (largest grid) from the kernel trace", "",
               "| kernel | launches | grid | avg ms (rocprofv3) | avg ms (bench.py HIP events, same run) |",
               "|---|---|---|---|---|"]
+    trace_ms = {}
     for kern in ("k_terms", "k_msm_points", "k_combine", "k_tree"):
         ds = [r for r in trace if short(r["Kernel_Name"]) == kern]
         if not ds:
@@ -111,6 +114,7 @@ def main():
         ss = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in ds if int(r["Grid_Size_X"]) == g]
         ev = f"{ev_ms:.3f}" if kern == ev_kern and ev_ms else "—"
         lines.append(f"| {kern} | {len(ss)} | {g} | {mean(ss) / 1e6:.3f} | {ev} |")
+        trace_ms[kern] = mean(ss) / 1e6
     os.makedirs(os.path.join(ROOT, "profiles", f"raw_{tag}"), exist_ok=True)
     for src, dst in (("trace/run_kernel_stats.csv", "kernel_stats.csv"), ("bench_trace.json", "bench_trace.json")):
         try:
@@ -143,7 +147,7 @@ def main():
         cyc_per_instr = (grbm / 8) / (vi / 1024) if vi else float("nan")   # 1024 SIMDs
         traffic[kern] = {"bytes_per_launch": hbm, "fetch_kb": fk, "write_kb": wk, "launches": len(f),
                          "valu_instr_per_wave": vi / waves if waves else None, "valu_instr_per_launch": vi,
-                         "eff_clock_ghz": clock}
+                         "eff_clock_ghz": clock, "rocprof_avg_ms": trace_ms.get(kern)}
         lines.append(f"| {kern} | {len(f)} | {f[0]['grid']} | {f[0]['vgpr']} | {fk:.0f} | {wk:.0f} | {hbm:.3e} | "
                      f"{waves:.0f} | {vi / waves:.0f} | {si / waves:.0f} | {li / waves:.0f} | {clock:.2f} | "
                      f"{cyc_per_instr:.2f} |")
@@ -167,8 +171,8 @@ def main():
             lines.append(f"| {kern} | {vb:.1f} | {vu:.1f} | {i32:.0f} | {i64:.0f} | {v2:.0f} |")
     lines += ["", "Notes:",
               "- `VALU cyc/instr/SIMD` = kernel cycles (GRBM_GUI_ACTIVE/8) / (SQ_INSTS_VALU / 1024 SIMDs): the "
-              "issue interval per SIMD; ~4.3 is the measured VOP3 issue floor on gfx950 at 8 waves/SIMD "
-              "(tools/ubench_int.hip), so values near it mean the kernel is VALU-issue bound.",
+              "issue interval per SIMD; compare with the issue-cost model of the hot loop's opcode mix "
+              "(profiles/valu_issue_model.json: tools/ubench_issue.hip costs in shader-clock cycles x tools/valu_model.py).",
               "- HBM bytes apply the gfx950 FETCH_SIZE x2 correction; the loads here are 16-B-per-lane "
               "(dwordx4) gathers of 128-B points, partly served by L2/MALL, so treat absolute bytes as approximate.",
               "- VALUBusy = 100 * SQ_ACTIVE_INST_VALU / CU_NUM / GRBM_GUI_ACTIVE (rocprofv3 derived metric): the share "
@@ -180,7 +184,7 @@ def main():
     try:
         bc = json.loads(open(os.path.join(base, "bench_valu.json")).read().strip().splitlines()[-1])["config"]
         cfg = {"batch_per_gpu": bc["batch_per_gpu"], "n": bc["n"],
-               "prefix_bits": (bc.get("prefix_tables") or {}).get("bits", 0)}
+               "prefix_bits": (bc.get("prefix_tables") or {}).get("bits", 0), "pipelines": bc.get("pipelines")}
     except (OSError, ValueError, KeyError, IndexError):
         pass
     json.dump({"tag": tag, "config": cfg, **traffic}, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"),
