@@ -172,8 +172,12 @@ void launch_init_tables(ge* dtab, fe* two_i, int nmax, hipStream_t s);
 // Prefix tables (SlotDev::ptab) of the bases G[0..n), H[0..n), h, g (g nullable: its rows are
 // left unwritten): tab[(2n + 2) << K].
 void launch_prefix_tables(ge* tab, const ge* G, const ge* H, const ge* h, const ge* g, int n, int K, hipStream_t s);
+// quad: the drain-tick form (scalar-multiplication regions' items take 4 lanes each, k_terms<true>)
 void launch_terms(const RegionList& rl, const SlotDev* slots, const ge* G, const ge* H, const ge* g, const ge* h,
-                  const ge* dtab, const fe* two_i, hipStream_t s);
+                  const ge* dtab, const fe* two_i, hipStream_t s, bool quad = false);
+inline bool region_is_sm(int kind) {
+    return kind == RK_STAGE0 || kind == RK_ROUND || kind == RK_FINAL_TERMS || kind == RK_M3;
+}
 
 // Generic canonical-tree MSM.  perm [m] / bins [MSM_BINS] (nullable): workspace of the
 // counting sort that groups items of equal chain length into the same waves (m >= MSM_SORT_MIN).

@@ -7,6 +7,7 @@
 // the reference's order, because the arithmetic is not associative.
 #include "bp_kernels.h"
 #include "ge25519_dev.h"
+#include "ge25519_quad.h"
 #include "sha256_dev.h"
 
 namespace bp {
@@ -761,6 +762,12 @@ void launch_lane_sort(const LaneSortPlan& plan, unsigned* bins, unsigned* offs, 
 // The RK_TREE region (if any) comes first and spans whole blocks: each block folds TPB/n
 // segments of the batch's 2B MSMs with the canonical tree of k_tree, barriers block-uniform;
 // its LDS is the q-operand array (no scalar multiplication runs in those blocks).
+//
+// QUAD (the drain ticks, Pipeline::push): every scalar-multiplication item takes a lane quad
+// instead of a lane (region items are 4 lanes each) and runs sm_quad — 3 product latencies per
+// point operation instead of 9, for ticks too small to fill the SIMDs, whose time is one
+// scalar-multiplication chain's latency.  The same operations, so the same bits.
+template <bool QUAD>
 __global__ __launch_bounds__(TPB, BP_TERMS_OCC) void k_terms(RegionList rl, const SlotDev* __restrict__ slots,
                                                const ge* __restrict__ G, const ge* __restrict__ H,
                                                const ge* __restrict__ g, const ge* __restrict__ h,
@@ -806,6 +813,7 @@ __global__ __launch_bounds__(TPB, BP_TERMS_OCC) void k_terms(RegionList rl, cons
         jb.base = -1;
         bool live = true;
         uint32_t li = (uint32_t)l;   // < 2^32: Pipeline::push keeps a tick below 2^32 lanes
+        if (QUAD) li >>= 2;          // the quad's item
         if (rg.kind == RK_STAGE0) {
             const uint32_t it = stage0_item(sd, li);
             live = it != UINT32_MAX && stage0_job(sd, it, G, H, g, h, jb);
@@ -821,8 +829,13 @@ __global__ __launch_bounds__(TPB, BP_TERMS_OCC) void k_terms(RegionList rl, cons
         }
         if (live) {
             const ge* pt = (sd.ptab && jb.base >= 0) ? sd.ptab + ((size_t)jb.base << sd.pbits) : nullptr;
-            ge t = scalarmult<true>(jb.s, jb.P, &qs[threadIdx.x], dtab, pt, pt ? sd.pbits : 0);
-            *jb.dst = jb.dev_norm ? ge_norm_dev(t) : ge_norm_host(t);
+            if (QUAD) {
+                const ge t = sm_quad(jb.s, jb.P, dtab, pt, pt ? sd.pbits : 0);
+                if ((threadIdx.x & 3) == 0) *jb.dst = jb.dev_norm ? ge_norm_dev(t) : ge_norm_host(t);
+            } else {
+                ge t = scalarmult<true>(jb.s, jb.P, &qs[threadIdx.x], dtab, pt, pt ? sd.pbits : 0);
+                *jb.dst = jb.dev_norm ? ge_norm_dev(t) : ge_norm_host(t);
+            }
         }
     }
 }
@@ -830,8 +843,10 @@ __global__ __launch_bounds__(TPB, BP_TERMS_OCC) void k_terms(RegionList rl, cons
 static inline unsigned nblk(size_t items) { return (unsigned)((items + TPB - 1) / TPB); }
 
 void launch_terms(const RegionList& rl, const SlotDev* slots, const ge* G, const ge* H, const ge* g, const ge* h,
-                  const ge* dtab, const fe* two_i, hipStream_t s) {
-    if (rl.total) k_terms<<<nblk(rl.total), TPB, 0, s>>>(rl, slots, G, H, g, h, dtab, two_i);
+                  const ge* dtab, const fe* two_i, hipStream_t s, bool quad) {
+    if (!rl.total) return;
+    if (quad) k_terms<true><<<nblk(rl.total), TPB, 0, s>>>(rl, slots, G, H, g, h, dtab, two_i);
+    else k_terms<false><<<nblk(rl.total), TPB, 0, s>>>(rl, slots, G, H, g, h, dtab, two_i);
 }
 
 

@@ -31,6 +31,7 @@
 
 #include "bp_kernels.h"
 #include "ge25519_dev.h"
+#include "ge25519_quad.h"
 
 namespace bp {
 
@@ -340,10 +341,6 @@ __global__ __launch_bounds__(PTPB) void k_pip_bidfill(const uint32_t* __restrict
 }
 
 // (min 4 waves per SIMD: the compiler keeps it at 128 VGPRs)
-template <bool DBL>
-__device__ __forceinline__ ge ge_op_quad(const ge& p, const ge& q);
-template <int CTRL>
-__device__ __forceinline__ ge ge_row_move(const ge& a);
 
 // Bucket-tree step: each lane reduces one aligned 4-element group of a bucket's list (2 levels).
 // When few groups remain (the deep buckets' tail steps, a wave-uniform test on the device-side
@@ -452,58 +449,7 @@ __global__ __launch_bounds__(PTPB) void k_pip_window(const ge* __restrict__ V, i
     if (t == 0) Sw[(size_t)(blockIdx.x / Wp) * W + w0 + blockIdx.x % Wp] = sh[0];
 }
 
-// ---- latency-bound chains: one point operation per lane QUAD.  ge25519_add / the doubling are
-// three dependent product stages — {A, B, T1 T2, Z1 Z2} (squares for a doubling), then C = (T1 T2) k,
-// then {E F, G H, F G, E H} — and the four products of a stage are independent, so the quad's
-// lanes form one each (operands selected per lane) and swap results over DPP: 3 product
-// latencies per operation instead of 9 on one lane.  Every value is the very product ge_add /
-// ge_dbl forms, so the bits are theirs.
-template <int SRC>
-__device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, SRC * 0x55, 0xF, 0xF, true);
-}
-template <int SRC>
-__device__ __forceinline__ fe fe_quad_bcast(const fe& a) {
-    fe r;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        uint32_t lo = quad_bcast<SRC>((uint32_t)a.v[i]), hi = quad_bcast<SRC>((uint32_t)(a.v[i] >> 32));
-        r.v[i] = (uint64_t)lo | ((uint64_t)hi << 32);
-    }
-    return r;
-}
-// (bit masks, not a ternary chain: the compiler turned that into a private array indexed by q,
-// i.e. scratch stores and loads inside the dependent chains)
-__device__ __forceinline__ fe fe_sel4(int q, const fe& a, const fe& b, const fe& c, const fe& d) {
-    const uint64_t m0 = 0ull - (uint64_t)(q & 1), m1 = 0ull - (uint64_t)((q >> 1) & 1);
-    fe r;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const uint64_t ab = a.v[i] ^ ((a.v[i] ^ b.v[i]) & m0), cd = c.v[i] ^ ((c.v[i] ^ d.v[i]) & m0);
-        r.v[i] = ab ^ ((ab ^ cd) & m1);
-    }
-    return r;
-}
-// DBL: add(p, p) (q ignored); else add(p, q).  p, q replicated over the quad; result replicated.
-template <bool DBL>
-__device__ __forceinline__ ge ge_op_quad(const ge& p, const ge& q) {
-    const int qd = threadIdx.x & 3;
-    const fe ymx = fe_sub(p.Y, p.X), ypx = fe_add(p.Y, p.X);
-    fe r1;
-    if (DBL) {
-        r1 = fe_sq(fe_sel4(qd, ymx, ypx, p.T, p.Z));
-    } else {
-        const fe qymx = fe_sub(q.Y, q.X), qypx = fe_add(q.Y, q.X);
-        r1 = fe_mul(fe_sel4(qd, ymx, ypx, p.T, p.Z), fe_sel4(qd, qymx, qypx, q.T, q.Z));
-    }
-    const fe A = fe_quad_bcast<0>(r1), B = fe_quad_bcast<1>(r1), CT = fe_quad_bcast<2>(r1);
-    fe D = fe_quad_bcast<3>(r1);
-    const fe C = fe_mul(CT, k_const());
-    D = fe_add(D, D);
-    const fe E = fe_sub(B, A), F = fe_sub(D, C), G = fe_add(D, C), H = fe_add(B, A);
-    const fe r3 = fe_mul(fe_sel4(qd, E, G, F, E), fe_sel4(qd, F, H, G, H));
-    return ge{fe_quad_bcast<0>(r3), fe_quad_bcast<1>(r3), fe_quad_bcast<2>(r3), fe_quad_bcast<3>(r3)};
-}
+// ---- latency-bound chains: one point operation per lane QUAD (ge25519_quad.h).
 
 // ---- the Horner chain: one point operation per 16-lane row, one product per lane quad.
 // fe_mul_q4: the product's 64 word products split over the quad by rows — lane rb forms
@@ -621,23 +567,6 @@ __global__ __launch_bounds__(64) void k_pip_horner(const ge* __restrict__ Sw, in
         }
     }
     if (threadIdx.x == 0) *out = T;
-}
-
-// A point moved across lane quads of one DPP row: CTRL 0x114 (row_shr:4, lane l takes l-4) or
-// 0x104 (row_shl:4, lane l takes l+4).
-template <int CTRL>
-__device__ __forceinline__ ge ge_row_move(const ge& a) {
-    auto mv = [](const fe& f) {
-        fe r;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)f.v[i], CTRL, 0xF, 0xF, true);
-            uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(f.v[i] >> 32), CTRL, 0xF, 0xF, true);
-            r.v[i] = (uint64_t)lo | ((uint64_t)hi << 32);
-        }
-        return r;
-    };
-    return ge{mv(a.X), mv(a.Y), mv(a.Z), mv(a.T)};
 }
 
 // chunk k of window w (one lane octet = two quads): buckets kM .. kM+M-1 -> V = S + (kM) R

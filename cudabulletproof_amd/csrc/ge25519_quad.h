@@ -1,0 +1,125 @@
+// ge25519_quad.h — point operations spread over a lane QUAD, for latency-bound chains (the
+// Pippenger chunks / window trees / tail steps, and the verify pipeline's drain ticks).
+//
+// ge25519_add (curve25519_ops.cu:326-378) is three dependent product stages — {A, B, T1 T2,
+// Z1 Z2} (squares for a doubling), then C = (T1 T2) k, then {E F, G H, F G, E H} — and the four
+// products of a stage are independent, so the quad's lanes form one each (operands selected per
+// lane) and swap results over DPP: 3 product latencies per operation instead of 9 on one lane.
+// Every value is the very product ge_add / ge_dbl forms, so the bits are theirs.  Points are
+// replicated over the quad's four lanes on entry and on exit.
+#pragma once
+#include "ge25519_dev.h"
+
+namespace bp {
+
+template <int SRC>
+__device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, SRC * 0x55, 0xF, 0xF, true);
+}
+template <int SRC>
+__device__ __forceinline__ fe fe_quad_bcast(const fe& a) {
+    fe r;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        uint32_t lo = quad_bcast<SRC>((uint32_t)a.v[i]), hi = quad_bcast<SRC>((uint32_t)(a.v[i] >> 32));
+        r.v[i] = (uint64_t)lo | ((uint64_t)hi << 32);
+    }
+    return r;
+}
+// (bit masks, not a ternary chain: the compiler turned that into a private array indexed by q,
+// i.e. scratch stores and loads inside the dependent chains)
+__device__ __forceinline__ fe fe_sel4(int q, const fe& a, const fe& b, const fe& c, const fe& d) {
+    const uint64_t m0 = 0ull - (uint64_t)(q & 1), m1 = 0ull - (uint64_t)((q >> 1) & 1);
+    fe r;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint64_t ab = a.v[i] ^ ((a.v[i] ^ b.v[i]) & m0), cd = c.v[i] ^ ((c.v[i] ^ d.v[i]) & m0);
+        r.v[i] = ab ^ ((ab ^ cd) & m1);
+    }
+    return r;
+}
+__device__ __forceinline__ fe fe_sel(bool c, const fe& a, const fe& b) {   // c ? a : b, as masks
+    const uint64_t m = 0ull - (uint64_t)c;
+    fe r;
+#pragma unroll
+    for (int i = 0; i < 4; i++) r.v[i] = b.v[i] ^ ((a.v[i] ^ b.v[i]) & m);
+    return r;
+}
+
+// Stages 2 and 3 of ge25519_add from the quad's stage-1 products (lane qd holds product qd of
+// {A, B, T1 T2, Z1 Z2}); the result replicated over the quad.
+__device__ __forceinline__ ge ge_quad_finish(const fe& r1) {
+    const int qd = threadIdx.x & 3;
+    const fe A = fe_quad_bcast<0>(r1), B = fe_quad_bcast<1>(r1), CT = fe_quad_bcast<2>(r1);
+    fe D = fe_quad_bcast<3>(r1);
+    const fe C = fe_mul(CT, k_const());
+    D = fe_add(D, D);
+    const fe E = fe_sub(B, A), F = fe_sub(D, C), G = fe_add(D, C), H = fe_add(B, A);
+    const fe r3 = fe_mul(fe_sel4(qd, E, G, F, E), fe_sel4(qd, F, H, G, H));
+    return ge{fe_quad_bcast<0>(r3), fe_quad_bcast<1>(r3), fe_quad_bcast<2>(r3), fe_quad_bcast<3>(r3)};
+}
+
+// DBL: add(p, p) (q ignored); else add(p, q).  p, q replicated over the quad; result replicated.
+template <bool DBL>
+__device__ __forceinline__ ge ge_op_quad(const ge& p, const ge& q) {
+    const int qd = threadIdx.x & 3;
+    const fe ymx = fe_sub(p.Y, p.X), ypx = fe_add(p.Y, p.X);
+    fe r1;
+    if (DBL) {
+        r1 = fe_sq(fe_sel4(qd, ymx, ypx, p.T, p.Z));
+    } else {
+        const fe qymx = fe_sub(q.Y, q.X), qypx = fe_add(q.Y, q.X);
+        r1 = fe_mul(fe_sel4(qd, ymx, ypx, p.T, p.Z), fe_sel4(qd, qymx, qypx, q.T, q.Z));
+    }
+    return ge_quad_finish(r1);
+}
+
+// A point moved across lane quads of one DPP row: CTRL 0x114 (row_shr:4, lane l takes l-4) or
+// 0x104 (row_shl:4, lane l takes l+4).
+template <int CTRL>
+__device__ __forceinline__ ge ge_row_move(const ge& a) {
+    auto mv = [](const fe& f) {
+        fe r;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)f.v[i], CTRL, 0xF, 0xF, true);
+            uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(f.v[i] >> 32), CTRL, 0xF, 0xF, true);
+            r.v[i] = (uint64_t)lo | ((uint64_t)hi << 32);
+        }
+        return r;
+    };
+    return ge{mv(a.X), mv(a.Y), mv(a.Z), mv(a.T)};
+}
+
+// ge25519_scalarmult (curve25519_ops.cu:397-415) of one quad: s and P replicated over the quad's
+// lanes (quads of one wave may hold different scalars).  The per-lane unified loop of
+// sm_lane_loop: every step is one ge25519_add(r, q) with q = r (the doubling) or P, chosen per
+// quad; the doubling's stage-1 products are the squares (Y-X)^2, (Y+X)^2, T^2, Z^2 as
+// fe_mul(x, x) (== fe_sq(x), the same 512-bit product).  Each lane keeps only its own q-side
+// operand of P.  Leading zeros from dtab, or the K-bit prefix table of the base (ptab) as
+// scalarmult does; the result replicated over the quad.
+__device__ __forceinline__ ge sm_quad(const fe& s, const ge& P, const ge* __restrict__ dtab, const ge* ptab, int K) {
+    const int qd = threadIdx.x & 3;
+    const fe qs = fe_sel4(qd, fe_sub(P.Y, P.X), fe_add(P.Y, P.X), P.T, P.Z);
+    const int lz = fe_clz256(s);
+    const bool pre = K > 0 && lz < K && ptab != nullptr;
+    ge r = *(pre ? &ptab[prefix_index(s, K)] : &dtab[lz]);
+    int i = pre ? 255 - K : 255 - lz;   // index of the pending bit
+    BitStream bs = bs_init(s, i < 0 ? 0 : i);
+    uint32_t bit = i >= 0 ? bs_next(bs) : 0;
+    bool add_phase = false;   // false: next op doubles; true: next op adds P
+    while (i >= 0) {
+        const fe x1 = fe_sel4(qd, fe_sub(r.Y, r.X), fe_add(r.Y, r.X), r.T, r.Z);
+        r = ge_quad_finish(fe_mul(x1, fe_sel(add_phase, qs, x1)));
+        if (!add_phase && bit) {
+            add_phase = true;
+        } else {
+            add_phase = false;
+            i--;
+            bit = bs_next(bs);
+        }
+    }
+    return r;
+}
+
+}  // namespace bp

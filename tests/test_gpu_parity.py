@@ -1163,6 +1163,108 @@ def test_pipeline_prefix_tables_same_bits(bp, oracle, n, B, mode, K):
             assert ok[p] == okr and np.array_equal(P[p], Pr), p
 
 
+def _pipeline_outputs(bp, n, B, mode, arrays, G, H, g, h, Pg, bits=0, gens=None, pushes=1):
+    """One pipeline over `pushes` copies of the batch: ok, P, check, flags, poly of the last."""
+    import torch
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    pipe = bp.VerifyPipeline(B, n, T(G), T(H), T(h), range_mode=mode, g=T(g) if mode == 2 else None)
+    if gens is not None:
+        pipe.use_gens(gens)
+    elif bits:
+        pipe.prefix_tables(bits)
+    batch = bp.RangeProofBatch.from_numpy(n, arrays, dev)
+    res = []
+    for _ in range(pushes):
+        o = [torch.zeros(B, dtype=torch.uint8, device=dev), torch.zeros(B, 16, dtype=torch.int64, device=dev),
+             torch.zeros(B, 16, dtype=torch.int64, device=dev), torch.zeros(B, dtype=torch.uint8, device=dev),
+             torch.zeros(B, 4, 16, dtype=torch.int64, device=dev)]
+        if mode == 0:
+            pipe.push(batch, o[0], None, o[2], P_in=Pg)
+        elif mode == 1:
+            pipe.push(batch, o[0], o[1], o[2])
+        else:
+            pipe.push(batch, o[0], o[1], o[2], flags_out=o[3], poly_out=o[4])
+        res.append(o)
+    pipe.flush()
+    torch.cuda.synchronize()
+    pipe.close()
+    return [[x.cpu() for x in o] for o in res]
+
+
+def _sample_vs_oracle(oracle, n, B, arrays, ok, P, G, H, g, h, step=5):
+    for p in range(0, B, step):
+        head = np.concatenate([arrays[k][p] for k in ("V", "A", "S", "T1", "T2")] +
+                              [np.zeros(8, np.uint64), arrays["t"][p], arrays["c"][p], arrays["x"][p]])
+        okr, Pr, _, _, _ = oracle.cuda_range_proof_verify(head, arrays["V"][p], n, arrays["a"][p], arrays["b"][p],
+                                                          arrays["L"][p], arrays["R"][p], G, H, g, h)
+        assert ok[p] == okr and np.array_equal(P[p], Pr), p
+
+
+@pytest.mark.parametrize("n,B,mode,K,pushes", [(16, 70, 1, 0, 1), (64, 66, 1, 12, 2), (16, 9, 2, 5, 1),
+                                               (64, 20, 2, 0, 3), (4, 5, 1, 1, 1), (16, 6, 0, 9, 2),
+                                               (1, 3, 1, 0, 1), (64, 1, 1, 0, 1)])
+def test_pipeline_quad_ticks_same_bits(bp, oracle, monkeypatch, n, B, mode, K, pushes):
+    """The drain-tick form (k_terms<true>: every scalar multiplication on a lane quad, sm_quad)
+    forced on every tick (HIPBP_QUAD=1) gives bit-identical verdicts, P, check points, mode-2
+    flags and polynomial sides to the lane form forced everywhere (HIPBP_QUAD=0): every region
+    kind, with and without prefix tables, batches in flight together; a sample equals the oracle."""
+    from cudabulletproof_amd import synth
+    G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+    g, h = oracle.gh()
+    arrays = synth.proofs(B, n, seed=70 + n + K + B)
+    rng = np.random.default_rng(B + K)
+    arrays["taux"] = rand_fe(rng, B, top=False)
+    arrays["mu"] = rand_fe(rng, B, top=False)
+    arrays["t"][0] = 0                                  # zero scalar: 256 identity doublings
+    if B > 2:
+        arrays["x"][1, 1:] = 0                           # a short fold scalar: long leading-zero run
+    arrays["a"][:, 0] = arrays["t"]
+    arrays["c"][:] = arrays["t"]
+    import torch
+    Pg = torch.from_numpy(oracle.base_points(B, 9).view(np.int64)).to("cuda:0")
+    outs = []
+    for q in ("0", "1"):
+        monkeypatch.setenv("HIPBP_QUAD", q)
+        outs.append(_pipeline_outputs(bp, n, B, mode, arrays, G, H, g, h, Pg, bits=K, pushes=pushes))
+    for oa, ob in zip(*outs):
+        for a, b in zip(oa, ob):
+            assert torch.equal(a, b)
+    if mode == 1:
+        o = outs[1][-1]
+        _sample_vs_oracle(oracle, n, B, arrays, o[0].numpy().astype(bool), o[1].numpy().view(np.uint64), G, H, g, h)
+
+
+@pytest.mark.parametrize("n,B,K", [(16, 70, 22), (64, 40, 20)])
+def test_pipeline_headline_table_width_same_bits(bp, oracle, n, B, K):
+    """The headline's table width (bench.py: K = 22 at n = 64, 70 GB): prefix tables of K = 20-22
+    bits through a generator set (as bench.py uses them) give the table-free pipeline's bits,
+    and a sample equals the oracle (n = 16 at K = 22: 18 GB of tables; n = 64 at K = 20: 17 GB)."""
+    import torch
+    from cudabulletproof_amd import synth
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+    g, h = oracle.gh()
+    arrays = synth.proofs(B, n, seed=300 + K)
+    arrays["t"][0] = 0
+    arrays["t"][1, 3] = np.uint64(1) << np.uint64(63 - K)   # exactly K leading zeros
+    arrays["t"][1, :3] = 0
+    arrays["a"][:, 0] = arrays["t"]
+    arrays["c"][:] = arrays["t"]
+    plain = _pipeline_outputs(bp, n, B, 1, arrays, G, H, g, h, None, pushes=2)
+    gens = bp.Generators(n, T(G), T(H), T(g), T(h), prefix_bits=K)
+    tab = _pipeline_outputs(bp, n, B, 1, arrays, G, H, g, h, None, gens=gens, pushes=2)
+    gens.close()
+    torch.cuda.empty_cache()
+    for oa, ob in zip(plain, tab):
+        for a, b in zip(oa, ob):
+            assert torch.equal(a, b)
+    o = tab[-1]
+    _sample_vs_oracle(oracle, n, B, arrays, o[0].numpy().astype(bool), o[1].numpy().view(np.uint64), G, H, g, h,
+                      step=7)
+
+
 def test_prefix_tables_reject_busy_and_bad_bits(bp, oracle):
     import torch
     from cudabulletproof_amd import synth
