@@ -37,6 +37,50 @@ for k, (n, t) in sorted(tot.items(), key=lambda x: -x[1][1]):
 out.append(f"| **all kernels** |  | {all_ns / 1e6:.3f} |  | {all_ns / nmsm / 1e6:.3f} | 100 |")
 out += ["", "Per MSM, the kernel time adds to more than the wall time of one call because the top part's chunks, "
         "window trees and Horner run on the side stream beside the bottom part's bucket trees (DESIGN §7c)."]
+# PMC passes (profile_pip.sh): per kernel, summed over its launches in the 3-MSM probe runs,
+# per MSM; HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE (KB; gfx950 FETCH_SIZE x2 correction)
+def counters(name):
+    path = os.path.join(src, f"pmc_{name}", "run_counter_collection.csv")
+    if not os.path.exists(path):
+        return None
+    per = {}
+    for r in csv.DictReader(open(path)):
+        d = per.setdefault(int(r["Dispatch_Id"]), {"kernel": r["Kernel_Name"].replace("(anonymous namespace)::", "")
+                                                      .split("(")[0],
+                                                   "dur": int(r["End_Timestamp"]) - int(r["Start_Timestamp"])})
+        d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    return per
+
+
+pm = {k: counters(k) for k in ("fetch", "write", "valu", "cyc", "busy", "tcc")}
+if pm["fetch"]:
+    nm = 4   # pip_probe.py 20 12 3 1: one warm-up + 3 timed MSMs
+    kern = sorted({d["kernel"] for d in pm["fetch"].values() if d["kernel"].startswith("bp::k_pip")})
+
+    def agg(name, key, k, f=sum):
+        ds = [d.get(key, 0.0) for d in (pm[name] or {}).values() if d["kernel"] == k]
+        return f(ds) if ds else float("nan")
+
+    def avg(xs):
+        return sum(xs) / len(xs)
+    out += ["", "## PMC counters per MSM (`rocprofv3 --pmc`, one pass per counter group, 4 MSMs on one stream)", "",
+            "| kernel | launches/MSM | ms/MSM | HBM MB/MSM (2xFETCH+WRITE) | GB/s | VALU winstr/MSM (M) | VALUBusy % "
+            "| VALUUtil % | L2 hit % | eff. clock GHz |", "|---|---|---|---|---|---|---|---|---|---|"]
+    for k in kern:
+        n = sum(1 for d in pm["fetch"].values() if d["kernel"] == k) / nm
+        dur = agg("fetch", "dur", k) / nm / 1e6
+        hbm = (2 * agg("fetch", "FETCH_SIZE", k) + agg("write", "WRITE_SIZE", k)) * 1024 / nm
+        vi = agg("valu", "SQ_INSTS_VALU", k) / nm
+        busy = agg("busy", "VALUBusy", k, avg)
+        util = agg("busy", "VALUUtilization", k, avg)
+        hit, miss = agg("tcc", "TCC_HIT_sum", k), agg("tcc", "TCC_MISS_sum", k)
+        grbm = agg("cyc", "GRBM_GUI_ACTIVE", k)
+        cdur = agg("cyc", "dur", k)
+        out.append(f"| {k.replace('bp::', '')} | {n:.1f} | {dur:.3f} | {hbm / 1e6:.1f} | {hbm / (dur * 1e-3) / 1e9:.0f} | "
+                   f"{vi / 1e6:.1f} | {busy:.1f} | {util:.1f} | {100 * hit / max(hit + miss, 1):.1f} | "
+                   f"{grbm / 8 / cdur:.2f} |")
+    out += ["", "Algorithmic bytes per MSM (SURVEY §8(d)): 2^20 x (128 B point + 32 B scalar) + 128 B = 167.8 MB. "
+            "GB/s is per kernel over its own launch time under the profiler (serialised)."]
 dst = os.path.join(root, "profiles", f"rocprof_{tag}_pip_summary.md")
 open(dst, "w").write("\n".join(out) + "\n")
 os.makedirs(os.path.join(root, "profiles", f"raw_{tag}_pip"), exist_ok=True)
