@@ -1,0 +1,89 @@
+"""configs[4] rank-shard probe (one process, many schedules): one rank's shard of the 2^16-proof
+batch (default 8192 proofs = N = 8) pushed through two verify pipelines on two streams, as
+bench.py's sharded_2p16 leg does, timed for every (push batch, drain policy) pair.  The drain
+policy is read per tick from the environment (HIPBP_QUAD, HIPBP_QUAD_MAX_ITEMS), so one process
+A/Bs them; every run's verdict digest must be the same.
+
+  python tools/shard_probe.py [shard] [push batches, comma-separated] [quad max items, comma-separated; 0 = off]
+"""
+import hashlib
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import cudabulletproof_amd as bp  # noqa: E402
+from cudabulletproof_amd import synth  # noqa: E402
+
+shard = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
+pushes = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1024,2048,4096").split(",")]
+qmaxes = [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "0,49152,131072,262144").split(",")]
+reps = int(os.environ.get("REPS", "3"))
+n, B = 64, 1024
+dev = torch.device("cuda:0")
+bp.lib()
+G, H, g, h = synth.generators(n, dev)
+T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)
+Gd, Hd, gd, hd = T(G), T(H), T(g), T(h)
+gens = bp.Generators(n, Gd, Hd, gd, hd, prefix_bits=int(os.environ.get("K", "22")))
+tiles = []
+for t in range(4):
+    pi = {k: T(v) for k, v in synth.prove_inputs(B, n, seed=5001 + t).items()}
+    out = bp.batch_generate_range_proof(n, pi["v"], pi["gamma"], pi["sL"], pi["sR"], pi["rnd"], Gd, Hd, gd, hd,
+                                        gens=gens)
+    tiles.append({k: out[k] for k in bp.RangeProofBatch.FIELDS})
+torch.cuda.synchronize()
+streams = [torch.cuda.Stream(dev) for _ in range(2)]
+
+
+def rows(j0, m):
+    parts, j = [], j0
+    while j < j0 + m:
+        k = min(B - j % B, j0 + m - j)
+        parts.append(((j // B) % 4, j % B, k))
+        j += k
+    return {f: torch.cat([tiles[t][f][r0:r0 + k] for t, r0, k in parts]) for f in bp.RangeProofBatch.FIELDS}
+
+
+print(f"shard {shard} proofs, two pipelines, K = {gens.bits}", flush=True)
+for Bs in pushes:
+    pipes = [bp.VerifyPipeline(Bs, n, Gd, Hd, hd, stream=streams[i]) for i in range(2)]
+    for pp in pipes:
+        pp.use_gens(gens)
+    jobs, j = [], 0
+    while j < shard:
+        jobs.append((j, min(Bs, shard - j)))
+        j += Bs
+    batches = [bp.RangeProofBatch(n, **rows(j0, m)) for j0, m in jobs]
+    offs = np.cumsum([0] + [m for _, m in jobs])
+    for qm in qmaxes:
+        os.environ["HIPBP_QUAD_MAX_ITEMS"] = str(qm)
+        if qm == 0:
+            os.environ["HIPBP_QUAD"] = "0"
+        else:
+            os.environ.pop("HIPBP_QUAD", None)
+        best, dig = None, None
+        for r in range(reps + 1):
+            ok = torch.zeros(shard, dtype=torch.uint8, device=dev)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for k, b in enumerate(batches):
+                pipes[k % 2].push(b, ok[offs[k]:offs[k + 1]])
+            for pp in pipes:
+                pp.flush()
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            if r:
+                best = dt if best is None else min(best, dt)
+            d = hashlib.sha256(ok.cpu().numpy().tobytes()).hexdigest()[:16]
+            assert dig is None or d == dig, (d, dig)
+            dig = d
+        print(f"push {Bs:5d}  quad_max {qm:7d}  {best * 1e3:7.2f} ms  {shard / best / 1e3:7.1f} K verifies/s  "
+              f"digest {dig}", flush=True)
+    for pp in pipes:
+        pp.close()
+os.environ.pop("HIPBP_QUAD", None)
+os.environ.pop("HIPBP_QUAD_MAX_ITEMS", None)
