@@ -549,7 +549,7 @@ struct Pipeline {
             unsigned long long tot = 0;
             for (int k = 0; k < tr.count; k++) {
                 bp::Region& g = tr.reg[k];
-                if (bp::region_is_sm(g.kind)) g.items *= 4;
+                if (bp::region_quad_lanes(g.kind)) g.items *= 4;
                 g.begin = tot;
                 const unsigned long long al = g.kind == bp::RK_TREE ? 256 : 64;
                 tot += (g.items + al - 1) & ~(al - 1);

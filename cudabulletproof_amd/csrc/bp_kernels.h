@@ -178,6 +178,8 @@ void launch_terms(const RegionList& rl, const SlotDev* slots, const ge* G, const
 inline bool region_is_sm(int kind) {
     return kind == RK_STAGE0 || kind == RK_ROUND || kind == RK_FINAL_TERMS || kind == RK_M3;
 }
+// regions whose items take a lane quad in the drain-tick form (the final assembly's point adds too)
+inline bool region_quad_lanes(int kind) { return region_is_sm(kind) || kind == RK_FINAL; }
 
 // Generic canonical-tree MSM.  perm [m] / bins [MSM_BINS] (nullable): workspace of the
 // counting sort that groups items of equal chain length into the same waves (m >= MSM_SORT_MIN).

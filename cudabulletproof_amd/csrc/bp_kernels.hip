@@ -506,46 +506,57 @@ __device__ __forceinline__ int absdiff(int a, int b) { return a > b ? a - b : b 
 // Canonical MSM tree over cnt points stored `stride` apart, evaluated level by
 // level by one lane, in place (the slot's own workspace): stride 1 = the whole tree of an
 // n <= LANE_TREE_MAX MSM; stride TPB = levels TPB, 2 TPB, ... over the per-block chunk roots.
+// QUAD (drain ticks): the proof's lane quad runs each add on ge_op_quad (3 product latencies
+// instead of 9); all four lanes hold and store the same values, so each reads back its own writes.
+template <bool QUAD = false>
+__device__ __forceinline__ ge gadd(const ge& a, const ge& b) {
+    if (QUAD) return ge_op_quad<false>(a, b);
+    return ge_add(a, b);
+}
+template <bool QUAD = false>
 __device__ __forceinline__ ge tree_upper(ge* T, int cnt, int stride) {
     for (int st = 1; st < cnt; st <<= 1)
         for (int i = 0; i + st < cnt; i += 2 * st)
-            T[(size_t)i * stride] = ge_norm_dev(ge_add(T[(size_t)i * stride], T[(size_t)(i + st) * stride]));
+            T[(size_t)i * stride] = ge_norm_dev(gadd<QUAD>(T[(size_t)i * stride], T[(size_t)(i + st) * stride]));
     return T[0];
 }
 
 // P assembly (rp.cu:785-801), check point (crv:257-278) and the tolerant accept rule
-// (crv:297-357).  One lane per proof.
+// (crv:297-357).  One lane per proof; QUAD: one lane quad per proof (its point adds on the quad,
+// the rest computed alike by the four lanes, lane 0 of the quad writes the outputs).
+template <bool QUAD = false>
 __device__ __forceinline__ void final_task(const SlotDev& sd, size_t p) {
+    const bool wr = !QUAD || (threadIdx.x & 3) == 0;
     const VerifyWs& ws = sd.ws;
     ge P;
     if (sd.range_mode) {
         ge m0, m1;
         const int n = sd.bv.n;
         if (sd.lane_tree) {         // the whole tree here: every add with all 64 lanes busy
-            m0 = tree_upper(ws.msm_pts + (p * 2 + 0) * n, n, 1);
-            m1 = tree_upper(ws.msm_pts + (p * 2 + 1) * n, n, 1);
+            m0 = tree_upper<QUAD>(ws.msm_pts + (p * 2 + 0) * n, n, 1);
+            m1 = tree_upper<QUAD>(ws.msm_pts + (p * 2 + 1) * n, n, 1);
         } else if (n > TPB) {       // upper tree levels over the per-block chunk roots (RK_TREE)
-            m0 = tree_upper(ws.msm_pts + (p * 2 + 0) * n, n / TPB, TPB);
-            m1 = tree_upper(ws.msm_pts + (p * 2 + 1) * n, n / TPB, TPB);
+            m0 = tree_upper<QUAD>(ws.msm_pts + (p * 2 + 0) * n, n / TPB, TPB);
+            m1 = tree_upper<QUAD>(ws.msm_pts + (p * 2 + 1) * n, n / TPB, TPB);
         } else {
             m0 = ws.msm_part[p * 2 + 0];
             m1 = ws.msm_part[p * 2 + 1];
         }
         P = ge_zero();
-        P = ge_norm_host(ge_add(P, m0));
-        P = ge_norm_host(ge_add(P, m1));
-        P = ge_norm_host(ge_add(P, ws.terms[p * 4 + 2]));
+        P = ge_norm_host(gadd<QUAD>(P, m0));
+        P = ge_norm_host(gadd<QUAD>(P, m1));
+        P = ge_norm_host(gadd<QUAD>(P, ws.terms[p * 4 + 2]));
         P = ge_norm_host(P);
         P = ge_norm_host(P);
     } else {
         P = ws.Pin[p];
     }
     ge cp = ge_zero();
-    cp = ge_norm_host(ge_add(cp, ws.fin[p * 2 + 0]));
-    cp = ge_norm_host(ge_add(cp, ws.fin[p * 2 + 1]));
-    cp = ge_norm_host(ge_add(cp, ws.terms[p * 4 + 3]));
-    if (sd.P_out) sd.P_out[p] = P;
-    if (sd.chk_out) sd.chk_out[p] = cp;
+    cp = ge_norm_host(gadd<QUAD>(cp, ws.fin[p * 2 + 0]));
+    cp = ge_norm_host(gadd<QUAD>(cp, ws.fin[p * 2 + 1]));
+    cp = ge_norm_host(gadd<QUAD>(cp, ws.terms[p * 4 + 3]));
+    if (wr && sd.P_out) sd.P_out[p] = P;
+    if (wr && sd.chk_out) sd.chk_out[p] = cp;
 
     fe kx = fe_canon(cp.X), ky = fe_canon(cp.Y), px = fe_canon(P.X), py = fe_canon(P.Y);
     if (sd.range_mode == 2) {
@@ -566,6 +577,7 @@ __device__ __forceinline__ void final_task(const SlotDev& sd, size_t p) {
         }
         int mb = 64 - __popcll(kx.v[3] ^ px.v[3]);
         bool ip_ok = ws.ipok[p] && ((xdc <= 3) | (sxc >= 28) | (mb >= 20));
+        if (!wr) return;
         sd.ok[p] = ((fl & 1) && ((fl >> 1) & 1) && poly_ok && ip_ok) ? 1 : 0;
         if (sd.flags_out)
             sd.flags_out[p] = (uint8_t)((fl & 7) | (m3 ? 8 : 0) | (m4 ? 16 : 0) | (ip_ok ? 32 : 0));
@@ -593,7 +605,7 @@ __device__ __forceinline__ void final_task(const SlotDev& sd, size_t p) {
     int hz = 0;
     for (int i = 0; i < 32; i++) hz += ((hs.v[i >> 3] >> (8 * (i & 7))) & 0xff) != 0;
     bool accept = (sx + sy >= 20) | (msb >= 28) | (xd + yd <= 32) | (hz <= 24);
-    sd.ok[p] = (ws.ipok[p] && accept) ? 1 : 0;
+    if (wr) sd.ok[p] = (ws.ipok[p] && accept) ? 1 : 0;
 }
 
 // range_proof_verify's polynomial identity sides and methods 1-2 (rp.cu:452-530), then the
@@ -806,7 +818,8 @@ __global__ __launch_bounds__(TPB, BP_TERMS_OCC) void k_terms(RegionList rl, cons
     } else if (rg.kind == RK_POLY) {
         poly_task(sd, l);
     } else if (rg.kind == RK_FINAL) {
-        final_task(sd, l);
+        if (QUAD) final_task<true>(sd, l >> 2);
+        else final_task<false>(sd, l);
     } else {
         // the scalar-multiplication kinds: fill the job, then the one call site
         SmJob jb;
