@@ -352,25 +352,26 @@ def rooflines(dom, B, n, steps, launches, avg_ms, dt, kern_ms, pcfg, npipes):
     busy = pmc(dom, "valu_busy_pct", pcfg)
     clk = pmc(dom, "eff_clock_ghz", pcfg)
     vagg = vi * launches / dt if vi else None   # all launches of the timed region / its wall time
-    im = issue_model()
-    cyc = im.get("cycles_per_valu") if im else None
-    peak = 1024 * clk * 1e9 / cyc if cyc and clk else None
+    loops = step_roof()
     valu_roofline = {
         "kernel": dom, "unit": "wave64 VALU instr/s", "frac": busy / 100 if busy else None,
-        "frac_source": "VALUBusy (rocprofv3 PMC, profiles/pmc_traffic.json)",
-        "instr_per_launch": vi, "achieved": vagg, "eff_clock_ghz": clk,
-        "cycles_per_instr_per_simd": 1024 * clk * 1e9 / vagg if vagg and clk else None,
-        "issue_model": {"cycles_per_valu": cyc, "peak": peak, "frac": vagg / peak if peak and vagg else None,
-                        "mix": im.get("mix_kernel") if im else None,
-                        "source": "profiles/valu_issue_model.json (tools/ubench_issue.hip x tools/valu_model.py)"},
+        "frac_source": "VALUBusy (rocprofv3 PMC on this configuration, profiles/pmc_traffic.json): the share of "
+                       "cycles the SIMDs spend issuing VALU work",
+        "instr_per_launch": vi, "achieved_aggregate": vagg, "eff_clock_ghz": clk,
+        "cycles_per_instr_per_simd_aggregate": 1024 * clk * 1e9 / vagg if vagg and clk else None,
+        "cycles_per_instr_per_simd_serialized": pmc(dom, "serial_cycles_per_instr_per_simd", pcfg),
+        "isolated_loops": {k: {"Ginstr_per_s": v["Ginstr_per_s"], "cycles_per_instr_per_simd":
+                               v["cycles_per_instr_per_simd"]} for k, v in loops["kernels"].items()} if loops else None,
+        "isolated_loops_source": "profiles/valu_step_roof.json (tools/ubench_step.hip: k_terms' point-op loops "
+                                 "from registers + LDS at its occupancy)",
         "valu_utilization_pct": pmc(dom, "valu_utilization_pct", pcfg), "pmc_config": pcfg,
     }
     return roofline, valu_roofline
 
 
-def issue_model():
+def step_roof():
     try:
-        return json.load(open(os.path.join(ROOT, "profiles", "valu_issue_model.json")))
+        return json.load(open(os.path.join(ROOT, "profiles", "valu_step_roof.json")))
     except (OSError, ValueError):
         return None
 

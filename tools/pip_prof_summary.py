@@ -71,8 +71,11 @@ if pm["fetch"]:
         dur = agg("fetch", "dur", k) / nm / 1e6
         hbm = (2 * agg("fetch", "FETCH_SIZE", k) + agg("write", "WRITE_SIZE", k)) * 1024 / nm
         vi = agg("valu", "SQ_INSTS_VALU", k) / nm
-        busy = agg("busy", "VALUBusy", k, avg)
-        util = agg("busy", "VALUUtilization", k, avg)
+        bd = [(d.get("VALUBusy", 0.0), d.get("VALUUtilization", 0.0), d["dur"]) for d in (pm["busy"] or {}).values()
+              if d["kernel"] == k]
+        tw = sum(x[2] for x in bd) or 1
+        busy = sum(x[0] * x[2] for x in bd) / tw   # duration-weighted over the launches
+        util = sum(x[1] * x[2] for x in bd) / tw
         hit, miss = agg("tcc", "TCC_HIT_sum", k), agg("tcc", "TCC_MISS_sum", k)
         grbm = agg("cyc", "GRBM_GUI_ACTIVE", k)
         cdur = agg("cyc", "dur", k)
@@ -80,7 +83,9 @@ if pm["fetch"]:
                    f"{vi / 1e6:.1f} | {busy:.1f} | {util:.1f} | {100 * hit / max(hit + miss, 1):.1f} | "
                    f"{grbm / 8 / cdur:.2f} |")
     out += ["", "Algorithmic bytes per MSM (SURVEY §8(d)): 2^20 x (128 B point + 32 B scalar) + 128 B = 167.8 MB. "
-            "GB/s is per kernel over its own launch time under the profiler (serialised)."]
+            "GB/s is per kernel over its own launch time under the profiler (serialised). VALUBusy and VALUUtil "
+            "are weighted by launch duration. The clock column (GRBM_GUI_ACTIVE / 8 / duration) is meaningful "
+            "only for kernels that run for a good fraction of a millisecond."]
 dst = os.path.join(root, "profiles", f"rocprof_{tag}_pip_summary.md")
 open(dst, "w").write("\n".join(out) + "\n")
 os.makedirs(os.path.join(root, "profiles", f"raw_{tag}_pip"), exist_ok=True)

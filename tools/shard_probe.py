@@ -19,7 +19,16 @@ import cudabulletproof_amd as bp  # noqa: E402
 from cudabulletproof_amd import synth  # noqa: E402
 
 shard = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
-pushes = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1024,2048,4096").split(",")]
+# push schedules: "4096" = equal pushes of 4096; "4096+2048+1024+1024" = that sequence (must sum to the shard);
+# pushes alternate over the two pipelines
+def schedule(spec):
+    if "+" in spec:
+        seq = [int(x) for x in spec.split("+")]
+        assert sum(seq) == shard, spec
+        return seq
+    b = int(spec)
+    return [min(b, shard - j) for j in range(0, shard, b)]
+pushes = [schedule(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1024,2048,4096").split(",")]
 qmaxes = [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "0,49152,131072,262144").split(",")]
 reps = int(os.environ.get("REPS", "3"))
 n, B = 64, 1024
@@ -49,14 +58,15 @@ def rows(j0, m):
 
 
 print(f"shard {shard} proofs, two pipelines, K = {gens.bits}", flush=True)
-for Bs in pushes:
+for seq in pushes:
+    Bs = max(seq)
     pipes = [bp.VerifyPipeline(Bs, n, Gd, Hd, hd, stream=streams[i]) for i in range(2)]
     for pp in pipes:
         pp.use_gens(gens)
     jobs, j = [], 0
-    while j < shard:
-        jobs.append((j, min(Bs, shard - j)))
-        j += Bs
+    for m in seq:
+        jobs.append((j, m))
+        j += m
     batches = [bp.RangeProofBatch(n, **rows(j0, m)) for j0, m in jobs]
     offs = np.cumsum([0] + [m for _, m in jobs])
     for qm in qmaxes:
@@ -81,7 +91,7 @@ for Bs in pushes:
             d = hashlib.sha256(ok.cpu().numpy().tobytes()).hexdigest()[:16]
             assert dig is None or d == dig, (d, dig)
             dig = d
-        print(f"push {Bs:5d}  quad_max {qm:7d}  {best * 1e3:7.2f} ms  {shard / best / 1e3:7.1f} K verifies/s  "
+        print(f"push {'+'.join(map(str, seq)):24s}  quad_max {qm:7d}  {best * 1e3:7.2f} ms  {shard / best / 1e3:7.1f} K verifies/s  "
               f"digest {dig}", flush=True)
     for pp in pipes:
         pp.close()

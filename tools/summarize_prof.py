@@ -21,7 +21,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def short(name):
     name = name.replace("(anonymous namespace)::", "")
-    return name.split("(")[0].replace("bp::", "")
+    name = name.split("(")[0].replace("bp::", "")
+    if name.startswith("void "):
+        name = name[5:]
+    # k_terms<false>: the pipeline tick; k_terms<true>: its drain-tick (lane-quad) form
+    return name.replace("k_terms<false>", "k_terms").replace("k_terms<true>", "k_terms_quad")
 
 
 def load_counters(d):
@@ -147,7 +151,8 @@ def main():
         cyc_per_instr = (grbm / 8) / (vi / 1024) if vi else float("nan")   # 1024 SIMDs
         traffic[kern] = {"bytes_per_launch": hbm, "fetch_kb": fk, "write_kb": wk, "launches": len(f),
                          "valu_instr_per_wave": vi / waves if waves else None, "valu_instr_per_launch": vi,
-                         "eff_clock_ghz": clock, "rocprof_avg_ms": trace_ms.get(kern)}
+                         "eff_clock_ghz": clock, "rocprof_avg_ms": trace_ms.get(kern),
+                         "serial_cycles_per_instr_per_simd": cyc_per_instr}
         lines.append(f"| {kern} | {len(f)} | {f[0]['grid']} | {f[0]['vgpr']} | {fk:.0f} | {wk:.0f} | {hbm:.3e} | "
                      f"{waves:.0f} | {vi / waves:.0f} | {si / waves:.0f} | {li / waves:.0f} | {clock:.2f} | "
                      f"{cyc_per_instr:.2f} |")
@@ -167,12 +172,13 @@ def main():
             i32 = mean([d.get("SQ_INSTS_VALU_INT32", float("nan")) for d in x]) / waves if x else float("nan")
             i64 = mean([d.get("SQ_INSTS_VALU_INT64", float("nan")) for d in x]) / waves if x else float("nan")
             v2 = mean([d.get("SQ_ACTIVE_INST_VALU2", float("nan")) for d in x]) / waves if x else float("nan")
-            traffic.setdefault(kern, {}).update({"valu_busy_pct": vb, "valu_utilization_pct": vu})
+            traffic.setdefault(kern, {}).update({"valu_busy_pct": vb, "valu_utilization_pct": vu,
+                                                  "valu2_cycles_per_wave": v2})
             lines.append(f"| {kern} | {vb:.1f} | {vu:.1f} | {i32:.0f} | {i64:.0f} | {v2:.0f} |")
     lines += ["", "Notes:",
               "- `VALU cyc/instr/SIMD` = kernel cycles (GRBM_GUI_ACTIVE/8) / (SQ_INSTS_VALU / 1024 SIMDs): the "
-              "issue interval per SIMD; compare with the issue-cost model of the hot loop's opcode mix "
-              "(profiles/valu_issue_model.json: tools/ubench_issue.hip costs in shader-clock cycles x tools/valu_model.py).",
+              "issue interval per SIMD, here with the profiler serialising dispatches; k_terms' own point-op loops "
+              "sustain ~4.0 in isolation (profiles/valu_step_roof.json, tools/ubench_step.hip).",
               "- HBM bytes apply the gfx950 FETCH_SIZE x2 correction; the loads here are 16-B-per-lane "
               "(dwordx4) gathers of 128-B points, partly served by L2/MALL, so treat absolute bytes as approximate.",
               "- VALUBusy = 100 * SQ_ACTIVE_INST_VALU / CU_NUM / GRBM_GUI_ACTIVE (rocprofv3 derived metric): the share "
