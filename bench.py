@@ -675,12 +675,13 @@ def h2d_leg(args, dev, pipes, batches, steps):
 
 def shard_push_batch(args, shard_size, npipe):
     """Proofs per push for a rank's shard.  A pushed batch completes depth - 1 ticks after its push,
-    and the drain ticks (fold rounds 3..5, final terms of the last batches) are latency-bound, so a
-    small shard (8192 proofs per rank at N = 8) goes through in fewer, larger pushes: ≈2 per
-    pipeline, at most 4096 proofs each; a large one keeps the bench's B (measured)."""
+    and its last ticks (fold rounds 3..5, final terms, final assembly) are latency-bound, so a small
+    shard (8192 proofs per rank at N = 8) goes through in one push per pipeline of at most 4096
+    proofs: the two pipelines' latency-bound drain ticks then run side by side (tools/shard_probe.py,
+    DESIGN §5: 4096+4096 169.4 K, 2048 x 4 162.5 K, decreasing schedules 150-156 K)."""
     if args.shard_batch > 0:
         return args.shard_batch
-    per = -(-shard_size // (2 * npipe))
+    per = -(-shard_size // npipe)
     Bs = args.batch
     while Bs < per and Bs < 4096:
         Bs *= 2

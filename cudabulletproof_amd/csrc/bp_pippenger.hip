@@ -69,15 +69,16 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t x, const FastDiv& f) {
 //    bucket of a sorted element is ((g / n) << c) | digit.
 // MSM m's scalars are s[m n .. m n + n); all share the points.  One thread per V scalars (m, i..):
 // it reads them once and writes their Wp keys, each store coalesced over consecutive i.
-// It also zeroes the bucket counts cnt[0 .. nb) and the two words (longest list, bidfill queue
-// length) that the histogram and k_pip_len0 accumulate into (two memset launches less on the serial path).
+// It also zeroes the bucket counts cnt[0 .. nb) and the three words (longest list, bidfill and tail
+// queue lengths) that the histogram, k_pip_len0 and k_pip_lay_part accumulate into (no memset
+// launches on the serial path).
 template <int V, typename KT>   // V > 1 needs n % V == 0 (one V-key store per window)
 __global__ __launch_bounds__(PTPB) void k_pip_keys(const fe* __restrict__ s, FastDiv fn, uint32_t count, int c,
                                                   int ib, int w0, int Wp, KT* keys, uint32_t* cnt, size_t nb,
                                                   unsigned* maxlen) {
     const size_t tid = (size_t)blockIdx.x * PTPB + threadIdx.x;
     for (size_t b = tid; b < nb; b += (size_t)gridDim.x * PTPB) cnt[b] = 0;
-    if (tid < 2) maxlen[tid] = 0;   // [0] the longest list, [1] k_pip_bidfill's queue length
+    if (tid < 3) maxlen[tid] = 0;   // [0] the longest list, [1] k_pip_bidfill's queue length, [2] k_pip_tail's
     const uint32_t n = fn.d, g = (uint32_t)tid * V;
     if (g >= count * n) return;
     const uint32_t m = fdiv(g, fn), i = g - m * n;
@@ -245,9 +246,12 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 
 // The extra layer T (the last block row) scans the bucket sizes in sorted order instead (cnt_t:
 // digit-major, virtual window minor, unpadded): OFF_T is each bucket's start in the sorted array.
+// Layer TT (TT < T; TT = 0: none) also queues every bucket whose list is still unfinished there
+// (LEN_TT > 0) for k_pip_tail: tailq[0 .. *tailn).
 __global__ __launch_bounds__(PTPB) void k_pip_lay_part(const uint32_t* __restrict__ len0,
                                                       const uint32_t* __restrict__ cnt_t, int T, size_t nb,
-                                                      uint32_t* LEN, uint32_t* PAD, uint32_t* part, unsigned nparts) {
+                                                      uint32_t* LEN, uint32_t* PAD, uint32_t* part, unsigned nparts,
+                                                      int TT, uint32_t* tailq, unsigned* tailn) {
     __shared__ uint32_t wsum[PTPB / 64];
     const int t = blockIdx.y;   // layer
     const size_t b0 = (size_t)blockIdx.x * SCAN_BLK + (size_t)threadIdx.x * SCAN_PER;
@@ -262,6 +266,7 @@ __global__ __launch_bounds__(PTPB) void k_pip_lay_part(const uint32_t* __restric
             uint32_t L = len0[b0 + k];
             for (int u = 0; u < t; u++) L = L <= 4 ? 0u : (L + 3) >> 2;
             const uint32_t pd = (L + 3) & ~3u;
+            if (TT && t == TT && L) tailq[atomicAdd(tailn, 1u)] = (uint32_t)(b0 + k);
             LEN[(size_t)t * nb + b0 + k] = L;
             PAD[(size_t)t * nb + b0 + k] = pd;
             sum += pd;
@@ -425,6 +430,55 @@ __global__ __launch_bounds__(PTPB, 4) void k_pip_step(int t, const unsigned* __r
     if (!fin) bid2[o] = b;
 }
 
+
+// The bucket trees' last levels, staged in LDS.  From layer TAIL_LAYER on only a few lists are
+// left (the top window's deep buckets and the rare crowded ones), and the step launches past it
+// are latency-bound (a few thousand busy lanes, one launch per two levels).  One block per
+// unfinished list instead: it loads an aligned chunk of up to TAIL_CHUNK nodes of the list into
+// LDS and runs the pairwise tree over it level by level, one pair per lane quad (ge_op_quad, the
+// same products as ge_add), with a barrier per level; a list longer than a chunk leaves one root
+// per chunk in place and goes round again.  Chunks are aligned to 512 = 2^9 list positions, so every
+// node is the canonical tree's (the layer-TAIL_LAYER nodes are its level-2 TAIL_LAYER nodes): the same
+// bits as the global steps.
+constexpr int TAIL_LAYER = 4;
+constexpr int TAIL_CHUNK = 512;
+__global__ __launch_bounds__(PTPB) void k_pip_tail(const uint32_t* __restrict__ tailq, const unsigned* __restrict__ tailn,
+                                                  ge* Q, const uint32_t* __restrict__ off,
+                                                  const uint32_t* __restrict__ len, ge* S) {
+    __shared__ ge sh[TAIL_CHUNK];
+    const int t = threadIdx.x;
+    const unsigned nq = *tailn;
+    for (unsigned qi = blockIdx.x; qi < nq; qi += gridDim.x) {   // block-uniform loop
+        const uint32_t b = tailq[qi];
+        ge* base = Q + off[b];
+        uint32_t L = len[b];
+        while (L > 1) {
+            const uint32_t nch = (L + TAIL_CHUNK - 1) / TAIL_CHUNK;
+            for (uint32_t c = 0; c < nch; c++) {
+                const int cnt = (int)(L - c * TAIL_CHUNK < (uint32_t)TAIL_CHUNK ? L - c * TAIL_CHUNK : TAIL_CHUNK);
+                for (int i = t; i < cnt; i += PTPB) sh[i] = base[(size_t)c * TAIL_CHUNK + i];
+                __syncthreads();
+                for (int st = 1; st < cnt; st <<= 1) {
+                    const int pairs = (cnt - st + 2 * st - 1) / (2 * st);   // i = 2 st a with i + st < cnt
+                    for (int a0 = 0; a0 < pairs; a0 += PTPB / 4) {         // block-uniform trip count
+                        const int a = a0 + (t >> 2);
+                        if (a < pairs) {   // pairs of one level touch disjoint entries
+                            const ge r = ge_op_quad<false>(sh[2 * st * a], sh[2 * st * a + st]);
+                            if ((t & 3) == 0) sh[2 * st * a] = r;
+                        }
+                        __syncthreads();
+                    }
+                }
+                // chunk c's root to list position c: chunk 0 (positions 0 .. 511, c < 512) is already read
+                if (t == 0) base[c] = sh[0];
+                __syncthreads();
+            }
+            L = nch;
+        }
+        if (t == 0) S[b] = base[0];
+        __syncthreads();
+    }
+}
 
 // one block per (virtual) window v = m Wp + lw: pairwise tree over its NC <= PTPB chunk values, in
 // LDS, into Sw[m W + w0 + lw] (MSM m's window sums, absolute window index).  A latency-bound
@@ -623,7 +677,7 @@ struct DBuf {
     template <typename T> T* as() const { return (T*)p; }
 };
 struct PipWs {
-    DBuf keys_in, keys, vals, temp, start, len[2], lay, bq, bid[2], Q[2], S, V, Sw, Tmid, maxlen, part;
+    DBuf keys_in, keys, vals, temp, start, len[2], lay, bq, bid[2], Q[2], S, V, Sw, Tmid, maxlen, part, tailq;
     hipStream_t side = nullptr;           // the Horner chain's stream
     hipEvent_t ev[4] = {};   // [1] top half's buckets done, [2] bottom half done, [3] chain done
 };
@@ -700,7 +754,9 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
     PIP_RET(ws.Q[0].need(qcap * sizeof(ge))); PIP_RET(ws.Q[1].need(qcap * sizeof(ge)));
     PIP_RET(ws.V.need((size_t)W * NC * sizeof(ge)));
     PIP_RET(ws.S.need(nb * sizeof(ge)));
-    PIP_RET(ws.maxlen.need(2 * sizeof(unsigned)));
+    PIP_RET(ws.maxlen.need(3 * sizeof(unsigned)));
+    const int TT = steps > TAIL_LAYER ? TAIL_LAYER : 0;   // the LDS tail takes over at layer TT (0: none)
+    if (TT) PIP_RET(ws.tailq.need(nb * sizeof(uint32_t)));
     const size_t nbq = N / BID_PIECE + 1;   // bidfill queue capacity (further pieces of long lists)
     PIP_RET(ws.bq.need(nbq * sizeof(uint2)));
     size_t tb_sort = 0;
@@ -739,7 +795,8 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
                                           ws.maxlen.as<unsigned>(), ws.S.as<ge>(), ws.bq.as<uint2>());
     // every step's layout (LEN, PAD, OFF)[t], t = 0 .. steps, and OFF[T] = the sorted-order starts
     k_pip_lay_part<<<dim3(nparts, T + 1), PTPB, 0, s>>>(ws.len[0].as<uint32_t>(), ws.len[1].as<uint32_t>(), T, nb,
-                                                        LEN, PAD, ws.part.as<uint32_t>(), nparts);
+                                                        LEN, PAD, ws.part.as<uint32_t>(), nparts, TT,
+                                                        ws.tailq.as<uint32_t>(), ws.maxlen.as<unsigned>() + 2);
     k_pip_lay_fin<<<dim3(nparts, T + 1), PTPB, 0, s>>>(PAD, ws.part.as<uint32_t>(), nparts, nb, OFF);
     k_pip_start<<<nb_of(nb), PTPB, 0, s>>>(OFF + (size_t)T * nb, nb, c, (uint32_t)W, ws.start.as<uint32_t>());
     if (k32) {
@@ -758,7 +815,7 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
     // at least nb lanes in every step (step 0 too: when n < 2^c / 4 the padded total is below
     // 4 nb), so the octet tail path, which takes up to nb / 8 groups, always has its 8 lanes each
     size_t lanes = std::max((tot0 + 3) / 4, nb);
-    for (int t = 0; t < steps; t++) {
+    for (int t = 0; t < (TT ? TT : steps); t++) {
         const int a = t & 1, b = a ^ 1;
         const size_t l0 = (size_t)t * nb, l1 = l0 + nb;
         k_pip_step<<<nb_of(lanes), PTPB, 0, s>>>(t, ws.maxlen.as<unsigned>(), P, fn, keys32, imask,
@@ -768,6 +825,10 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
                                                   ws.bid[b].as<uint32_t>(), ws.S.as<ge>(), nb, lanes);
         lanes = lanes / 4 + nb;
     }
+    if (TT)   // layer TT's unfinished lists (written by step TT - 1 into Q[TT & 1]), in LDS
+        k_pip_tail<<<(unsigned)std::min(nb, (size_t)2048), PTPB, 0, s>>>(
+            ws.tailq.as<uint32_t>(), ws.maxlen.as<unsigned>() + 2, ws.Q[TT & 1].as<ge>(), OFF + (size_t)TT * nb,
+            LEN + (size_t)TT * nb, ws.S.as<ge>());
     return hipGetLastError();
 }
 
@@ -878,7 +939,7 @@ hipError_t pippenger_release(hipStream_t s) {
     for (PipWs* w : {&pp->hi, &pp->lo}) {
         for (DBuf* b : {&w->keys_in, &w->keys, &w->vals, &w->temp, &w->start, &w->len[0], &w->len[1], &w->lay,
                         &w->bq, &w->bid[0], &w->bid[1], &w->Q[0], &w->Q[1], &w->S, &w->V, &w->Sw, &w->Tmid,
-                        &w->maxlen, &w->part})
+                        &w->maxlen, &w->part, &w->tailq})
             if (b->p) PIP_RET(hipFree(b->p));
         for (auto& ev : w->ev)
             if (ev) PIP_RET(hipEventDestroy(ev));

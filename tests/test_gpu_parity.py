@@ -880,7 +880,8 @@ def test_msm_pippenger_rejects_bad_window(bp):
 
 
 @pytest.mark.parametrize("kind,n", [("same", 3000), ("zero", 3000), ("one_bit", 3000), ("same", 10000),
-                                    ("one_bit", 9001)])
+                                    ("one_bit", 9001),
+                                    ("same", 140000)])   # LDS tail: a 547-node layer-4 list, two chunks
 def test_msm_pippenger_degenerate_scalars(bp, oracle, kind, n):
     """Every point in one bucket per window (deep bucket trees, many empty buckets).  n > 4096: the
     lists are longer than one k_pip_bidfill piece (BID_PIECE), so the extra-piece queue runs."""
