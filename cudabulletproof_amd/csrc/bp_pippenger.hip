@@ -246,8 +246,8 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 
 // The extra layer T (the last block row) scans the bucket sizes in sorted order instead (cnt_t:
 // digit-major, virtual window minor, unpadded): OFF_T is each bucket's start in the sorted array.
-// Layer TT (TT < T; TT = 0: none) also queues every bucket whose list is still unfinished there
-// (LEN_TT > 0) for k_pip_tail: tailq[0 .. *tailn).
+// Layer TT (TT < T; TT = 0: none) also queues every bucket whose list there needs more than one
+// more step (LEN_TT > 4) for k_pip_tail: tailq[0 .. *tailn); step TT finishes the others.
 __global__ __launch_bounds__(PTPB) void k_pip_lay_part(const uint32_t* __restrict__ len0,
                                                       const uint32_t* __restrict__ cnt_t, int T, size_t nb,
                                                       uint32_t* LEN, uint32_t* PAD, uint32_t* part, unsigned nparts,
@@ -266,7 +266,7 @@ __global__ __launch_bounds__(PTPB) void k_pip_lay_part(const uint32_t* __restric
             uint32_t L = len0[b0 + k];
             for (int u = 0; u < t; u++) L = L <= 4 ? 0u : (L + 3) >> 2;
             const uint32_t pd = (L + 3) & ~3u;
-            if (TT && t == TT && L) tailq[atomicAdd(tailn, 1u)] = (uint32_t)(b0 + k);
+            if (TT && t == TT && L > 4) tailq[atomicAdd(tailn, 1u)] = (uint32_t)(b0 + k);
             LEN[(size_t)t * nb + b0 + k] = L;
             PAD[(size_t)t * nb + b0 + k] = pd;
             sum += pd;
@@ -359,7 +359,7 @@ __global__ __launch_bounds__(PTPB, 4) void k_pip_step(int t, const unsigned* __r
                                                   const uint32_t* __restrict__ bid, const uint32_t* __restrict__ off,
                                                   const uint32_t* __restrict__ len, const uint32_t* __restrict__ pad,
                                                   const uint32_t* __restrict__ off2, ge* Qout, uint32_t* bid2,
-                                                  ge* S, size_t nb, size_t lanes) {
+                                                  ge* S, size_t nb, size_t lanes, int tail_t) {
     const size_t k = (size_t)blockIdx.x * PTPB + threadIdx.x;
     if (k >= lanes || t >= pip_steps(maxlen)) return;
     const bool first = t == 0;
@@ -373,6 +373,7 @@ __global__ __launch_bounds__(PTPB, 4) void k_pip_step(int t, const unsigned* __r
         if (pos >= total) return;   // whole octets leave together
         const uint32_t b = bid[pos];
         const uint32_t j = pos - off[b], L = len[b];
+        if (t == tail_t && L > 4) return;   // k_pip_tail's list (whole octets leave together)
         const uint32_t r = L - j < 4 ? L - j : 4;
         const size_t base = first ? (size_t)start[b] + j : (size_t)off[b] + j;
         auto load = [&](uint32_t e) -> ge {
@@ -402,6 +403,7 @@ __global__ __launch_bounds__(PTPB, 4) void k_pip_step(int t, const unsigned* __r
     if (pos >= total) return;
     const uint32_t b = bid[pos];
     const uint32_t j = pos - off[b], L = len[b];
+    if (t == tail_t && L > 4) return;   // k_pip_tail's list
     const uint32_t r = L - j < 4 ? L - j : 4;
     const size_t base = first ? (size_t)start[b] + j : (size_t)off[b] + j;
     auto load = [&](uint32_t t) -> ge {
@@ -432,9 +434,11 @@ __global__ __launch_bounds__(PTPB, 4) void k_pip_step(int t, const unsigned* __r
 
 
 // The bucket trees' last levels, staged in LDS.  From layer TAIL_LAYER on only a few lists are
-// left (the top window's deep buckets and the rare crowded ones), and the step launches past it
-// are latency-bound (a few thousand busy lanes, one launch per two levels).  One block per
-// unfinished list instead: it loads an aligned chunk of up to TAIL_CHUNK nodes of the list into
+// longer than 4 (the top window's deep buckets and the rare crowded ones), and the step launches
+// past it are latency-bound (a few thousand busy lanes, one launch per two levels).  Step
+// TAIL_LAYER still finishes the lists of 2..4 nodes (most of the lower windows' buckets of
+// 257..1024 points, tens of thousands of them: one add per lane); every longer list gets a block
+// here instead: it loads an aligned chunk of up to TAIL_CHUNK nodes of the list into
 // LDS and runs the pairwise tree over it level by level, one pair per lane quad (ge_op_quad, the
 // same products as ge_add), with a barrier per level; a list longer than a chunk leaves one root
 // per chunk in place and goes round again.  Chunks are aligned to 512 = 2^9 list positions, so every
@@ -815,17 +819,17 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
     // at least nb lanes in every step (step 0 too: when n < 2^c / 4 the padded total is below
     // 4 nb), so the octet tail path, which takes up to nb / 8 groups, always has its 8 lanes each
     size_t lanes = std::max((tot0 + 3) / 4, nb);
-    for (int t = 0; t < (TT ? TT : steps); t++) {
+    for (int t = 0; t < (TT ? TT + 1 : steps); t++) {
         const int a = t & 1, b = a ^ 1;
         const size_t l0 = (size_t)t * nb, l1 = l0 + nb;
         k_pip_step<<<nb_of(lanes), PTPB, 0, s>>>(t, ws.maxlen.as<unsigned>(), P, fn, keys32, imask,
                                                   ws.vals.as<uint32_t>(),
                                                   ws.start.as<uint32_t>(), ws.Q[a].as<ge>(), ws.bid[a].as<uint32_t>(),
                                                   OFF + l0, LEN + l0, PAD + l0, OFF + l1, ws.Q[b].as<ge>(),
-                                                  ws.bid[b].as<uint32_t>(), ws.S.as<ge>(), nb, lanes);
+                                                  ws.bid[b].as<uint32_t>(), ws.S.as<ge>(), nb, lanes, TT ? TT : -1);
         lanes = lanes / 4 + nb;
     }
-    if (TT)   // layer TT's unfinished lists (written by step TT - 1 into Q[TT & 1]), in LDS
+    if (TT)   // layer TT's lists that need more than one more step (written by step TT - 1 into Q[TT & 1]), in LDS
         k_pip_tail<<<(unsigned)std::min(nb, (size_t)2048), PTPB, 0, s>>>(
             ws.tailq.as<uint32_t>(), ws.maxlen.as<unsigned>() + 2, ws.Q[TT & 1].as<ge>(), OFF + (size_t)TT * nb,
             LEN + (size_t)TT * nb, ws.S.as<ge>());
