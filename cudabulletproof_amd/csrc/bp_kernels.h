@@ -248,7 +248,7 @@ struct ProveWs {
     int pbits;
 };
 enum ProveStage { PS_PREP = 0, PS_TERMS0, PS_CHAIN0, PS_COMMIT, PS_TERMS1, PS_TX, PS_RTERMS, PS_RCHAIN, PS_ROUND,
-                  PS_FINAL };
+                  PS_FINAL, PS_SORT0 /* terms0's heavy-list sort, before PS_TERMS0 */ };
 void launch_prove(int stage, int r, const ProveIn& in, const ProveWs& ws, const ProveOut& out, const ge* G,
                   const ge* H, const ge* g, const ge* h, const ge* dtab, const fe* two_i, hipStream_t s);
 

@@ -521,7 +521,7 @@ void launch_prove(int stage, int r, const ProveIn& in, const ProveWs& ws, const 
             (void)hipMemsetAsync(ws.cnt, 0, 2 * sizeof(unsigned), s);
             k_prove_prep<<<nblk(B), TPB, 0, s>>>(in, ws, dtab);
             break;
-        case PS_TERMS0:
+        case PS_SORT0:
             if (ws.slist) {   // heavy list -> chain-length order (the list length is on the device)
                 const size_t cap = ws.cap;
                 (void)hipMemsetAsync(ws.sbins, 0, MSM_BINS * sizeof(unsigned), s);
@@ -529,6 +529,8 @@ void launch_prove(int stage, int r, const ProveIn& in, const ProveWs& ws, const 
                 launch_ops_scan(ws.sbins, 1, s);
                 k_prove_sort_scatter<<<(unsigned)((cap + SORT_T - 1) / SORT_T), SORT_T, 0, s>>>(in, ws);
             }
+            break;
+        case PS_TERMS0:
             k_prove_terms0<<<nblk(B * (4 * (size_t)n + 4) + 2 * n), TPB, 0, s>>>(in, ws, G, H, g, h, dtab);
             break;
         case PS_CHAIN0: k_prove_chain0<<<nblk(B * 4), TPB, 0, s>>>(in, ws); break;
