@@ -151,7 +151,6 @@ struct Engine {
     // different streams overlap (one batch's latency-bound stages under another's term launch)
     struct ProverBufs { Buf b[19]; };
     std::map<hipStream_t, ProverBufs*> provers;
-    hipEvent_t prove_gate = nullptr;   // recorded after the last prover terms0 (prove_run)
     // pinned host staging for the single-proof entry points (a pageable source of an
     // async copy must outlive the copy; this one does, and the stream is synced after use)
     uint8_t* pinned = nullptr;
@@ -1028,18 +1027,7 @@ static int prove_run(const hipbp_prove_input* in, const ge25519* G, const ge2551
     };
     run(bp::PS_PREP, 0);
     run(bp::PS_SORT0, 0);
-    // The terms0 gate: terms0 (≈90 % of a batch, VALU-bound across the whole GPU) of successive
-    // calls runs one after another across streams, in call order, so each batch's latency-bound
-    // rest (chains, T terms, IPA rounds: ≈40 ms at B = 65536) runs under the NEXT batch's terms0
-    // instead of beside another batch's rest.  Two streams without it fell into lockstep: both
-    // terms0 together, then both tails together with the GPU mostly idle.  HIPBP_PROVE_GATE=0: off.
-    static const bool gate = getenv("HIPBP_PROVE_GATE") ? atoi(getenv("HIPBP_PROVE_GATE")) != 0 : true;
-    if (gate) {
-        if (!e->prove_gate) BP_RET_ON(hipEventCreateWithFlags(&e->prove_gate, hipEventDisableTiming));
-        else BP_RET_ON(hipStreamWaitEvent(s, e->prove_gate, 0));
-    }
     run(bp::PS_TERMS0, 0);
-    if (gate) BP_RET_ON(hipEventRecord(e->prove_gate, s));
     run(bp::PS_CHAIN0, 0);
     run(bp::PS_COMMIT, 0);
     run(bp::PS_TERMS1, 0);
