@@ -272,8 +272,10 @@ bp::BatchView view_of(const hipbp_proof_batch* b) {
 //   1: RK_STAGE0 (both MSMs' point terms, fold round 0, t*h, c*Q [, the 7 polynomial terms])
 //   2: RK_TREE (MSM trees of n > LANE_TREE_MAX points) [, RK_POLY]   r+1 (1 <= r < L): RK_ROUND r
 //   FT = L+1 (1 when L = 0): RK_FINAL_TERMS           mode 2, max(3, FT): RK_M3
-//   FIN = 1 + the last of those: RK_FINAL (the trees of n <= LANE_TREE_MAX MSMs, P, check point,
-//   accept)
+//   min(3, FIN - 1): RK_LTREE (the trees of n <= LANE_TREE_MAX MSMs, one lane per proof)
+//   FIN = 1 + the last of those: RK_FINAL (P, check point, accept)
+// Ticks too small to fill the SIMDs (a drain's last ticks, a one-proof verify) run in the lane-quad
+// form (QUAD_MAX_ITEMS below).
 // A round-r item forms its own input point G'/H' from two round r-1 terms (each folded point
 // has exactly one consumer), so no launch of its own is needed for the fold combinations.
 // A generator set (hipbp_gens_create): a device snapshot of G[n] | H[n] | h | g and, optionally,
@@ -539,6 +541,9 @@ struct Pipeline {
                     if (st == 2 && range_mode && !lane_tree) add(tr, bp::RK_TREE, idx, 0, B * 2 * n, 256);
                 } else if (pass == chain_pass) {
                     if (st == g.fin) add(tr, bp::RK_FINAL, idx, 0, B, 64);
+                    // the lane MSM trees need only stage 0's terms: a few ticks before the final one,
+                    // so a drain's last tick is the short P / check-point assembly alone
+                    if (range_mode && lane_tree && st == std::min(3, g.fin - 1)) add(tr, bp::RK_LTREE, idx, 0, B, 64);
                     if (st == 2 && range_mode == 2) add(tr, bp::RK_POLY, idx, 0, B, 64);
                     if (st == 0) add(tr, bp::RK_PREP, idx, 0, range_mode ? 2 * B : B, 64);
                 } else if (pass == 2) {
@@ -563,7 +568,7 @@ struct Pipeline {
         const char* qe = getenv("HIPBP_QUAD");
         const char* qm = getenv("HIPBP_QUAD_MAX_ITEMS");
         const unsigned long long qmax = qm ? strtoull(qm, nullptr, 10) : QUAD_MAX_ITEMS;
-        const bool quad = sm_items > 0 && (qe ? atoi(qe) != 0 : sm_items <= qmax);
+        const bool quad = qe ? atoi(qe) != 0 : sm_items <= qmax;   // (a tick of chains alone is small too)
         if (quad) {   // re-lay the regions: scalar-multiplication items 4 lanes each
             unsigned long long tot = 0;
             for (int k = 0; k < tr.count; k++) {

@@ -144,7 +144,8 @@ void launch_lane_sort(const LaneSortPlan& plan, unsigned* bins, unsigned* offs, 
 // RK_POLY (mode 2: polynomial identity sides), RK_M3 (mode 2: method-3 products), RK_FINAL
 // (P, check point, accept).
 enum RegionKind { RK_STAGE0 = 0, RK_ROUND = 1, RK_FINAL_TERMS = 2, RK_FINAL = 4, RK_PREP = 5,
-                  RK_TREE = 6, RK_POLY = 7, RK_M3 = 8 };
+                  RK_TREE = 6, RK_POLY = 7, RK_M3 = 8,
+                  RK_LTREE = 9 /* the n <= LANE_TREE_MAX MSM trees, one lane (quad) per proof, into msm_part */ };
 struct Region {
     int kind;
     int slot;
@@ -153,8 +154,9 @@ struct Region {
     unsigned long long begin;
     unsigned long long items;   // lanes [begin+items, next begin) are wave-alignment padding
 };
-// MSMs of at most this many points (the range proofs') are reduced by final_task's lane,
-// one MSM tree per lane (63 adds for n = 64, lanes fully busy, latency well inside a tick);
+// MSMs of at most this many points (the range proofs') are reduced by one lane per proof (the
+// RK_LTREE region, a few ticks before the final one), one MSM tree per lane (63 adds for n = 64,
+// lanes fully busy, latency well inside a tick);
 // larger ones by RK_TREE blocks (levels 1..128 with LDS barriers) + final_task's upper levels.
 constexpr int LANE_TREE_MAX = 64;
 constexpr int MAX_REGIONS = 24;   // >= log2(MAX_N) + 3 stages in flight + 3 stages with 2 regions
@@ -179,7 +181,7 @@ inline bool region_is_sm(int kind) {
     return kind == RK_STAGE0 || kind == RK_ROUND || kind == RK_FINAL_TERMS || kind == RK_M3;
 }
 // regions whose items take a lane quad in the drain-tick form (the final assembly's point adds too)
-inline bool region_quad_lanes(int kind) { return region_is_sm(kind) || kind == RK_FINAL; }
+inline bool region_quad_lanes(int kind) { return region_is_sm(kind) || kind == RK_FINAL || kind == RK_LTREE; }
 
 // Generic canonical-tree MSM.  perm [m] / bins [MSM_BINS] (nullable): workspace of the
 // counting sort that groups items of equal chain length into the same waves (m >= MSM_SORT_MIN).

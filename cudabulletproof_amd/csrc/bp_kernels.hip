@@ -532,13 +532,10 @@ __device__ __forceinline__ void final_task(const SlotDev& sd, size_t p) {
     if (sd.range_mode) {
         ge m0, m1;
         const int n = sd.bv.n;
-        if (sd.lane_tree) {         // the whole tree here: every add with all 64 lanes busy
-            m0 = tree_upper<QUAD>(ws.msm_pts + (p * 2 + 0) * n, n, 1);
-            m1 = tree_upper<QUAD>(ws.msm_pts + (p * 2 + 1) * n, n, 1);
-        } else if (n > TPB) {       // upper tree levels over the per-block chunk roots (RK_TREE)
+        if (n > TPB) {              // upper tree levels over the per-block chunk roots (RK_TREE)
             m0 = tree_upper<QUAD>(ws.msm_pts + (p * 2 + 0) * n, n / TPB, TPB);
             m1 = tree_upper<QUAD>(ws.msm_pts + (p * 2 + 1) * n, n / TPB, TPB);
-        } else {
+        } else {                    // RK_TREE blocks (n <= TPB) or RK_LTREE (lane trees) wrote them
             m0 = ws.msm_part[p * 2 + 0];
             m1 = ws.msm_part[p * 2 + 1];
         }
@@ -606,6 +603,20 @@ __device__ __forceinline__ void final_task(const SlotDev& sd, size_t p) {
     for (int i = 0; i < 32; i++) hz += ((hs.v[i >> 3] >> (8 * (i & 7))) & 0xff) != 0;
     bool accept = (sx + sy >= 20) | (msb >= 28) | (xd + yd <= 32) | (hz <= 24);
     if (wr) sd.ok[p] = (ws.ipok[p] && accept) ? 1 : 0;
+}
+
+// The two MSMs' canonical trees of a proof whose MSMs have n <= LANE_TREE_MAX points (RK_LTREE):
+// every add with all lanes busy; QUAD (drain ticks): on the proof's lane quad.
+template <bool QUAD>
+__device__ __forceinline__ void ltree_task(const SlotDev& sd, size_t p) {
+    const VerifyWs& ws = sd.ws;
+    const int n = sd.bv.n;
+    const ge m0 = tree_upper<QUAD>(ws.msm_pts + (p * 2 + 0) * n, n, 1);
+    const ge m1 = tree_upper<QUAD>(ws.msm_pts + (p * 2 + 1) * n, n, 1);
+    if (!QUAD || (threadIdx.x & 3) == 0) {
+        ws.msm_part[p * 2 + 0] = m0;
+        ws.msm_part[p * 2 + 1] = m1;
+    }
 }
 
 // range_proof_verify's polynomial identity sides and methods 1-2 (rp.cu:452-530), then the
@@ -820,6 +831,9 @@ __global__ __launch_bounds__(TPB, BP_TERMS_OCC) void k_terms(RegionList rl, cons
     } else if (rg.kind == RK_FINAL) {
         if (QUAD) final_task<true>(sd, l >> 2);
         else final_task<false>(sd, l);
+    } else if (rg.kind == RK_LTREE) {
+        if (QUAD) ltree_task<true>(sd, l >> 2);
+        else ltree_task<false>(sd, l);
     } else {
         // the scalar-multiplication kinds: fill the job, then the one call site
         SmJob jb;
