@@ -299,6 +299,8 @@ struct Gens {
 // Drain-tick threshold (Pipeline::push): ticks with at most this many scalar-multiplication items
 // run them on lane quads.
 constexpr unsigned long long QUAD_MAX_ITEMS = 49152;
+// ... and up to this many on lane pairs.
+constexpr unsigned long long PAIR_MAX_ITEMS = 98304;
 
 struct Pipeline {
     Engine* e = nullptr;
@@ -559,21 +561,26 @@ struct Pipeline {
         if (overflow) { g_err = "pipeline region list overflow (internal)"; return HIPBP_ERR_ARG; }
         // Drain-tick form: a tick whose scalar multiplications cannot fill the SIMDs (the last
         // fold rounds and final terms of the last batches, a one-proof verify) lasts one
-        // scalar-multiplication chain's latency; its items then take a lane quad each (k_terms<true>,
+        // scalar-multiplication chain's latency; its items then take a lane quad each (k_terms<4>,
         // 3 product latencies per point op instead of 9).  HIPBP_QUAD=0/1 forces it off/on;
         // HIPBP_QUAD_MAX_ITEMS sets the tick's scalar-multiplication items up to which it is used.
         unsigned long long sm_items = 0;
         for (int k = 0; k < tr.count; k++)
             if (bp::region_is_sm(tr.reg[k].kind)) sm_items += tr.reg[k].items;
+        // Between the two (up to PAIR_MAX_ITEMS), lane pairs (HIPBP_QUAD=2 forces them,
+        // HIPBP_PAIR_MAX_ITEMS sets the bound).
         const char* qe = getenv("HIPBP_QUAD");
         const char* qm = getenv("HIPBP_QUAD_MAX_ITEMS");
+        const char* pm = getenv("HIPBP_PAIR_MAX_ITEMS");
         const unsigned long long qmax = qm ? strtoull(qm, nullptr, 10) : QUAD_MAX_ITEMS;
-        const bool quad = qe ? atoi(qe) != 0 : sm_items <= qmax;   // (a tick of chains alone is small too)
-        if (quad) {   // re-lay the regions: scalar-multiplication items 4 lanes each
+        const unsigned long long pmax = pm ? strtoull(pm, nullptr, 10) : PAIR_MAX_ITEMS;
+        int ql = sm_items <= qmax ? 4 : sm_items <= pmax ? 2 : 1;   // (a tick of chains alone is small too)
+        if (qe) ql = atoi(qe) == 1 ? 4 : atoi(qe) == 2 ? 2 : 1;
+        if (ql > 1) {   // re-lay the regions: scalar-multiplication items ql lanes each
             unsigned long long tot = 0;
             for (int k = 0; k < tr.count; k++) {
                 bp::Region& g = tr.reg[k];
-                if (bp::region_quad_lanes(g.kind)) g.items *= 4;
+                g.items *= bp::region_lanes(g.kind, ql);
                 g.begin = tot;
                 const unsigned long long al = g.kind == bp::RK_TREE ? 256 : 64;
                 tot += (g.items + al - 1) & ~(al - 1);
@@ -582,7 +589,7 @@ struct Pipeline {
         }
         if (tr.total >= (1ull << 32)) { g_err = "pipeline tick exceeds 2^32 lanes (batch too large for n)"; return HIPBP_ERR_ARG; }
         if (tm) tm->mark(bp::KT_TERMS, false, s);
-        bp::launch_terms(tr, slots_dev, G, H, g ? g : h, h, e->dtab, e->two_i, s, quad);
+        bp::launch_terms(tr, slots_dev, G, H, g ? g : h, h, e->dtab, e->two_i, s, ql);
         if (tm) tm->mark(bp::KT_TERMS, true, s);
         BP_RET_ON(hipGetLastError());
         if (has && plan.count) {   // the new batch's scalars exist now (its RK_PREP ran): order its lanes

@@ -174,14 +174,19 @@ void launch_init_tables(ge* dtab, fe* two_i, int nmax, hipStream_t s);
 // Prefix tables (SlotDev::ptab) of the bases G[0..n), H[0..n), h, g (g nullable: its rows are
 // left unwritten): tab[(2n + 2) << K].
 void launch_prefix_tables(ge* tab, const ge* G, const ge* H, const ge* h, const ge* g, int n, int K, hipStream_t s);
-// quad: the drain-tick form (scalar-multiplication regions' items take 4 lanes each, k_terms<true>)
+// ql: lanes per scalar-multiplication item (1; 2: lane pairs; 4: lane quads, the drain-tick form,
+// whose chain regions take 4 lanes per proof too), k_terms<ql>
 void launch_terms(const RegionList& rl, const SlotDev* slots, const ge* G, const ge* H, const ge* g, const ge* h,
-                  const ge* dtab, const fe* two_i, hipStream_t s, bool quad = false);
+                  const ge* dtab, const fe* two_i, hipStream_t s, int ql = 1);
 inline bool region_is_sm(int kind) {
     return kind == RK_STAGE0 || kind == RK_ROUND || kind == RK_FINAL_TERMS || kind == RK_M3;
 }
-// regions whose items take a lane quad in the drain-tick form (the final assembly's point adds too)
-inline bool region_quad_lanes(int kind) { return region_is_sm(kind) || kind == RK_FINAL || kind == RK_LTREE; }
+// lanes per item of a region in the form with ql lanes per scalar multiplication (the chain regions
+// go on quads in the quad form only)
+inline int region_lanes(int kind, int ql) {
+    if (region_is_sm(kind)) return ql;
+    return (ql == 4 && (kind == RK_FINAL || kind == RK_LTREE)) ? 4 : 1;
+}
 
 // Generic canonical-tree MSM.  perm [m] / bins [MSM_BINS] (nullable): workspace of the
 // counting sort that groups items of equal chain length into the same waves (m >= MSM_SORT_MIN).

@@ -786,11 +786,13 @@ void launch_lane_sort(const LaneSortPlan& plan, unsigned* bins, unsigned* offs, 
 // segments of the batch's 2B MSMs with the canonical tree of k_tree, barriers block-uniform;
 // its LDS is the q-operand array (no scalar multiplication runs in those blocks).
 //
-// QUAD (the drain ticks, Pipeline::push): every scalar-multiplication item takes a lane quad
-// instead of a lane (region items are 4 lanes each) and runs sm_quad — 3 product latencies per
-// point operation instead of 9, for ticks too small to fill the SIMDs, whose time is one
-// scalar-multiplication chain's latency.  The same operations, so the same bits.
-template <bool QUAD>
+// QL = lanes per scalar-multiplication item (Pipeline::push picks it per tick): 1 the throughput
+// form; 4 (the drain ticks, too small to fill the SIMDs, whose time is one scalar-multiplication
+// chain's latency) a lane quad per item running sm_quad, 3 product latencies per point operation
+// instead of 9, and the chains (RK_LTREE, RK_FINAL) on quads too; 2 a lane pair per item running
+// sm_pair (5 product latencies, 10 products instead of 9), for ticks between the two.  Region items
+// are QL lanes each.  The same operations in every form, so the same bits.
+template <int QL>
 __global__ __launch_bounds__(TPB, BP_TERMS_OCC) void k_terms(RegionList rl, const SlotDev* __restrict__ slots,
                                                const ge* __restrict__ G, const ge* __restrict__ H,
                                                const ge* __restrict__ g, const ge* __restrict__ h,
@@ -829,10 +831,10 @@ __global__ __launch_bounds__(TPB, BP_TERMS_OCC) void k_terms(RegionList rl, cons
     } else if (rg.kind == RK_POLY) {
         poly_task(sd, l);
     } else if (rg.kind == RK_FINAL) {
-        if (QUAD) final_task<true>(sd, l >> 2);
+        if (QL == 4) final_task<true>(sd, l >> 2);
         else final_task<false>(sd, l);
     } else if (rg.kind == RK_LTREE) {
-        if (QUAD) ltree_task<true>(sd, l >> 2);
+        if (QL == 4) ltree_task<true>(sd, l >> 2);
         else ltree_task<false>(sd, l);
     } else {
         // the scalar-multiplication kinds: fill the job, then the one call site
@@ -840,7 +842,8 @@ __global__ __launch_bounds__(TPB, BP_TERMS_OCC) void k_terms(RegionList rl, cons
         jb.base = -1;
         bool live = true;
         uint32_t li = (uint32_t)l;   // < 2^32: Pipeline::push keeps a tick below 2^32 lanes
-        if (QUAD) li >>= 2;          // the quad's item
+        if (QL == 4) li >>= 2;       // the quad's / pair's item
+        if (QL == 2) li >>= 1;
         if (rg.kind == RK_STAGE0) {
             const uint32_t it = stage0_item(sd, li);
             live = it != UINT32_MAX && stage0_job(sd, it, G, H, g, h, jb);
@@ -856,9 +859,12 @@ __global__ __launch_bounds__(TPB, BP_TERMS_OCC) void k_terms(RegionList rl, cons
         }
         if (live) {
             const ge* pt = (sd.ptab && jb.base >= 0) ? sd.ptab + ((size_t)jb.base << sd.pbits) : nullptr;
-            if (QUAD) {
+            if (QL == 4) {
                 const ge t = sm_quad(jb.s, jb.P, dtab, pt, pt ? sd.pbits : 0);
                 if ((threadIdx.x & 3) == 0) *jb.dst = jb.dev_norm ? ge_norm_dev(t) : ge_norm_host(t);
+            } else if (QL == 2) {
+                const ge t = sm_pair(jb.s, jb.P, dtab, pt, pt ? sd.pbits : 0);
+                if ((threadIdx.x & 1) == 0) *jb.dst = jb.dev_norm ? ge_norm_dev(t) : ge_norm_host(t);
             } else {
                 ge t = scalarmult<true>(jb.s, jb.P, &qs[threadIdx.x], dtab, pt, pt ? sd.pbits : 0);
                 *jb.dst = jb.dev_norm ? ge_norm_dev(t) : ge_norm_host(t);
@@ -870,10 +876,11 @@ __global__ __launch_bounds__(TPB, BP_TERMS_OCC) void k_terms(RegionList rl, cons
 static inline unsigned nblk(size_t items) { return (unsigned)((items + TPB - 1) / TPB); }
 
 void launch_terms(const RegionList& rl, const SlotDev* slots, const ge* G, const ge* H, const ge* g, const ge* h,
-                  const ge* dtab, const fe* two_i, hipStream_t s, bool quad) {
+                  const ge* dtab, const fe* two_i, hipStream_t s, int ql) {
     if (!rl.total) return;
-    if (quad) k_terms<true><<<nblk(rl.total), TPB, 0, s>>>(rl, slots, G, H, g, h, dtab, two_i);
-    else k_terms<false><<<nblk(rl.total), TPB, 0, s>>>(rl, slots, G, H, g, h, dtab, two_i);
+    if (ql == 4) k_terms<4><<<nblk(rl.total), TPB, 0, s>>>(rl, slots, G, H, g, h, dtab, two_i);
+    else if (ql == 2) k_terms<2><<<nblk(rl.total), TPB, 0, s>>>(rl, slots, G, H, g, h, dtab, two_i);
+    else k_terms<1><<<nblk(rl.total), TPB, 0, s>>>(rl, slots, G, H, g, h, dtab, two_i);
 }
 
 

@@ -1206,10 +1206,11 @@ def _sample_vs_oracle(oracle, n, B, arrays, ok, P, G, H, g, h, step=5):
                                                (64, 20, 2, 0, 3), (4, 5, 1, 1, 1), (16, 6, 0, 9, 2),
                                                (1, 3, 1, 0, 1), (64, 1, 1, 0, 1)])
 def test_pipeline_quad_ticks_same_bits(bp, oracle, monkeypatch, n, B, mode, K, pushes):
-    """The drain-tick form (k_terms<true>: every scalar multiplication on a lane quad, sm_quad)
-    forced on every tick (HIPBP_QUAD=1) gives bit-identical verdicts, P, check points, mode-2
-    flags and polynomial sides to the lane form forced everywhere (HIPBP_QUAD=0): every region
-    kind, with and without prefix tables, batches in flight together; a sample equals the oracle."""
+    """The drain-tick forms — k_terms<4> (every scalar multiplication on a lane quad, sm_quad, the
+    chains too) and k_terms<2> (lane pairs, sm_pair) — forced on every tick (HIPBP_QUAD=1 / 2) give
+    bit-identical verdicts, P, check points, mode-2 flags and polynomial sides to the lane form
+    forced everywhere (HIPBP_QUAD=0): every region kind, with and without prefix tables, batches in
+    flight together; a sample equals the oracle."""
     from cudabulletproof_amd import synth
     G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
     g, h = oracle.gh()
@@ -1225,12 +1226,13 @@ def test_pipeline_quad_ticks_same_bits(bp, oracle, monkeypatch, n, B, mode, K, p
     import torch
     Pg = torch.from_numpy(oracle.base_points(B, 9).view(np.int64)).to("cuda:0")
     outs = []
-    for q in ("0", "1"):
+    for q in ("0", "1", "2"):   # lanes, quads, pairs on every tick
         monkeypatch.setenv("HIPBP_QUAD", q)
         outs.append(_pipeline_outputs(bp, n, B, mode, arrays, G, H, g, h, Pg, bits=K, pushes=pushes))
-    for oa, ob in zip(*outs):
-        for a, b in zip(oa, ob):
-            assert torch.equal(a, b)
+    for other in outs[1:]:
+        for oa, ob in zip(outs[0], other):
+            for a, b in zip(oa, ob):
+                assert torch.equal(a, b)
     if mode == 1:
         o = outs[1][-1]
         _sample_vs_oracle(oracle, n, B, arrays, o[0].numpy().astype(bool), o[1].numpy().view(np.uint64), G, H, g, h)
