@@ -121,7 +121,7 @@ constexpr int MSM_BINS = 513;   // chain lengths 0..512
 
 enum SortSetKind { SS_STAGE0 = 0, SS_ROUND = 1, SS_FT = 2 };
 constexpr int LANE_SORT_SETS = 18;
-constexpr int LANE_SORT_BLOCK = 1024;
+constexpr int LANE_SORT_BLOCK = 256;   // one wave per SIMD: fits beside a running k_terms launch
 struct LaneSortPlan {
     int count;
     int pad;

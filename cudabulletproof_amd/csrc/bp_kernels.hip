@@ -731,22 +731,39 @@ __global__ __launch_bounds__(LANE_SORT_BLOCK) void k_lane_hist(LaneSortPlan pl, 
 }
 
 // Per set (one block each): longest-first exclusive scan of its bins into offs; bins re-zeroed.
-__global__ __launch_bounds__(SCAN_T) void k_lane_scan(unsigned* bins, unsigned* offs, int longest_first) {
-    __shared__ unsigned a[SCAN_T];
-    const int t = threadIdx.x, k = longest_first ? OPS_BINS - 1 - t : t;
+// LANE_SORT_BLOCK (256) threads, LS_PER consecutive scan positions each: a small block gets a CU as
+// soon as one block of a running k_terms launch retires there (a 1024-thread block needs a whole
+// CU's wave slots and waited for milliseconds behind a concurrent pipeline's stage-0 tick).
+constexpr int LS_PER = (OPS_BINS + LANE_SORT_BLOCK - 1) / LANE_SORT_BLOCK;
+__global__ __launch_bounds__(LANE_SORT_BLOCK) void k_lane_scan(unsigned* bins, unsigned* offs, int longest_first) {
+    __shared__ unsigned wsum[LANE_SORT_BLOCK / 64];
+    const int t = threadIdx.x;
     unsigned* bb = bins + (size_t)blockIdx.x * OPS_BINS;
-    const unsigned v = t < OPS_BINS ? bb[k] : 0u;
-    a[t] = v;
-    __syncthreads();
-    for (int off = 1; off < SCAN_T; off <<= 1) {
-        unsigned x = t >= off ? a[t - off] : 0u;
-        __syncthreads();
-        a[t] += x;
-        __syncthreads();
+    unsigned v[LS_PER], sum = 0;
+#pragma unroll
+    for (int u = 0; u < LS_PER; u++) {   // scan position p = LS_PER t + u -> bin k(p)
+        const int p = LS_PER * t + u, k = longest_first ? OPS_BINS - 1 - p : p;
+        v[u] = p < OPS_BINS ? bb[k] : 0u;
+        sum += v[u];
     }
-    if (t < OPS_BINS) {
-        offs[(size_t)blockIdx.x * OPS_BINS + k] = a[t] - v;
-        bb[k] = 0;
+    unsigned inc = sum;   // inclusive scan over the block: waves, then the wave totals
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned x = __shfl_up(inc, d, 64);
+        if ((t & 63) >= d) inc += x;
+    }
+    if ((t & 63) == 63) wsum[t >> 6] = inc;
+    __syncthreads();
+    unsigned run = inc - sum;
+    for (int w = 0; w < (t >> 6); w++) run += wsum[w];
+#pragma unroll
+    for (int u = 0; u < LS_PER; u++) {
+        const int p = LS_PER * t + u, k = longest_first ? OPS_BINS - 1 - p : p;
+        if (p < OPS_BINS) {
+            offs[(size_t)blockIdx.x * OPS_BINS + k] = run;
+            bb[k] = 0;
+        }
+        run += v[u];
     }
 }
 
@@ -773,7 +790,7 @@ __global__ __launch_bounds__(LANE_SORT_BLOCK) void k_lane_scatter(LaneSortPlan p
 void launch_lane_sort(const LaneSortPlan& plan, unsigned* bins, unsigned* offs, hipStream_t s) {
     if (!plan.count || !plan.blocks) return;
     k_lane_hist<<<plan.blocks, LANE_SORT_BLOCK, 0, s>>>(plan, bins);
-    k_lane_scan<<<plan.count, SCAN_T, 0, s>>>(bins, offs, plan.longest_first);
+    k_lane_scan<<<plan.count, LANE_SORT_BLOCK, 0, s>>>(bins, offs, plan.longest_first);
     k_lane_scatter<<<plan.blocks, LANE_SORT_BLOCK, 0, s>>>(plan, offs);
 }
 
