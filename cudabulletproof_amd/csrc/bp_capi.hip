@@ -347,11 +347,11 @@ struct Pipeline {
     int lane_sort_mask = 7;   // bit 0 stage 0, bit 1 rounds, bit 2 final terms, bit 3 shortest first
     Buf sort_bins, sort_offs;
     bp::LaneSortPlan plan{};
-    // The lane sort's three small launches run on a high-priority stream of their own (between
-    // two events), so a concurrent pipeline's big tick on another stream cannot starve them of
-    // workgroup slots and hold this pipeline's next tick back (measured: a 4096-proof shard batch's
-    // sort waited 7 ms behind the other pipeline's stage 0).  HIPBP_SORT_STREAM=0: on the
-    // pipeline's own stream.
+    // HIPBP_SORT_STREAM=1: the lane sort's three small launches on a high-priority stream of their
+    // own (between two events), so a concurrent pipeline's big tick cannot starve them of workgroup
+    // slots (a 4096-proof shard batch's sort once waited 7 ms behind the other pipeline's stage 0).
+    // Off by default since the sort runs in 256-thread blocks, which fit beside a running tick:
+    // then 172.5 vs 171.5 K (shard) and 190.4 vs 189.5 K (headline) verifies/s without it.
     hipStream_t sort_s = nullptr;
     hipEvent_t ev_tick = nullptr, ev_sorted = nullptr;
     // fixed-base prefix tables of G, H, h, g (hipbp_pipeline_prefix_tables: ptab, owned; or a
@@ -378,7 +378,7 @@ struct Pipeline {
         for (auto& sl : slots)
             if ((r = hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming)) != hipSuccess) return r;
         const char* ss = getenv("HIPBP_SORT_STREAM");
-        if (!ss || atoi(ss) != 0) {
+        if (ss && atoi(ss) != 0) {
             int lo_pr = 0, hi_pr = 0;
             if ((r = hipDeviceGetStreamPriorityRange(&lo_pr, &hi_pr)) != hipSuccess) return r;
             if ((r = hipStreamCreateWithPriority(&sort_s, hipStreamNonBlocking, hi_pr)) != hipSuccess) return r;
