@@ -25,7 +25,7 @@ def test_traffic_model_terms():
     assert m["prefix_table_gathers"] == 1024 * 258 * 128
     assert m["msm_lane_trees"] == 1024 * 2 * 63 * 384
     assert bench.traffic_model(1024, 64, 0)["prefix_table_gathers"] == 0
-    assert bench.sm_per_verify(64) == 386
+    assert bench.sm_per_verify(64) == 384   # 2n MSM terms + 4 (n/2 + ... + 1) fold terms + t h, c Q, a0 G', b0 H'
 
 
 def test_rooflines_without_matching_pmc(monkeypatch):
