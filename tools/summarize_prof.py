@@ -24,8 +24,10 @@ def short(name):
     name = name.split("(")[0].replace("bp::", "")
     if name.startswith("void "):
         name = name[5:]
-    # k_terms<false>: the pipeline tick; k_terms<true>: its drain-tick (lane-quad) form
-    return name.replace("k_terms<false>", "k_terms").replace("k_terms<true>", "k_terms_quad")
+    # k_terms<1>: the pipeline tick (one lane per item); k_terms<2> / <4>: its drain-tick forms on a
+    # lane pair / quad
+    return (name.replace("k_terms<1>", "k_terms").replace("k_terms<2>", "k_terms_pair")
+            .replace("k_terms<4>", "k_terms_quad"))
 
 
 def load_counters(d):
@@ -110,7 +112,7 @@ def main():
               "| kernel | launches | grid | avg ms (rocprofv3) | avg ms (bench.py HIP events, same run) |",
               "|---|---|---|---|---|"]
     trace_ms = {}
-    for kern in ("k_terms", "k_msm_points", "k_combine", "k_tree"):
+    for kern in ("k_terms", "k_terms_pair", "k_terms_quad", "k_msm_points", "k_combine", "k_tree"):
         ds = [r for r in trace if short(r["Kernel_Name"]) == kern]
         if not ds:
             continue
@@ -134,7 +136,8 @@ def main():
               "| SQ_WAVES | VALU instr/wave | SALU instr/wave | LDS instr/wave | eff. clock GHz | VALU cyc/instr/SIMD |",
               "|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
     traffic = {}
-    for kern in ("k_terms", "k_msm_points", "k_combine", "k_tree", "k_prep_range", "k_prep_ipa"):
+    for kern in ("k_terms", "k_terms_pair", "k_terms_quad", "k_msm_points", "k_combine", "k_tree", "k_prep_range",
+                 "k_prep_ipa"):
         f, w, v, c = steady(fetch, kern), steady(write, kern), steady(valu, kern), steady(cyc, kern)
         if not f:
             continue
@@ -162,7 +165,7 @@ def main():
         lines += ["", "## VALU roofline (the binding resource), steady-state launches", "",
                   "| kernel | VALUBusy % | VALUUtilization % | INT32 VALU instr/wave | INT64 VALU instr/wave | "
                   "dual-issue quad-cycles/wave |", "|---|---|---|---|---|---|"]
-        for kern in ("k_terms", "k_msm_points", "k_combine", "k_tree"):
+        for kern in ("k_terms", "k_terms_pair", "k_terms_quad", "k_msm_points", "k_combine", "k_tree"):
             b, x, v = steady(busy, kern), steady(mix, kern), steady(valu, kern)
             if not b:
                 continue
