@@ -296,11 +296,16 @@ struct Gens {
     }
 };
 
-// Drain-tick threshold (Pipeline::push): ticks with at most this many scalar-multiplication items
-// run them on lane quads.
-constexpr unsigned long long QUAD_MAX_ITEMS = 49152;
-// ... and up to this many on lane pairs.
-constexpr unsigned long long PAIR_MAX_ITEMS = 98304;
+// Drain-tick thresholds (Pipeline::push): ticks with at most this many scalar-multiplication items
+// run them on lane quads, up to PAIR_MAX_ITEMS on lane pairs.  The cost model (tools/ubench_issue.hip
+// with -DLAT: one wave alone issues one instruction per ~9 cycles, the SIMD one per ~4.4): a tick
+// lasts about (instructions per wave) x max(9, 4.4 w) cycles for w waves per SIMD, counting the other
+// pipeline's concurrent tick (they drain side by side).  Quads cut the instructions per wave of a
+// point operation from ~1700 to ~750 for 4x the lanes, pairs to ~1140 for 2x: with both pipelines'
+// drains together, a 65,536-item tick is fastest on lanes, 32,768 on pairs, 16,384 on quads
+// (configs[4] shard: 173.8 K verifies/s vs 172.1 K with the round-3 bounds 49,152 / 98,304).
+constexpr unsigned long long QUAD_MAX_ITEMS = 16384;
+constexpr unsigned long long PAIR_MAX_ITEMS = 32768;
 
 struct Pipeline {
     Engine* e = nullptr;

@@ -809,8 +809,13 @@ void launch_lane_sort(const LaneSortPlan& plan, unsigned* bins, unsigned* offs, 
 // instead of 9, and the chains (RK_LTREE, RK_FINAL) on quads too; 2 a lane pair per item running
 // sm_pair (5 product latencies, 10 products instead of 9), for ticks between the two.  Region items
 // are QL lanes each.  The same operations in every form, so the same bits.
+#ifdef BP_TERMS_WPE   // A/B: a register budget for more waves per SIMD than k_terms runs (room for other kernels' waves)
+#define BP_TERMS_BOUNDS __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(BP_TERMS_WPE, 8)))
+#else
+#define BP_TERMS_BOUNDS __launch_bounds__(TPB, BP_TERMS_OCC)
+#endif
 template <int QL>
-__global__ __launch_bounds__(TPB, BP_TERMS_OCC) void k_terms(RegionList rl, const SlotDev* __restrict__ slots,
+__global__ BP_TERMS_BOUNDS void k_terms(RegionList rl, const SlotDev* __restrict__ slots,
                                                const ge* __restrict__ G, const ge* __restrict__ H,
                                                const ge* __restrict__ g, const ge* __restrict__ h,
                                                const ge* __restrict__ dtab, const fe* __restrict__ two_i) {
@@ -895,9 +900,11 @@ static inline unsigned nblk(size_t items) { return (unsigned)((items + TPB - 1) 
 void launch_terms(const RegionList& rl, const SlotDev* slots, const ge* G, const ge* H, const ge* g, const ge* h,
                   const ge* dtab, const fe* two_i, hipStream_t s, int ql) {
     if (!rl.total) return;
-    if (ql == 4) k_terms<4><<<nblk(rl.total), TPB, 0, s>>>(rl, slots, G, H, g, h, dtab, two_i);
-    else if (ql == 2) k_terms<2><<<nblk(rl.total), TPB, 0, s>>>(rl, slots, G, H, g, h, dtab, two_i);
-    else k_terms<1><<<nblk(rl.total), TPB, 0, s>>>(rl, slots, G, H, g, h, dtab, two_i);
+    // A/B knob: unused dynamic LDS per block, to cap how many k_terms blocks share a CU
+    static const unsigned pad = [] { const char* e = getenv("HIPBP_TERMS_LDS_PAD"); return e ? (unsigned)atoi(e) : 0u; }();
+    if (ql == 4) k_terms<4><<<nblk(rl.total), TPB, pad, s>>>(rl, slots, G, H, g, h, dtab, two_i);
+    else if (ql == 2) k_terms<2><<<nblk(rl.total), TPB, pad, s>>>(rl, slots, G, H, g, h, dtab, two_i);
+    else k_terms<1><<<nblk(rl.total), TPB, pad, s>>>(rl, slots, G, H, g, h, dtab, two_i);
 }
 
 

@@ -4,7 +4,8 @@ bench.py's sharded_2p16 leg does, timed for every (push batch, drain policy) pai
 policy is read per tick from the environment (HIPBP_QUAD, HIPBP_QUAD_MAX_ITEMS), so one process
 A/Bs them; every run's verdict digest must be the same.
 
-  python tools/shard_probe.py [shard] [push batches, comma-separated] [quad max items, comma-separated; 0 = off]
+  python tools/shard_probe.py [shard] [push batches, comma-separated] [quad max items, comma-separated; 0 = off;
+                                                                        "Q:P" also sets the pair bound P]
 """
 import hashlib
 import os
@@ -29,7 +30,7 @@ def schedule(spec):
     b = int(spec)
     return [min(b, shard - j) for j in range(0, shard, b)]
 pushes = [schedule(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1024,2048,4096").split(",")]
-qmaxes = [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "0,49152,131072,262144").split(",")]
+qmaxes = [x for x in (sys.argv[3] if len(sys.argv) > 3 else "0,49152,131072,262144").split(",")]
 reps = int(os.environ.get("REPS", "3"))
 n, B = 64, 1024
 dev = torch.device("cuda:0")
@@ -69,8 +70,13 @@ for seq in pushes:
         j += m
     batches = [bp.RangeProofBatch(n, **rows(j0, m)) for j0, m in jobs]
     offs = np.cumsum([0] + [m for _, m in jobs])
-    for qm in qmaxes:
+    for qspec in qmaxes:
+        qm = int(qspec.split(":")[0])
         os.environ["HIPBP_QUAD_MAX_ITEMS"] = str(qm)
+        if ":" in qspec:
+            os.environ["HIPBP_PAIR_MAX_ITEMS"] = qspec.split(":")[1]
+        else:
+            os.environ.pop("HIPBP_PAIR_MAX_ITEMS", None)
         if qm == 0:
             os.environ["HIPBP_QUAD"] = "0"
         else:
@@ -91,9 +97,10 @@ for seq in pushes:
             d = hashlib.sha256(ok.cpu().numpy().tobytes()).hexdigest()[:16]
             assert dig is None or d == dig, (d, dig)
             dig = d
-        print(f"push {'+'.join(map(str, seq)):24s}  quad_max {qm:7d}  {best * 1e3:7.2f} ms  {shard / best / 1e3:7.1f} K verifies/s  "
+        print(f"push {'+'.join(map(str, seq)):24s}  quad:pair {qspec:>13s}  {best * 1e3:7.2f} ms  {shard / best / 1e3:7.1f} K verifies/s  "
               f"digest {dig}", flush=True)
     for pp in pipes:
         pp.close()
 os.environ.pop("HIPBP_QUAD", None)
 os.environ.pop("HIPBP_QUAD_MAX_ITEMS", None)
+os.environ.pop("HIPBP_PAIR_MAX_ITEMS", None)

@@ -1,4 +1,5 @@
 // ubench_issue.hip — VALU issue cost per wave64 instruction on gfx950, in SHADER CLOCK cycles
+// (with LAT defined, ubench_lat: ONE wave per SIMD and one dependent chain, i.e. the latency)
 // (the clock the VALU runs at, whatever the DVFS state), for the opcodes of the verify's hot loop.
 //
 // ubench_enc.hip priced instructions from wall time at a nominal 2.4 GHz; the k_terms PMC run
@@ -15,7 +16,15 @@
 #include <vector>
 
 #define ITERS 8192
+#ifdef LAT
+#define CH 1      // one chain ...
+#define REP 16    // ... of 16 dependent copies per loop trip (the loop's own cost amortised)
+#define WPS 1
+#else
 #define CH 8
+#define REP 8
+#define WPS 8
+#endif
 
 #define OPS(X)                                                                                       \
     X(0, "v_addc_co_u32", "v_addc_co_u32_e64 %0, %3, %0, %1, %3")                          \
@@ -40,9 +49,10 @@
     X(19, "v_fma_f64", "v_fma_f64 %2, %2, %2, %2")                                                    \
     X(20, "v_mul_lo_u32", "v_mul_lo_u32 %0, %0, %1")                                                  \
     X(21, "v_mul_hi_u32", "v_mul_hi_u32 %0, %0, %1")                                                  \
-    X(22, "s_nop_0", "s_nop 0")
+    X(22, "s_nop_0", "s_nop 0")                                                                        \
+    X(23, "v_mov_b32_dpp", "v_mov_b32_dpp %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf")
 
-constexpr int NOPS = 23;
+constexpr int NOPS = 24;
 
 template <int OP>
 __global__ __launch_bounds__(256) void k(uint32_t* out, unsigned long long* clk, uint32_t seed) {
@@ -57,7 +67,8 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, unsigned long long* clk,
     const unsigned long long t0 = clock64(), r0 = wall_clock64();
     for (int it = 0; it < ITERS; it++) {
 #pragma unroll
-        for (int c = 0; c < CH; c++) {
+        for (int r = 0; r < REP; r++) {
+            const int c = r % CH;
 #define X(id, name, text) \
     if (OP == id) asm volatile(text : "+v"(a[c]), "+v"(b[c]), "+v"(w[c]), "+s"(sm[c]) : : "vcc");
             OPS(X)
@@ -96,7 +107,7 @@ void run(const char* name, uint32_t* out, unsigned long long* dclk, int blocks, 
     int rate_khz = 0;
     hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, 0);
     const double ghz = sc / sr * rate_khz * 1e-6;                 // shader clock during the loop
-    const double winstr = (double)waves * ITERS * CH;
+    const double winstr = (double)waves * ITERS * REP;
     const double cyc = (ms * 1e-3) * ghz * 1e9 * 1024 / winstr;   // issue cycles per wave-instr per SIMD
     printf("  \"%s\": {\"cycles\": %.3f, \"ghz\": %.4f, \"ms\": %.3f}%s\n", name, cyc, ghz, ms, last ? "" : ",");
     hipEventDestroy(e0);
@@ -117,12 +128,13 @@ void run_all(uint32_t* out, unsigned long long* dclk, int blocks) {
 int main() {
     hipDeviceProp_t p;
     hipGetDeviceProperties(&p, 0);
-    const int blocks = p.multiProcessorCount * 8;   // 8 blocks of 4 waves per CU = 8 waves per SIMD
+    const int blocks = p.multiProcessorCount * WPS;   // WPS blocks of 4 waves per CU = WPS waves per SIMD
     uint32_t* out;
     unsigned long long* dclk;
     hipMalloc(&out, (size_t)blocks * 256 * 4);
     hipMalloc(&dclk, (size_t)blocks * 4 * 16);
-    printf("{\"device\": \"%s\", \"cus\": %d, \"waves_per_simd\": 8, \"ops\": {\n", p.gcnArchName, p.multiProcessorCount);
+    printf("{\"device\": \"%s\", \"cus\": %d, \"waves_per_simd\": %d, \"chains\": %d, \"ops\": {\n", p.gcnArchName,
+           p.multiProcessorCount, WPS, CH);
     run_all<0>(out, dclk, blocks);
     printf("}}\n");
     hipFree(out);
