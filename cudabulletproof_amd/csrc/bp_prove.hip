@@ -530,9 +530,13 @@ void launch_prove(int stage, int r, const ProveIn& in, const ProveWs& ws, const 
                 k_prove_sort_scatter<<<(unsigned)((cap + SORT_T - 1) / SORT_T), SORT_T, 0, s>>>(in, ws);
             }
             break;
-        case PS_TERMS0:
-            k_prove_terms0<<<nblk(B * (4 * (size_t)n + 4) + 2 * n), TPB, 0, s>>>(in, ws, G, H, g, h, dtab);
+        case PS_TERMS0: {
+            // A/B knob: unused dynamic LDS per block, capping terms0 blocks per CU (room for the other
+            // stream's chains)
+            static const unsigned pad = [] { const char* e = getenv("HIPBP_PROVE_T0_PAD"); return e ? (unsigned)atoi(e) : 0u; }();
+            k_prove_terms0<<<nblk(B * (4 * (size_t)n + 4) + 2 * n), TPB, pad, s>>>(in, ws, G, H, g, h, dtab);
             break;
+        }
         case PS_CHAIN0: k_prove_chain0<<<nblk(B * 4), TPB, 0, s>>>(in, ws); break;
         case PS_COMMIT: k_prove_commit<<<nblk(B), TPB, 0, s>>>(in, ws, two_i); break;
         case PS_TERMS1: k_prove_terms1<<<nblk(B * 4), TPB, 0, s>>>(in, ws, g, h, dtab); break;

@@ -60,24 +60,42 @@ def prove_summary(tag):
     """tools/profile_prove.sh output -> profiles/rocprof_<tag>_prove_summary.md"""
     base = os.path.join(ROOT, "gpurun_out", f"prof_{tag}_prove")
     stats = list(csv.DictReader(open(os.path.join(base, "trace", "run_kernel_stats.csv"))))
-    busy = load_counters(os.path.join(base, "pmc_busy"))
-    valu = load_counters(os.path.join(base, "pmc_valu"))
+    pmc = {d: load_counters(os.path.join(base, d)) if os.path.isdir(os.path.join(base, d)) else {}
+           for d in ("pmc_busy", "pmc_valu", "pmc_fetch", "pmc_write")}
+    try:
+        bt = json.loads(open(os.path.join(base, "bench_trace.json")).read().strip().splitlines()[-1])
+        pv = bt.get("prove") or {}
+    except (OSError, ValueError, IndexError):
+        pv = {}
     lines = [f"# rocprofv3 summary — prover, {tag}", "",
-             "Command: `tools/profile_prove.sh " + tag + "` on one MI355X (tools/prove_probe.py 16384 random: "
-             "two batches of 16384 64-bit proofs, hipbp_batch_generate_range_proof on one stream).", "",
-             "## Kernel trace (`rocprofv3 --kernel-trace --stats`)", "",
-             "| kernel | calls | avg ms | total ms | % time | VALUBusy % (mean over launches) | VALU instr/wave |",
+             "Command: `tools/profile_prove.sh " + tag + "` on one MI355X: bench.py's prove leg (B = 65536 64-bit "
+             "proofs per hipbp_batch_generate_range_proof batch, K = 22 prefix tables, two streams, 2 timed + 1 "
+             "warm-up batch), after a 3-step verify leg whose kernels are not listed.",
+             "", f"Prove leg in the traced run: {pv.get('value', float('nan')):.0f} proofs/s "
+             f"({pv.get('ms_per_batch', float('nan')):.1f} ms per batch of {pv.get('batch', '?')}), "
+             f"deterministic across streams: {pv.get('deterministic_across_streams')}.", "",
+             "## Kernel trace (`rocprofv3 --kernel-trace --stats`) and PMC per launch (mean over launches)", "",
+             "| kernel | calls | avg ms | total ms | VALUBusy % | VALU instr/wave | HBM MB/launch (2xFETCH+WRITE) |",
              "|---|---|---|---|---|---|---|"]
+
+    def per(d, k, f):
+        return [f(v) for v in pmc[d].values() if v["kernel"] == k]
     for r in stats:
         k = short(r["Name"])
-        b = [v.get("VALUBusy", float("nan")) for v in busy.values() if v["kernel"] == k]
-        vi = [v.get("SQ_INSTS_VALU", 0) / v["SQ_WAVES"] for v in valu.values() if v["kernel"] == k and v.get("SQ_WAVES")]
+        if not k.startswith("k_prove"):
+            continue
+        b = per("pmc_busy", k, lambda v: v.get("VALUBusy", float("nan")))
+        vi = per("pmc_valu", k, lambda v: v.get("SQ_INSTS_VALU", 0) / v["SQ_WAVES"] if v.get("SQ_WAVES") else float("nan"))
+        fe = per("pmc_fetch", k, lambda v: v.get("FETCH_SIZE", float("nan")))
+        wr = per("pmc_write", k, lambda v: v.get("WRITE_SIZE", float("nan")))
+        hbm = (2 * mean(fe) + mean(wr)) * 1024 / 1e6 if fe and wr else float("nan")
         lines.append(f"| {k} | {r['Calls']} | {float(r['AverageNs']) / 1e6:.3f} | {float(r['TotalDurationNs']) / 1e6:.2f} | "
-                     f"{float(r['Percentage']):.1f} | {mean(b):.1f} | {mean(vi):.0f} |")
-    lines += ["", "Per-batch launches: prep, terms0 (all A/S terms: the heavy scalar-mults), chain0, commit, "
-              "terms1, tx, then per IPA round rterms/chain/round, final. rterms launches last about one "
-              "scalar-mult latency whatever their size (latency-bound tails); bench.py runs two batches on "
-              "two streams so one batch's tails run under the other's terms0."]
+                     f"{mean(b):.1f} | {mean(vi):.0f} | {hbm:.1f} |")
+    lines += ["", "Per batch: prep, sort, terms0 (all A/S terms: the heavy scalar-mults, K = 22 prefix tables for "
+              "the generator bases), chain0, commit, terms1, tx, then per IPA round rterms / chain / round, final. "
+              "The rterms and chain launches are latency-bound tails (one scalar-mult chain whatever their size); "
+              "the two streams put one batch's tails under the other's terms0.",
+              "HBM bytes apply the gfx950 FETCH_SIZE x2 correction (MI355X_MICROARCH.md)."]
     out_md = os.path.join(ROOT, "profiles", f"rocprof_{tag}_prove_summary.md")
     open(out_md, "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
