@@ -151,6 +151,7 @@ struct Engine {
     // different streams overlap (one batch's latency-bound stages under another's term launch)
     struct ProverBufs { Buf b[19]; };
     std::map<hipStream_t, ProverBufs*> provers;
+    hipEvent_t prove_gate = nullptr;   // HIPBP_PROVE_GATE: recorded after the last prover terms0
     // pinned host staging for the single-proof entry points (a pageable source of an
     // async copy must outlive the copy; this one does, and the stream is synced after use)
     uint8_t* pinned = nullptr;
@@ -1044,7 +1045,16 @@ static int prove_run(const hipbp_prove_input* in, const ge25519* G, const ge2551
     };
     run(bp::PS_PREP, 0);
     run(bp::PS_SORT0, 0);
+    // A/B knob (HIPBP_PROVE_GATE=1, off by default): terms0 of successive calls runs one after another
+    // across streams, so that each batch's latency-bound rest can run under the next batch's terms0
+    // (with HIPBP_PROVE_T0_PAD leaving it a wave slot).
+    static const bool gate = getenv("HIPBP_PROVE_GATE") && atoi(getenv("HIPBP_PROVE_GATE")) != 0;
+    if (gate) {
+        if (!e->prove_gate) BP_RET_ON(hipEventCreateWithFlags(&e->prove_gate, hipEventDisableTiming));
+        else BP_RET_ON(hipStreamWaitEvent(s, e->prove_gate, 0));
+    }
     run(bp::PS_TERMS0, 0);
+    if (gate) BP_RET_ON(hipEventRecord(e->prove_gate, s));
     run(bp::PS_CHAIN0, 0);
     run(bp::PS_COMMIT, 0);
     run(bp::PS_TERMS1, 0);
