@@ -22,6 +22,7 @@ import argparse
 import hashlib
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -78,6 +79,7 @@ def parse():
     ap.add_argument("--no-host", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip the headline self-check (verify_check)")
     ap.add_argument("--no-h2d", action="store_true", help="skip the H2D-inclusive headline (with_h2d)")
+    ap.add_argument("--no-repeats", action="store_true", help="skip the 5 repeated timed regions (repeats)")
     ap.add_argument("--rehearse", action="store_true",
                     help="exercise the N>1 path on one GPU (all ranks on cuda:0, gloo collectives); not a measurement")
     return ap.parse_args()
@@ -230,7 +232,6 @@ def configs0_leg(reps=15):
     all of its output; that exit status is recorded, not treated as an error.  Runs before this
     process touches the GPU (children only)."""
     import re
-    import statistics
     import subprocess
     ref = os.path.join(ROOT, "oracle", "_ref")
     cpu_bin, hip_bin = (os.path.join(ref, f"complete_bulletproof_test_{k}") for k in ("cpu", "hip"))
@@ -956,6 +957,20 @@ def main():
     dt = time.perf_counter() - t0
     stats = bp.timing_collect()
     bp.timing_enable(False)
+    # SURVEY 8(d) timing rule (>= 5 repetitions, median): the same K-step region 5 more times, the
+    # pipelines still full; `value` stays the first region (the driver's contract), these go beside it
+    reps = []
+    for _ in range(0 if args.no_repeats else 5):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        tr = time.perf_counter()
+        for k in range(args.steps):
+            step(k)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        reps.append(time.perf_counter() - tr)
     for pp in pipes:
         pp.flush()
     torch.cuda.synchronize(dev)
@@ -974,6 +989,10 @@ def main():
         c = torch.tensor([passes_warm], dtype=torch.int64, device=dev)
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
         passes_warm = int(c.item())
+        if reps:
+            t = torch.tensor(reps, dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            reps = [float(x) for x in t.tolist()]
 
     total = B * args.steps * world
     value = total / dt
@@ -1019,6 +1038,11 @@ def main():
                        "pipeline_depth": pipe.depth if pipe else None, "pipelines": len(pipes) or None,
                        "prefix_tables": prefix,
                        "proof_bytes": proof_bytes(n, 1), "passes_in_warmup_batch": passes_warm},
+            "repeats": ({"n": len(reps), "steps_each": args.steps,
+                         "median": total / statistics.median(reps), "min": total / max(reps),
+                         "max": total / min(reps), "unit": "verifies/s",
+                         "note": "the same K-step region 5 more times after `value`'s, pipelines full"}
+                        if reps else None),
             "roofline": roofline, "valu_roofline": valu_roofline, "cpu_baseline": cpu, "verify_check": check,
             "with_h2d": h2d, "configs0": configs0, "msm": msm, "ipa": ipa, "prove": prove,
             "sharded_2p16": sharded, "host_api": host_api,
