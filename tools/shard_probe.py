@@ -32,6 +32,7 @@ def schedule(spec):
 pushes = [schedule(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1024,2048,4096").split(",")]
 qmaxes = [x for x in (sys.argv[3] if len(sys.argv) > 3 else "0,49152,131072,262144").split(",")]
 reps = int(os.environ.get("REPS", "3"))
+RR = os.environ.get("RR", "0") == "1"   # round-robin drain after a sync on the pushes' first ticks
 n, B = 64, 1024
 dev = torch.device("cuda:0")
 bp.lib()
@@ -88,6 +89,11 @@ for seq in pushes:
             t0 = time.perf_counter()
             for k, b in enumerate(batches):
                 pipes[k % 2].push(b, ok[offs[k]:offs[k + 1]])
+            if RR:   # wait out the pushes' first ticks, then drain the pipelines tick by tick in turn
+                torch.cuda.synchronize()
+                for _ in range(max(pp.depth for pp in pipes)):
+                    for pp in pipes:
+                        pp.push(None)
             for pp in pipes:
                 pp.flush()
             torch.cuda.synchronize()
