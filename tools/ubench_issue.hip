@@ -50,9 +50,14 @@
     X(20, "v_mul_lo_u32", "v_mul_lo_u32 %0, %0, %1")                                                  \
     X(21, "v_mul_hi_u32", "v_mul_hi_u32 %0, %0, %1")                                                  \
     X(22, "s_nop_0", "s_nop 0")                                                                        \
-    X(23, "v_mov_b32_dpp", "v_mov_b32_dpp %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf")
+    X(23, "v_mov_b32_dpp", "v_mov_b32_dpp %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf")         \
+    X(24, "pair:mad+mov", "v_mad_u64_u32 %2, %3, %0, %1, %2\n\tv_mov_b32_e32 %0, %1")                    \
+    X(25, "pair:mad+add_u32", "v_mad_u64_u32 %2, %3, %0, %1, %2\n\tv_add_u32_e32 %0, %1, %0")           \
+    X(26, "pair:addc+mov", "v_addc_co_u32_e64 %0, %3, %0, %1, %3\n\tv_mov_b32_e32 %1, %0")               \
+    X(27, "pair:mad+addc", "v_mad_u64_u32 %2, %3, %0, %1, %2\n\tv_addc_co_u32_e64 %0, %3, %0, %1, %3")   \
+    X(28, "pair:mov+mov", "v_mov_b32_e32 %0, %1\n\tv_mov_b32_e32 %1, %0")
 
-constexpr int NOPS = 24;
+constexpr int NOPS = 29;
 
 template <int OP>
 __global__ __launch_bounds__(256) void k(uint32_t* out, unsigned long long* clk, uint32_t seed) {
