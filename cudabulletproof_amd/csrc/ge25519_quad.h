@@ -98,28 +98,78 @@ __device__ __forceinline__ ge ge_row_move(const ge& a) {
 // fe_mul(x, x) (== fe_sq(x), the same 512-bit product).  Each lane keeps only its own q-side
 // operand of P.  Leading zeros from dtab, or the K-bit prefix table of the base (ptab) as
 // scalarmult does; the result replicated over the quad.
-__device__ __forceinline__ ge sm_quad(const fe& s, const ge& P, const ge* __restrict__ dtab, const ge* ptab, int K) {
+//
+// Between operations the point is not replicated: each lane keeps only its own stage-1 operand
+// ("operand form"), with the lanes' roles chosen so that the stage-3 products land where the next
+// stage-1 operands are formed:
+//   stage 1   lane 0: A = (Y1-X1)(Y2-X2)   1: T1 T2   2: Z1 Z2   3: B = (Y1+X1)(Y2+X2)
+//   stage 3   lane 0: X3 = E F   1: T3 = E H   2: Z3 = G F   3: Y3 = G H   (bit 1 picks G over E,
+//             bit 0 H over F: two 2-way selects)
+// so T3 and Z3 are already the next T and Z operands, and lanes 0 and 3 swap X3 / Y3 (one DPP
+// quad_perm) to form Y3 - X3 and Y3 + X3.  One step: 745 VALU instead of 808 (tools/isa_count.py,
+// p_quad_step / p_quad_step_of); the products are the same (G F is the integer F G), so the bits.
+template <int CTRL>
+__device__ __forceinline__ fe fe_dpp(const fe& a) {
+    fe r;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)a.v[i], CTRL, 0xF, 0xF, true);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(a.v[i] >> 32), CTRL, 0xF, 0xF, true);
+        r.v[i] = (uint64_t)lo | ((uint64_t)hi << 32);
+    }
+    return r;
+}
+// p: r in operand form, o = this lane's stage-1 operand; q = this lane's q-side operand (the
+// doubling passes o); returns the result's stage-3 product (X3 | T3 | Z3 | Y3 by lane)
+__device__ __forceinline__ fe ge_quad_of_step(const fe& o, const fe& q) {
     const int qd = threadIdx.x & 3;
-    const fe qs = fe_sel4(qd, fe_sub(P.Y, P.X), fe_add(P.Y, P.X), P.T, P.Z);
+    const fe p1 = fe_mul(o, q);
+    const fe A = fe_quad_bcast<0>(p1), CT = fe_quad_bcast<1>(p1), D0 = fe_quad_bcast<2>(p1), B = fe_quad_bcast<3>(p1);
+    const fe C = fe_mul(CT, k_const());
+    const fe D = fe_add(D0, D0);
+    fe E, F, G, H;
+    fe_addsub(B, A, H, E);   // H = B + A, E = B - A
+    fe_addsub(D, C, G, F);   // G = D + C, F = D - C
+    return fe_mul(fe_sel(qd & 2, G, E), fe_sel(qd & 1, H, F));
+}
+// stage-3 products -> the next operation's operand form (lanes 0 <-> 3 swap: quad_perm [3,1,2,0]):
+// lane 0 Y3 - X3, lane 3 Y3 + X3 (= X3 + Y3: the sum and its lossy "- p" are symmetric)
+__device__ __forceinline__ fe quad_of_next(const fe& r3) {
+    const int qd = threadIdx.x & 3;
+    const fe sw = fe_dpp<0x27>(r3);
+    fe s, d;
+    fe_addsub(sw, r3, s, d);
+    return fe_sel(qd == 0, d, fe_sel(qd == 3, s, r3));
+}
+__device__ __forceinline__ fe quad_of_form(const ge& r) {
+    return fe_sel4(threadIdx.x & 3, fe_sub(r.Y, r.X), r.T, r.Z, fe_add(r.Y, r.X));
+}
+__device__ __forceinline__ ge quad_of_point(const fe& r3) {   // X3 | T3 | Z3 | Y3 -> replicated
+    return ge{fe_quad_bcast<0>(r3), fe_quad_bcast<3>(r3), fe_quad_bcast<2>(r3), fe_quad_bcast<1>(r3)};
+}
+__device__ __forceinline__ ge sm_quad(const fe& s, const ge& P, const ge* __restrict__ dtab, const ge* ptab, int K) {
+    const fe qs = quad_of_form(P);
     const int lz = fe_clz256(s);
     const bool pre = K > 0 && lz < K && ptab != nullptr;
-    ge r = *(pre ? &ptab[prefix_index(s, K)] : &dtab[lz]);
+    const ge r0 = *(pre ? &ptab[prefix_index(s, K)] : &dtab[lz]);
     int i = pre ? 255 - K : 255 - lz;   // index of the pending bit
-    BitStream bs = bs_init(s, i < 0 ? 0 : i);
-    uint32_t bit = i >= 0 ? bs_next(bs) : 0;
+    if (i < 0) return r0;
+    BitStream bs = bs_init(s, i);
+    uint32_t bit = bs_next(bs);
     bool add_phase = false;   // false: next op doubles; true: next op adds P
-    while (i >= 0) {
-        const fe x1 = fe_sel4(qd, fe_sub(r.Y, r.X), fe_add(r.Y, r.X), r.T, r.Z);
-        r = ge_quad_finish(fe_mul(x1, fe_sel(add_phase, qs, x1)));
+    fe o = quad_of_form(r0), r3;
+    while (true) {
+        r3 = ge_quad_of_step(o, fe_sel(add_phase, qs, o));
         if (!add_phase && bit) {
             add_phase = true;
         } else {
             add_phase = false;
-            i--;
+            if (--i < 0) break;
             bit = bs_next(bs);
         }
+        o = quad_of_next(r3);
     }
-    return r;
+    return quad_of_point(r3);
 }
 
 // The same on a lane PAIR: each lane forms two of a stage's four products (lane 0: A and T1 T2 /

@@ -25,4 +25,4 @@ def test_field_asm_header_is_generated(tmp_path):
     got, committed = _regen("gen_field_asm", "field_asm.h", tmp_path)
     assert got == committed
     # every exact form is reachable only through a rare-edge test and rejoins at the end
-    assert committed.count("s_cbranch_scc1") == 2 + 1 + 2 + 1   # sub 2, add 1, fold 2, canon 1
+    assert committed.count("s_cbranch_scc1") == 2 + 1 + 2 + 1 + 1   # sub 2, add 1, fold 2, canon 1, addsub 1

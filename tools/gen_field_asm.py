@@ -298,6 +298,119 @@ def gen_sub():
                                            "sq3", "srare"], lines)
 
 
+def renamed(ins, names):
+    """ins with its %[x] operands (and SGPR write/read lists) renamed by names {old: new}."""
+    out = []
+    for text, w, r, v in ins:
+        for a, b in names.items():
+            text = text.replace(f"%[{a}]", f"%[{b}]")
+        out.append((text, [names.get(x, x) for x in w], [names.get(x, x) for x in r], v))
+    return out
+
+
+def gen_addsub():
+    """fe_add(a, b) and fe_sub(a, b) of the same operands in one block (ge25519_add's E = B - A with
+    H = B + A, and F = D - C with G = D + C; the lane-quad forms' next operands Y - X / Y + X), for
+    the latency-bound drain chains: the two carry chains interleaved, so a link reads its carry two
+    instructions after the write (an s_nop 0 instead of an s_nop 1 per link), and one wave-uniform
+    rare-edge branch for both: sub's test 1 (some g_i, i = 1..3, may be 2^64-1), add's fix_test and
+    sub's test 2, OR-ed.  Fast path: add's fast fix-up and sub's fast "+ p".  Slow path: both from
+    the inputs again, exactly as fe_add_asm and fe_sub_asm do (add chain + fix_seq; sub's exact chain
+    + exact "+ p").  Same bits as the two separate blocks."""
+    h = [f"h{i}" for i in range(8)]   # a + b
+    pre = [V("v_max3_u32 %[vt3], %[b2], %[b4], %[b6]"),
+           V("v_cmp_eq_u32 %[sr1], -1, %[vt3]", ["sr1"]),
+           V("v_add_co_u32 %[h0], %[scy], %[a0], %[b0]", ["scy"]),
+           V("v_sub_co_u32 %[t0], %[sby], %[a0], %[b0]", ["sby"])]
+    for i in range(1, 8):
+        pre.append(V(f"v_addc_co_u32 %[h{i}], %[scy], %[a{i}], %[b{i}], %[scy]", ["scy"], ["scy"]))
+        pre.append(V(f"v_subb_co_u32 %[t{i}], %[sby], %[a{i}], %[b{i}], %[sby]", ["sby"], ["sby"]))
+    pre += [V("v_max_u32 %[vt3], %[h1], %[h4]"),                      # add: fix_test
+            V("v_not_b32 %[vt4], %[t1]"),                              # sub: test 2
+            V("v_cmp_gt_i32 %[stp], 0, %[h7]", ["stp"]),
+            V("v_max3_u32 %[vt4], %[vt4], %[t2], %[t4]"),
+            V("v_cmp_eq_u32 %[srare], -1, %[vt3]", ["srare"]),
+            V("v_cmp_eq_u32 %[sr2], -1, %[vt4]", ["sr2"]),
+            S("s_or_b64 %[sm], %[scy], %[stp]", ["sm"]),
+            S("s_or_b64 %[srare], %[srare], %[sr1]", ["srare"]),
+            S("s_or_b64 %[srare], %[srare], %[sr2]", ["srare"])]
+    fast = [V("v_cndmask_b32 %[vt1], 0, 19, %[sm]", [], ["sm"]),
+            V("v_cndmask_b32 %[vt4], 0, 19, %[sby]", [], ["sby"]),
+            V("v_cndmask_b32 %[vt2], 0, %[c80], %[sm]", [], ["sm"]),
+            V("v_cndmask_b32 %[vt5], 0, %[c80], %[sby]", [], ["sby"]),
+            V("v_add_co_u32 %[h0], %[sk0], %[h0], %[vt1]", ["sk0"]),
+            V("v_sub_co_u32 %[t0], %[sk1], %[t0], %[vt4]", ["sk1"]),
+            V("v_addc_co_u32 %[h4], %[sk2], %[h4], 0, %[sm]", ["sk2"], ["sm"]),
+            V("v_add_u32 %[h7], %[h7], %[vt2]"),
+            V("v_add_u32 %[t7], %[t7], %[vt5]"),
+            V("v_addc_co_u32 %[h1], %[sk0], %[h1], 0, %[sk0]", ["sk0"], ["sk0"]),
+            V("v_subb_co_u32 %[t1], %[sk1], %[t1], 0, %[sk1]", ["sk1"], ["sk1"]),
+            V("v_addc_co_u32 %[h5], %[sk2], %[h5], 0, %[sk2]", ["sk2"], ["sk2"])]
+    add_exact = [V("v_add_co_u32 %[h0], %[scy], %[a0], %[b0]", ["scy"])]
+    for i in range(1, 8):
+        add_exact.append(V(f"v_addc_co_u32 %[h{i}], %[scy], %[a{i}], %[b{i}], %[scy]", ["scy"], ["scy"]))
+    add_exact += fix_seq(h, h, "scy")
+    # sub's exact chain + exact "+ p" (gen_sub's sequences) on t, its borrow in sby
+    sub_exact = []
+    for i in (1, 2, 3):
+        sub_exact.append(V(f"v_and_b32 %[vt1], %[b{2 * i}], %[b{2 * i + 1}]"))
+        sub_exact.append(V(f"v_cmp_eq_u32 %[sq{i}], -1, %[vt1]", [f"sq{i}"]))
+    sub_exact.append(V("v_sub_co_u32 %[t0], %[sk0], %[a0], %[b0]", ["sk0"]))
+    sub_exact.append(V("v_subb_co_u32 %[t1], %[sby], %[a1], %[b1], %[sk0]", ["sby"], ["sk0"]))
+    for i in (1, 2, 3):
+        sub_exact.append(V(f"v_subb_co_u32 %[t{2 * i}], %[sk0], %[a{2 * i}], %[b{2 * i}], %[sby]", ["sk0"], ["sby"]))
+        sub_exact.append(V(f"v_subb_co_u32 %[t{2 * i + 1}], %[sk1], %[a{2 * i + 1}], %[b{2 * i + 1}], %[sk0]",
+                           ["sk1"], ["sk0"]))
+        sub_exact.append(S(f"s_and_b64 %[sq{i}], %[sq{i}], %[sby]", [f"sq{i}"]))
+        sub_exact.append(S(f"s_andn2_b64 %[sby], %[sk1], %[sq{i}]", ["sby"]))
+    sub_exact += renamed([
+        V("v_cndmask_b32 %[vt1], 0, 19, %[scy]", [], ["scy"]),
+        V("v_cndmask_b32 %[vt2], 0, %[c80], %[scy]", [], ["scy"]),
+        V("v_sub_co_u32 %[h0], %[sk0], %[h0], %[vt1]", ["sk0"]),
+        V("v_subb_co_u32 %[h1], %[sd1], %[h1], 0, %[sk0]", ["sd1"], ["sk0"]),
+        V("v_subb_co_u32 %[h2], %[sk1], %[h2], 0, %[sd1]", ["sk1"], ["sd1"]),
+        V("v_subb_co_u32 %[h3], %[sk1], %[h3], 0, %[sk1]", ["sk1"], ["sk1"]),
+        V("v_and_b32 %[vt1], %[h2], %[h3]"),
+        V("v_cmp_eq_u32 %[sd2], -1, %[vt1]", ["sd2"]),
+        S("s_and_b64 %[sd2], %[sd2], %[scy]", ["sd2"]),
+        V("v_subb_co_u32 %[h4], %[sk2], %[h4], 0, %[sd2]", ["sk2"], ["sd2"]),
+        V("v_subb_co_u32 %[h5], %[sk2], %[h5], 0, %[sk2]", ["sk2"], ["sk2"]),
+        V("v_and_b32 %[vt1], %[h4], %[h5]"),
+        V("v_cmp_eq_u32 %[sd3], -1, %[vt1]", ["sd3"]),
+        S("s_and_b64 %[sd3], %[sd3], %[scy]", ["sd3"]),
+        V("v_subb_co_u32 %[h6], %[sk3], %[h6], 0, %[sd3]", ["sk3"], ["sd3"]),
+        V("v_subb_co_u32 %[h7], %[sk3], %[h7], 0, %[sk3]", ["sk3"], ["sk3"]),
+        V("v_add_u32 %[h7], %[h7], %[vt2]")], {**{f"h{i}": f"t{i}" for i in range(8)}, "scy": "sby"})
+    lp, sp = schedule(pre + branch_if_rare("3f"))
+    lf, _ = schedule(fast, sp)
+    ls, _ = schedule(add_exact + sub_exact, sp)
+    lines = lp + lf + ["s_branch 4f", "3:"] + ls + ["4:"]
+    t = [f"t{i}" for i in range(8)]
+    sgprs = FIX_SGPRS + ["scy", "sby", "sr1", "sr2", "srare", "sq1", "sq2", "sq3"]
+    ins = [f"a{i}" for i in range(8)] + [f"b{i}" for i in range(8)]
+    text = "\\n\\t".join(lines + ["s_nop 4"])
+    out = ["// fe_add(a, b) and fe_sub(a, b) in one block (curve25519_ops.cu:41-90): the two carry chains",
+           "// interleaved, one rare-edge branch for both (tools/gen_field_asm.py gen_addsub).",
+           "__device__ __forceinline__ void fe_addsub_asm(uint32_t os[8], uint32_t od[8], const uint32_t fa[8], "
+           "const uint32_t ga[8]) {"]
+    for p, pre_ in (("fa", "a"), ("ga", "b")):
+        out.append("    const uint32_t " + ", ".join(f"{pre_}{i} = {p}[{i}]" for i in range(8)) + ";")
+    vt = ["vt1", "vt2", "vt3", "vt4", "vt5"]
+    out.append("    uint32_t " + ", ".join(h + t + vt) + ";")
+    out.append("    uint64_t " + ", ".join(sgprs) + ";")
+    out.append(f'    asm volatile("{text}"')
+    out.append("                 : " + ", ".join([f'[{x}] "=&v"({x})' for x in h + t + vt] +
+                                          [f'[{x}] "=&s"({x})' for x in sgprs]))
+    out.append("                 : " + ", ".join([f'[{x}] "v"({x})' for x in ins] +
+                                          ['[c80] "v"(0x80000000u)', '[p0l] "s"(0xFFFFFFEDu)']))
+    out.append('                 : "scc");')
+    for i in range(8):
+        out.append(f"    os[{i}] = h{i}; od[{i}] = t{i};")
+    out.append("    (void)" + "; (void)".join(sgprs + vt) + ";")
+    out.append("}")
+    return out
+
+
 def gen_canon():
     """host fe25519_tobytes' conditional "- p" (curve25519_ops.cu:220-251) = device fe_mul_one:
     the fix-up with no carry, in place."""
@@ -312,7 +425,7 @@ def main(path=OUT):
     out = ["// GENERATED by tools/gen_field_asm.py -- do not edit by hand.",
            "// gfx950 inline-asm fe25519 add and product fold: the same bits as the C forms in fe25519_dev.h.",
            "#pragma once", "#include <stdint.h>", "namespace bp {"]
-    out += gen_add() + [""] + gen_sub() + [""] + gen_fold() + [""] + gen_canon()
+    out += gen_add() + [""] + gen_sub() + [""] + gen_fold() + [""] + gen_canon() + [""] + gen_addsub()
     out.append("}  // namespace bp")
     open(path, "w").write("\n".join(out) + "\n")
     print("wrote", path)

@@ -29,3 +29,15 @@ extern "C" __global__ void p_ge_add_sel_zone(ge* o, const ge* p, const geq* q, c
     o[threadIdx.x] = ge_add_sel<true, true>(p[threadIdx.x], &qs[threadIdx.x], u[threadIdx.x] != 0);
 }
 extern "C" __global__ void p_fe_canon(fe* o, const fe* a) { o[threadIdx.x] = fe_canon(a[threadIdx.x]); }
+// one step of the drain-tick forms (sm_quad / sm_pair loop bodies): the latency-bound chains
+#include "../cudabulletproof_amd/csrc/ge25519_quad.h"
+extern "C" __global__ void p_quad_step(ge* o, const ge* p, const fe* qs, const int* u) {
+    const int qd = threadIdx.x & 3;
+    const ge r = p[threadIdx.x];
+    const fe x1 = fe_sel4(qd, fe_sub(r.Y, r.X), fe_add(r.Y, r.X), r.T, r.Z);
+    o[threadIdx.x] = ge_quad_finish(fe_mul(x1, fe_sel(u[threadIdx.x] != 0, qs[threadIdx.x], x1)));
+}
+extern "C" __global__ void p_quad_step_of(fe* o, const fe* p, const fe* qs, const int* u) {
+    const fe x = p[threadIdx.x];
+    o[threadIdx.x] = quad_of_next(ge_quad_of_step(x, fe_sel(u[threadIdx.x] != 0, qs[threadIdx.x], x)));
+}

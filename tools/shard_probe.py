@@ -33,6 +33,7 @@ pushes = [schedule(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1024,2048
 qmaxes = [x for x in (sys.argv[3] if len(sys.argv) > 3 else "0,49152,131072,262144").split(",")]
 reps = int(os.environ.get("REPS", "3"))
 RR = os.environ.get("RR", "0") == "1"   # round-robin drain after a sync on the pushes' first ticks
+NP = int(os.environ.get("NP", "2"))   # pipelines (streams)
 n, B = 64, 1024
 dev = torch.device("cuda:0")
 bp.lib()
@@ -47,7 +48,7 @@ for t in range(4):
                                         gens=gens)
     tiles.append({k: out[k] for k in bp.RangeProofBatch.FIELDS})
 torch.cuda.synchronize()
-streams = [torch.cuda.Stream(dev) for _ in range(2)]
+streams = [torch.cuda.Stream(dev) for _ in range(NP)]
 
 
 def rows(j0, m):
@@ -59,10 +60,10 @@ def rows(j0, m):
     return {f: torch.cat([tiles[t][f][r0:r0 + k] for t, r0, k in parts]) for f in bp.RangeProofBatch.FIELDS}
 
 
-print(f"shard {shard} proofs, two pipelines, K = {gens.bits}", flush=True)
+print(f"shard {shard} proofs, {NP} pipelines, K = {gens.bits}", flush=True)
 for seq in pushes:
     Bs = max(seq)
-    pipes = [bp.VerifyPipeline(Bs, n, Gd, Hd, hd, stream=streams[i]) for i in range(2)]
+    pipes = [bp.VerifyPipeline(Bs, n, Gd, Hd, hd, stream=streams[i]) for i in range(NP)]
     for pp in pipes:
         pp.use_gens(gens)
     jobs, j = [], 0
@@ -88,7 +89,7 @@ for seq in pushes:
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for k, b in enumerate(batches):
-                pipes[k % 2].push(b, ok[offs[k]:offs[k + 1]])
+                pipes[k % NP].push(b, ok[offs[k]:offs[k + 1]])
             if RR:   # wait out the pushes' first ticks, then drain the pipelines tick by tick in turn
                 torch.cuda.synchronize()
                 for _ in range(max(pp.depth for pp in pipes)):
