@@ -48,7 +48,10 @@ for t in range(4):
                                         gens=gens)
     tiles.append({k: out[k] for k in bp.RangeProofBatch.FIELDS})
 torch.cuda.synchronize()
-streams = [torch.cuda.Stream(dev) for _ in range(NP)]
+# PRIO=1: the last pipeline's stream at high priority (its stage 0 starts behind the first's lane sort,
+# so its drain ends last)
+PRIO = os.environ.get("PRIO", "0") == "1"
+streams = [torch.cuda.Stream(dev, priority=-1 if PRIO and i == NP - 1 else 0) for i in range(NP)]
 
 
 def rows(j0, m):
