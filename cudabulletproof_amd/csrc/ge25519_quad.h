@@ -106,7 +106,8 @@ __device__ __forceinline__ ge ge_row_move(const ge& a) {
 //   stage 3   lane 0: X3 = E F   1: T3 = E H   2: Z3 = G F   3: Y3 = G H   (bit 1 picks G over E,
 //             bit 0 H over F: two 2-way selects)
 // so T3 and Z3 are already the next T and Z operands, and lanes 0 and 3 swap X3 / Y3 (one DPP
-// quad_perm) to form Y3 - X3 and Y3 + X3.  One step: 745 VALU instead of 808 (tools/isa_count.py,
+// quad_perm) to form Y3 - X3 and Y3 + X3 (fe_addsub: both chains in one block).  One step: 744 VALU
+// and 103 s_nop instead of 808 and 139 (tools/isa_count.py,
 // p_quad_step / p_quad_step_of); the products are the same (G F is the integer F G), so the bits.
 template <int CTRL>
 __device__ __forceinline__ fe fe_dpp(const fe& a) {
@@ -172,10 +173,12 @@ __device__ __forceinline__ ge sm_quad(const fe& s, const ge& P, const ge* __rest
     return quad_of_point(r3);
 }
 
-// The same on a lane PAIR: each lane forms two of a stage's four products (lane 0: A and T1 T2 /
-// E F and F G; lane 1: B and Z1 Z2 / G H and E H) and the pair swaps them over DPP: 5 product
-// latencies per point operation instead of 9, with 10 products per operation instead of 9 (a quad
-// forms 12): the form for ticks that fill the SIMDs at two lanes per item but not at four.
+// The same on a lane PAIR, in operand form: lane 0 holds {Y-X, T}, lane 1 {Y+X, Z}; stage 1: lane 0
+// forms A and T1 T2, lane 1 B and Z1 Z2; the pair swaps them over DPP; stage 3: lane 0 X3 = E F and
+// T3 = E H, lane 1 Z3 = G F and Y3 = G H (one operand select: G over E on lane 1), so T3 and Z3 are
+// already the next operands and the pair swaps X3 / Y3 to form Y3 - X3 / Y3 + X3 (fe_addsub).  5
+// product latencies per point operation instead of 9, with 10 products per operation instead of 9
+// (a quad forms 12): the form for ticks that fill the SIMDs at two lanes per item but not at four.
 __device__ __forceinline__ fe fe_pair_swap(const fe& a) {   // lane l <- lane l ^ 1
     fe r;
 #pragma unroll
@@ -186,40 +189,62 @@ __device__ __forceinline__ fe fe_pair_swap(const fe& a) {   // lane l <- lane l 
     }
     return r;
 }
+__device__ __forceinline__ void pair_of_form(const ge& r, fe& oa, fe& ob) {
+    const bool odd = threadIdx.x & 1;
+    fe s, d;
+    fe_addsub(r.Y, r.X, s, d);
+    oa = fe_sel(odd, s, d);
+    ob = fe_sel(odd, r.Z, r.T);
+}
+// one operation from operand form (oa, ob) with this lane's q-side operands (qa, qb; the doubling
+// passes oa, ob): r1 = X3 | Z3, r2 = T3 | Y3
+__device__ __forceinline__ void ge_pair_of_step(const fe& oa, const fe& ob, const fe& qa, const fe& qb, fe& r1, fe& r2) {
+    const bool odd = threadIdx.x & 1;
+    const fe p1 = fe_mul(oa, qa);   // A | B
+    const fe p2 = fe_mul(ob, qb);   // T1 T2 | Z1 Z2
+    const fe o1 = fe_pair_swap(p1), o2 = fe_pair_swap(p2);
+    const fe A = fe_sel(odd, o1, p1), B = fe_sel(odd, p1, o1), CT = fe_sel(odd, o2, p2), D0 = fe_sel(odd, p2, o2);
+    const fe C = fe_mul(CT, k_const());
+    const fe D = fe_add(D0, D0);
+    fe E, F, G, H;
+    fe_addsub(B, A, H, E);
+    fe_addsub(D, C, G, F);
+    const fe x = fe_sel(odd, G, E);
+    r1 = fe_mul(x, F);
+    r2 = fe_mul(x, H);
+}
 __device__ __forceinline__ ge sm_pair(const fe& s, const ge& P, const ge* __restrict__ dtab, const ge* ptab, int K) {
     const bool odd = threadIdx.x & 1;
-    const fe qymx = fe_sub(P.Y, P.X), qypx = fe_add(P.Y, P.X);
-    const fe qa = fe_sel(odd, qypx, qymx), qb = fe_sel(odd, P.Z, P.T);   // this lane's q-side operands
+    fe qa, qb;   // this lane's q-side operands
+    pair_of_form(P, qa, qb);
     const int lz = fe_clz256(s);
     const bool pre = K > 0 && lz < K && ptab != nullptr;
-    ge r = *(pre ? &ptab[prefix_index(s, K)] : &dtab[lz]);
+    const ge r0 = *(pre ? &ptab[prefix_index(s, K)] : &dtab[lz]);
     int i = pre ? 255 - K : 255 - lz;   // index of the pending bit
-    BitStream bs = bs_init(s, i < 0 ? 0 : i);
-    uint32_t bit = i >= 0 ? bs_next(bs) : 0;
+    if (i < 0) return r0;
+    BitStream bs = bs_init(s, i);
+    uint32_t bit = bs_next(bs);
     bool add_phase = false;   // false: next op doubles; true: next op adds P
-    while (i >= 0) {
-        const fe xa = fe_sel(odd, fe_add(r.Y, r.X), fe_sub(r.Y, r.X)), xb = fe_sel(odd, r.Z, r.T);
-        const fe p1 = fe_mul(xa, fe_sel(add_phase, qa, xa));   // A (lane 0) / B (lane 1)
-        const fe p2 = fe_mul(xb, fe_sel(add_phase, qb, xb));   // T1 T2 / Z1 Z2
-        const fe o1 = fe_pair_swap(p1), o2 = fe_pair_swap(p2);
-        const fe A = fe_sel(odd, o1, p1), B = fe_sel(odd, p1, o1), CT = fe_sel(odd, o2, p2);
-        fe D = fe_sel(odd, p2, o2);
-        const fe C = fe_mul(CT, k_const());
-        D = fe_add(D, D);
-        const fe E = fe_sub(B, A), F = fe_sub(D, C), G = fe_add(D, C), H = fe_add(B, A);
-        const fe r1 = fe_mul(fe_sel(odd, G, E), fe_sel(odd, H, F));   // X3 = E F (lane 0) / Y3 = G H
-        const fe r2 = fe_mul(fe_sel(odd, E, F), fe_sel(odd, H, G));   // Z3 = F G / T3 = E H
-        const fe s1 = fe_pair_swap(r1), s2 = fe_pair_swap(r2);
-        r = ge{fe_sel(odd, s1, r1), fe_sel(odd, r1, s1), fe_sel(odd, s2, r2), fe_sel(odd, r2, s2)};
+    fe oa, ob, r1, r2;
+    pair_of_form(r0, oa, ob);
+    while (true) {
+        ge_pair_of_step(oa, ob, fe_sel(add_phase, qa, oa), fe_sel(add_phase, qb, ob), r1, r2);
         if (!add_phase && bit) {
             add_phase = true;
         } else {
             add_phase = false;
-            i--;
+            if (--i < 0) break;
             bit = bs_next(bs);
         }
+        const fe snd = fe_sel(odd, r2, r1);   // X3 | Y3
+        const fe got = fe_pair_swap(snd);      // Y3 | X3
+        fe sm, df;
+        fe_addsub(got, snd, sm, df);           // lane 0: Y3 - X3; lane 1: X3 + Y3
+        oa = fe_sel(odd, sm, df);
+        ob = fe_sel(odd, r1, r2);              // T3 | Z3
     }
-    return r;
+    const fe s1 = fe_pair_swap(r1), s2 = fe_pair_swap(r2);
+    return ge{fe_sel(odd, s1, r1), fe_sel(odd, r2, s2), fe_sel(odd, r1, s1), fe_sel(odd, s2, r2)};
 }
 
 }  // namespace bp

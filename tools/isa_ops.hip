@@ -41,3 +41,15 @@ extern "C" __global__ void p_quad_step_of(fe* o, const fe* p, const fe* qs, cons
     const fe x = p[threadIdx.x];
     o[threadIdx.x] = quad_of_next(ge_quad_of_step(x, fe_sel(u[threadIdx.x] != 0, qs[threadIdx.x], x)));
 }
+extern "C" __global__ void p_pair_step_of(fe* o, const fe* p, const fe* qs, const int* u) {
+    const fe oa = p[2 * threadIdx.x], ob = p[2 * threadIdx.x + 1];
+    const bool ad = u[threadIdx.x] != 0;
+    fe r1, r2;
+    ge_pair_of_step(oa, ob, fe_sel(ad, qs[2 * threadIdx.x], oa), fe_sel(ad, qs[2 * threadIdx.x + 1], ob), r1, r2);
+    const bool odd = threadIdx.x & 1;
+    const fe snd = fe_sel(odd, r2, r1), got = fe_pair_swap(snd);
+    fe sm, df;
+    fe_addsub(got, snd, sm, df);
+    o[2 * threadIdx.x] = fe_sel(odd, sm, df);
+    o[2 * threadIdx.x + 1] = fe_sel(odd, r1, r2);
+}
