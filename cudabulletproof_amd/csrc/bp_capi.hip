@@ -1544,7 +1544,12 @@ int hipbp_batch_range_proof_verify_host(const RangeProof* proofs, const ge25519*
     int ndev = 0;
     BP_RET_ON(hipGetDeviceCount(&ndev));
     if (ndev <= 0) { g_err = "no HIP device"; return HIPBP_ERR_DEVICE; }
-    const int ng = num_gpus <= 0 ? ndev : std::min(num_gpus, ndev);
+    int ng = num_gpus <= 0 ? ndev : std::min(num_gpus, ndev);
+    // HIPBP_HOST_SHARDS=k (tests): k shards, shard d on device d % ndev, so the multi-device split,
+    // its host threads and the verdict merge also run on a one-GPU box (threads of one device
+    // serialise on its engine's mutex)
+    if (const char* hs = getenv("HIPBP_HOST_SHARDS"))
+        if (atoi(hs) > 0) ng = atoi(hs);
     // The flat batch needs one (a/b length, rounds) shape: the first proof that passes the checks
     // sets it (the reference prover's proofs all share it); proofs of another shape go one by one.
     size_t abl = 0, Lr = 0;
@@ -1584,7 +1589,7 @@ int hipbp_batch_range_proof_verify_host(const RangeProof* proofs, const ge25519*
         const size_t lo = M * d / ng, hi = M * (d + 1) / ng;
         if (hi == lo) continue;
         workers.emplace_back([&, d, lo, hi]() {
-            rcs[d] = host_shard(d, proofs, V, main.data() + lo, hi - lo, abl, Lr, n, G, H, h, ok);
+            rcs[d] = host_shard(d % ndev, proofs, V, main.data() + lo, hi - lo, abl, Lr, n, G, H, h, ok);
             if (rcs[d] != HIPBP_OK) errs[d] = g_err;   // g_err is per thread
         });
     }

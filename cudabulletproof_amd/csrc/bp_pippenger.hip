@@ -510,57 +510,7 @@ __global__ __launch_bounds__(PTPB) void k_pip_window(const ge* __restrict__ V, i
 // ---- latency-bound chains: one point operation per lane QUAD (ge25519_quad.h).
 
 // ---- the Horner chain: one point operation per 16-lane row, one product per lane quad.
-// fe_mul_q4: the product's 64 word products split over the quad by rows — lane rb forms
-// (x_{2rb+1} 2^32 + x_{2rb}) * y as an exact 320-bit partial (mul2x8_asm) — and two DPP levels of
-// shifted adds sum the partials (the exact 512-bit product) on lane rb = 0, which folds it.
-// Valid on the quad's lane 0 only; the same 512 bits as mul512, so the same result bits.
-__device__ __forceinline__ uint32_t dpp_qperm_1133(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xF5, 0xF, 0xF, true);   // lane l <- l | 1
-}
-__device__ __forceinline__ uint32_t dpp_qperm_2222(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xAA, 0xF, 0xF, true);   // lane l <- quad lane 2
-}
-__device__ __forceinline__ fe fe_mul_q4(const fe& x, const fe& y) {
-    const int rb = threadIdx.x & 3;
-    const uint64_t m0 = 0ull - (uint64_t)(rb & 1), m1 = 0ull - (uint64_t)((rb >> 1) & 1);
-    const uint64_t x01 = x.v[0] ^ ((x.v[0] ^ x.v[1]) & m0), x23 = x.v[2] ^ ((x.v[2] ^ x.v[3]) & m0);
-    const uint64_t xr = x01 ^ ((x01 ^ x23) & m1);
-    const uint32_t a[2] = {(uint32_t)xr, (uint32_t)(xr >> 32)};
-    uint32_t b[8], w[10], q[12], r[16];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        b[2 * i] = (uint32_t)y.v[i];
-        b[2 * i + 1] = (uint32_t)(y.v[i] >> 32);
-    }
-    mul2x8_asm(w, a, b);
-    // lanes 0, 2: q = own partial + the next lane's partial at +2 words (12 words)
-    uint32_t n1[10];
-#pragma unroll
-    for (int i = 0; i < 10; i++) n1[i] = dpp_qperm_1133(w[i]);
-    unsigned c = 0;
-    q[0] = w[0];
-    q[1] = w[1];
-#pragma unroll
-    for (int i = 2; i < 10; i++) q[i] = __builtin_addc(w[i], n1[i - 2], c, &c);
-    q[10] = __builtin_addc(n1[8], 0u, c, &c);
-    q[11] = n1[9] + c;   // < 2^(32*12) in total: no carry out
-    // lane 0: r = q + lane 2's q at +4 words (16 words, the exact 512-bit product)
-    uint32_t n2[12];
-#pragma unroll
-    for (int i = 0; i < 12; i++) n2[i] = dpp_qperm_2222(q[i]);
-    c = 0;
-#pragma unroll
-    for (int i = 0; i < 4; i++) r[i] = q[i];
-#pragma unroll
-    for (int i = 4; i < 12; i++) r[i] = __builtin_addc(q[i], n2[i - 4], c, &c);
-#pragma unroll
-    for (int i = 12; i < 15; i++) r[i] = __builtin_addc(n2[i - 4], 0u, c, &c);
-    r[15] = n2[11] + c;
-    uint64_t t[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) t[i] = (uint64_t)r[2 * i] | ((uint64_t)r[2 * i + 1] << 32);
-    return fe_fold512(t);
-}
+// (fe_mul_q4, the product split over a lane quad: ge25519_quad.h)
 template <int SRC>   // lane SRC of each 16-lane row to the whole row
 __device__ __forceinline__ fe fe_row_bcast(const fe& a) {
     fe r;

@@ -10,6 +10,9 @@
 #pragma once
 #include "ge25519_dev.h"
 
+#ifndef BP_QUAD_SPLITC
+#define BP_QUAD_SPLITC 1
+#endif
 namespace bp {
 
 template <int SRC>
@@ -46,6 +49,57 @@ __device__ __forceinline__ fe fe_sel(bool c, const fe& a, const fe& b) {   // c 
     return r;
 }
 
+// fe_mul_q4: the product's 64 word products split over the quad by rows — lane rb forms
+// (x_{2rb+1} 2^32 + x_{2rb}) * y as an exact 320-bit partial (mul2x8_asm) — and two DPP levels of
+// shifted adds sum the partials (the exact 512-bit product) on lane rb = 0, which folds it.
+// Valid on the quad's lane 0 only; the same 512 bits as mul512, so the same result bits.
+__device__ __forceinline__ uint32_t dpp_qperm_1133(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xF5, 0xF, 0xF, true);   // lane l <- l | 1
+}
+__device__ __forceinline__ uint32_t dpp_qperm_2222(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xAA, 0xF, 0xF, true);   // lane l <- quad lane 2
+}
+__device__ __forceinline__ fe fe_mul_q4(const fe& x, const fe& y) {
+    const int rb = threadIdx.x & 3;
+    const uint64_t m0 = 0ull - (uint64_t)(rb & 1), m1 = 0ull - (uint64_t)((rb >> 1) & 1);
+    const uint64_t x01 = x.v[0] ^ ((x.v[0] ^ x.v[1]) & m0), x23 = x.v[2] ^ ((x.v[2] ^ x.v[3]) & m0);
+    const uint64_t xr = x01 ^ ((x01 ^ x23) & m1);
+    const uint32_t a[2] = {(uint32_t)xr, (uint32_t)(xr >> 32)};
+    uint32_t b[8], w[10], q[12], r[16];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        b[2 * i] = (uint32_t)y.v[i];
+        b[2 * i + 1] = (uint32_t)(y.v[i] >> 32);
+    }
+    mul2x8_asm(w, a, b);
+    // lanes 0, 2: q = own partial + the next lane's partial at +2 words (12 words)
+    uint32_t n1[10];
+#pragma unroll
+    for (int i = 0; i < 10; i++) n1[i] = dpp_qperm_1133(w[i]);
+    unsigned c = 0;
+    q[0] = w[0];
+    q[1] = w[1];
+#pragma unroll
+    for (int i = 2; i < 10; i++) q[i] = __builtin_addc(w[i], n1[i - 2], c, &c);
+    q[10] = __builtin_addc(n1[8], 0u, c, &c);
+    q[11] = n1[9] + c;   // < 2^(32*12) in total: no carry out
+    // lane 0: r = q + lane 2's q at +4 words (16 words, the exact 512-bit product)
+    uint32_t n2[12];
+#pragma unroll
+    for (int i = 0; i < 12; i++) n2[i] = dpp_qperm_2222(q[i]);
+    c = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) r[i] = q[i];
+#pragma unroll
+    for (int i = 4; i < 12; i++) r[i] = __builtin_addc(q[i], n2[i - 4], c, &c);
+#pragma unroll
+    for (int i = 12; i < 15; i++) r[i] = __builtin_addc(n2[i - 4], 0u, c, &c);
+    r[15] = n2[11] + c;
+    uint64_t t[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) t[i] = (uint64_t)r[2 * i] | ((uint64_t)r[2 * i + 1] << 32);
+    return fe_fold512(t);
+}
 // Stages 2 and 3 of ge25519_add from the quad's stage-1 products (lane qd holds product qd of
 // {A, B, T1 T2, Z1 Z2}); the result replicated over the quad.
 __device__ __forceinline__ ge ge_quad_finish(const fe& r1) {
@@ -126,7 +180,11 @@ __device__ __forceinline__ fe ge_quad_of_step(const fe& o, const fe& q) {
     const int qd = threadIdx.x & 3;
     const fe p1 = fe_mul(o, q);
     const fe A = fe_quad_bcast<0>(p1), CT = fe_quad_bcast<1>(p1), D0 = fe_quad_bcast<2>(p1), B = fe_quad_bcast<3>(p1);
+#if BP_QUAD_SPLITC   // C = (T1 T2) k split over the quad by rows (fe_mul_q4), then from lane 0 to all
+    const fe C = fe_quad_bcast<0>(fe_mul_q4(CT, k_const()));
+#else
     const fe C = fe_mul(CT, k_const());
+#endif
     const fe D = fe_add(D0, D0);
     fe E, F, G, H;
     fe_addsub(B, A, H, E);   // H = B + A, E = B - A

@@ -4,6 +4,7 @@ restatement (oracle/) on seeded inputs.  Everything is bit-exact: this is intege
 Run on the GPU box: python -m pytest tests -m gpu -q
 """
 import hashlib
+import os
 
 import numpy as np
 import pytest
@@ -262,6 +263,15 @@ def test_batch_verify_host_structs(bp, golden, n):
     for ng in (1, 0):
         got = bp.batch_range_proof_verify_host(proofs, V, n, d["G"], d["H"], d["g"], d["h"], num_gpus=ng)
         assert np.array_equal(got, want), (ng, np.nonzero(got != want)[0][:10])
+    # the multi-device path (shards cut from the index list, one host thread each, verdicts merged),
+    # here with every shard on this box's one GPU: 2 and 3 shards give the same verdicts
+    for k in ("2", "3"):
+        os.environ["HIPBP_HOST_SHARDS"] = k
+        try:
+            got = bp.batch_range_proof_verify_host(proofs, V, n, d["G"], d["H"], d["g"], d["h"])
+        finally:
+            del os.environ["HIPBP_HOST_SHARDS"]
+        assert np.array_equal(got, want), (k, np.nonzero(got != want)[0][:10])
     # the reference's length check (crv:140-143): generator vectors shorter than the proofs' n
     got = bp.batch_range_proof_verify_host(ref[:2], d["V"][:2], n, d["G"][:n // 2], d["H"][:n // 2], d["g"], d["h"])
     assert not got.any()
