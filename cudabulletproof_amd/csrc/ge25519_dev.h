@@ -12,6 +12,20 @@
 
 namespace bp {
 
+#ifndef BP_LANE_ADDSUB
+#define BP_LANE_ADDSUB 1
+#endif
+// E/H and F/G of ge25519_add: one fused block (fe_addsub, chains interleaved) or two calls
+// (-DBP_LANE_ADDSUB=0, for A/B builds); the same bits either way.
+BP_DEV void lane_addsub(const fe& f, const fe& g, fe& sum, fe& diff) {
+#if BP_LANE_ADDSUB
+    fe_addsub(f, g, sum, diff);
+#else
+    diff = fe_sub(f, g);
+    sum = fe_add(f, g);
+#endif
+}
+
 struct ge {
     fe X, Y, Z, T;
 };
@@ -39,10 +53,9 @@ BP_DEV ge ge_add_q(const ge& p, const geq& q) {
     fe C = fe_mul(fe_mul(p.T, q.T), k_const());
     fe D = fe_mul(p.Z, q.Z);
     D = fe_add(D, D);
-    fe E = fe_sub(B, A);
-    fe F = fe_sub(D, C);
-    fe G = fe_add(D, C);
-    fe H = fe_add(B, A);
+    fe E, F, G, H;
+    lane_addsub(B, A, H, E);   // H = B + A, E = B - A
+    lane_addsub(D, C, G, F);   // G = D + C, F = D - C
     return ge{fe_mul(E, F), fe_mul(G, H), fe_mul(F, G), fe_mul(E, H)};
 }
 
@@ -55,10 +68,9 @@ BP_DEV ge ge_dbl(const ge& p) {
     fe C = fe_mul(fe_sq(p.T), k_const());
     fe D = fe_sq(p.Z);
     D = fe_add(D, D);
-    fe E = fe_sub(B, A);
-    fe F = fe_sub(D, C);
-    fe G = fe_add(D, C);
-    fe H = fe_add(B, A);
+    fe E, F, G, H;
+    lane_addsub(B, A, H, E);   // H = B + A, E = B - A
+    lane_addsub(D, C, G, F);   // G = D + C, F = D - C
     return ge{fe_mul(E, F), fe_mul(G, H), fe_mul(F, G), fe_mul(E, H)};
 }
 
@@ -137,10 +149,9 @@ BP_DEV ge ge_add_qp(const ge& p, const geq* q, bool zone = false) {
     fe C = fe_mul(fe_mul(p.T, qget<QLDS>(&q->T)), k_const());
     fe D = zone ? fe_mul_one(p.Z) : fe_mul(p.Z, qget<QLDS>(&q->Z));
     D = fe_add(D, D);
-    fe E = fe_sub(B, A);
-    fe F = fe_sub(D, C);
-    fe G = fe_add(D, C);
-    fe H = fe_add(B, A);
+    fe E, F, G, H;
+    lane_addsub(B, A, H, E);   // H = B + A, E = B - A
+    lane_addsub(D, C, G, F);   // G = D + C, F = D - C
     return ge{fe_mul(E, F), fe_mul(G, H), fe_mul(F, G), fe_mul(E, H)};
 }
 
@@ -171,10 +182,9 @@ BP_DEV ge ge_add_sel(const ge& p, const geq* q, bool use_q) {
         D = fe_mul(p.Z, use_q ? qz : p.Z);
     }
     D = fe_add(D, D);
-    fe E = fe_sub(B, A);
-    fe F = fe_sub(D, C);
-    fe G = fe_add(D, C);
-    fe H = fe_add(B, A);
+    fe E, F, G, H;
+    lane_addsub(B, A, H, E);   // H = B + A, E = B - A
+    lane_addsub(D, C, G, F);   // G = D + C, F = D - C
     return ge{fe_mul(E, F), fe_mul(G, H), fe_mul(F, G), fe_mul(E, H)};
 }
 
