@@ -933,6 +933,13 @@ __global__ __launch_bounds__(TPB) void k_field_op(int op, fe* r, const fe* __res
             break;
         }
         case 7: z = fe_sq(x); break;   // fe25519_sq (dedicated squaring; == mul(x, x))
+        case 8:                         // fe_addsub's sum / difference (the drain forms' fused
+        case 9: {                       // block: its rare-edge path is tested through these)
+            fe sm, df;
+            fe_addsub(x, y, sm, df);
+            z = op == 8 ? sm : df;
+            break;
+        }
         default:
 #pragma unroll
             for (int k = 0; k < 4; k++) z.v[k] = x.v[k] + y.v[k];

@@ -284,7 +284,9 @@ int hipbp_msm_pippenger_horner(ge25519* results, const ge25519* window_sums, siz
 int hipbp_point_tree(ge25519* result, const ge25519* points, size_t n, void* stream);
 /* Elementwise device field ops: op 0 add, 1 sub, 2 mul, 3 square (reference kernel quirk),
  * 4 SoA add (limbwise, no carry), 5 invert (host chain), 6 the product fold alone on the
- * 512-bit t = a || b (fe25519_mul's reduction, curve25519_ops.cu:114-145), 7 fe25519_sq. */
+ * 512-bit t = a || b (fe25519_mul's reduction, curve25519_ops.cu:114-145), 7 fe25519_sq,
+ * 8 / 9 the sum / difference of the fused add-and-sub block the lane-quad forms use (the same
+ * values as ops 0 / 1). */
 int hipbp_field_op(int op, fe25519* r, const fe25519* a, const fe25519* b, size_t count, void* stream);
 /* Frees every workspace the library caches for `stream` on the current device (canonical MSM /
  * point-tree, prover, one-shot verify pipelines, the Pippenger workspace pair with its side stream

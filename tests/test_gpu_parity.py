@@ -722,7 +722,7 @@ def _edge_cases(op, rng):
     return out
 
 
-@pytest.mark.parametrize("op", ["add", "sub", "fold", "mul"])
+@pytest.mark.parametrize("op", ["add", "sub", "fold", "mul", "addsub_add", "addsub_sub"])
 def test_field_fast_forms_one_edge_lane_per_wave(bp, oracle, op):
     """The field asm runs a short form unless some lane of the wave sits on one of the rare edges
     (a limb or word equal to 2^64-1 / 2^32-1, t0 >= p0, t0 < 19): the exact form then runs for the
@@ -731,8 +731,10 @@ def test_field_fast_forms_one_edge_lane_per_wave(bp, oracle, op):
     random, and the last ones near-edge values only (words 2^32-2, high words all ones with low
     words not) that the short form must get right."""
     import torch
-    rng = np.random.default_rng({"add": 1, "sub": 2, "fold": 3, "mul": 4}[op])
-    cases = _edge_cases(op, rng)
+    rng = np.random.default_rng({"add": 1, "sub": 2, "fold": 3, "mul": 4, "addsub_add": 5, "addsub_sub": 6}[op])
+    # the fused add/sub block (fe_addsub_asm) takes its exact path when either op's edge fires, so
+    # it gets both ops' edge cases whichever of its outputs is checked
+    cases = _edge_cases(op, rng) if not op.startswith("addsub") else _edge_cases("add", rng) + _edge_cases("sub", rng)
     waves = len(cases) + 64
     N = 64 * waves
     a = rand_fe(rng, N, top=True)
@@ -766,7 +768,7 @@ def test_field_fast_forms_one_edge_lane_per_wave(bp, oracle, op):
         if op == "fold":
             want = _ref_fold([int(x) for x in a[i]] + [int(x) for x in b[i]])
         else:
-            want = [int(x) for x in getattr(oracle, "fe_" + op)(a[i], b[i])]
+            want = [int(x) for x in getattr(oracle, "fe_" + op.replace("addsub_", ""))(a[i], b[i])]
         assert [int(x) for x in got[i]] == want, (op, i, [hex(int(x)) for x in a[i]], [hex(int(x)) for x in b[i]])
 
 
