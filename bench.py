@@ -722,7 +722,7 @@ def shard_leg(args, dev, world, rank, pipes, gens, G, H, g, h, streams=None):
     verifies its shard through its pipelines; the pass counts meet in one all_reduce(SUM) and the
     2^16 verdict bytes in one all_gather over RCCL (every rank ends with all verdicts).  Timed
     from a barrier to the end of the collectives (pipeline fill and drain included), max over ranks,
-    after one untimed pass; the median of 3 timed passes; strong scaling: the same 2^16 proofs
+    after one untimed pass; the median of 5 timed passes; strong scaling: the same 2^16 proofs
     whatever N."""
     import torch
     import torch.distributed as dist
@@ -783,11 +783,12 @@ def shard_leg(args, dev, world, rank, pipes, gens, G, H, g, h, streams=None):
         torch.cuda.synchronize(dev)
         return time.perf_counter() - t0, passes, allv
 
-    # one untimed pass (the new pipelines' first ticks, code-object loads), then 3 timed passes:
-    # `value` is the median, max over ranks per pass; every pass must give the same verdicts
+    # one untimed pass (the new pipelines' first ticks, code-object loads), then 5 timed passes
+    # (>= 5 repetitions, median): `value` is the median, max over ranks per pass;
+    # every pass must give the same verdicts
     run_once()
     times, digests = [], set()
-    for _ in range(3):
+    for _ in range(5):
         dt, passes, allv = run_once()
         times.append(dt)
         digests.add(allv.cpu().numpy().tobytes())

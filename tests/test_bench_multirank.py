@@ -44,7 +44,7 @@ def test_bench_two_ranks_rehearsal_matches_one_rank():
     s1, s2 = l1["sharded_2p16"], l2["sharded_2p16"]
     assert s1["proofs"] == s2["proofs"] == 3000 and s2["scaling"] == "strong"
     assert s1["passes"] == s2["passes"] > 0 and s1["verdicts_sha256"] == s2["verdicts_sha256"]
-    assert s1["same_verdicts_every_pass"] and s2["same_verdicts_every_pass"] and s2["passes_timed"] == 3
+    assert s1["same_verdicts_every_pass"] and s2["same_verdicts_every_pass"] and s2["passes_timed"] == 5
     # the repeated timed regions of the headline ran on every rank (max over ranks per region)
     assert l1["repeats"]["n"] == l2["repeats"]["n"] == 5
     assert l2["config"]["passes_in_warmup_batch"] >= l1["config"]["passes_in_warmup_batch"]
