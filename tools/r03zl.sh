@@ -1,5 +1,6 @@
 #!/usr/bin/env bash
-# configs[4] 8192 shard leg: the headline's streams vs fresh streams, alternated
+# configs[4] 8192 shard leg: the headline's streams vs fresh streams, alternated (the
+# BENCH_SHARD_STREAMS toggle it used was removed after the A/B: profiles/shard/shard8k_streams_r03zl.txt)
 set -o pipefail
 mkdir -p gpurun_out
 for rep in 1 2; do for m in reuse fresh; do
