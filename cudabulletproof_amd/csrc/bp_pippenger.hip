@@ -565,13 +565,29 @@ __global__ __launch_bounds__(64) void k_pip_horner(const ge* __restrict__ Sw, in
         T = Sw[w_top];
         w--;
     }
-    for (; w >= w_end; w--) {
-        if (BP_HORNER16) {
-            for (int d = 0; d < c; d++) T = ge_op16<true>(T, T);
-            T = ge_op16<false>(T, Sw[w]);
-        } else {
-            for (int d = 0; d < c; d++) T = ge_op_quad<true>(T, T);
-            T = ge_op_quad<false>(T, Sw[w]);
+    if (BP_HORNER16 == 2) {   // lane quads in operand form (ge25519_quad.h), squares for the doublings
+        fe o = quad_of_form(T), r3;
+        bool pend = false;       // r3 holds the last operation's stage-3 products, o is stale
+        for (; w >= w_end; w--) {
+            for (int d = 0; d < c; d++) {
+                if (pend) o = quad_of_next(r3);
+                r3 = ge_quad_of_step<true>(o, o);
+                pend = true;
+            }
+            if (pend) o = quad_of_next(r3);
+            r3 = ge_quad_of_step(o, quad_of_form(Sw[w]));
+            pend = true;
+        }
+        if (pend) T = quad_of_point(r3);
+    } else {
+        for (; w >= w_end; w--) {
+            if (BP_HORNER16) {
+                for (int d = 0; d < c; d++) T = ge_op16<true>(T, T);
+                T = ge_op16<false>(T, Sw[w]);
+            } else {
+                for (int d = 0; d < c; d++) T = ge_op_quad<true>(T, T);
+                T = ge_op_quad<false>(T, Sw[w]);
+            }
         }
     }
     if (threadIdx.x == 0) *out = T;

@@ -176,9 +176,10 @@ __device__ __forceinline__ fe fe_dpp(const fe& a) {
 }
 // p: r in operand form, o = this lane's stage-1 operand; q = this lane's q-side operand (the
 // doubling passes o); returns the result's stage-3 product (X3 | T3 | Z3 | Y3 by lane)
+template <bool SQ = false>   // SQ: a doubling known to the whole wave (stage 1 as squares, q unused)
 __device__ __forceinline__ fe ge_quad_of_step(const fe& o, const fe& q) {
     const int qd = threadIdx.x & 3;
-    const fe p1 = fe_mul(o, q);
+    const fe p1 = SQ ? fe_sq(o) : fe_mul(o, q);
     const fe A = fe_quad_bcast<0>(p1), CT = fe_quad_bcast<1>(p1), D0 = fe_quad_bcast<2>(p1), B = fe_quad_bcast<3>(p1);
 #if BP_QUAD_SPLITC   // C = (T1 T2) k split over the quad by rows (fe_mul_q4), then from lane 0 to all
     const fe C = fe_quad_bcast<0>(fe_mul_q4(CT, k_const()));

@@ -53,3 +53,7 @@ extern "C" __global__ void p_pair_step_of(fe* o, const fe* p, const fe* qs, cons
     o[2 * threadIdx.x] = fe_sel(odd, sm, df);
     o[2 * threadIdx.x + 1] = fe_sel(odd, r1, r2);
 }
+extern "C" __global__ void p_quad_dbl_of(fe* o, const fe* p) {
+    const fe x = p[threadIdx.x];
+    o[threadIdx.x] = quad_of_next(ge_quad_of_step<true>(x, x));
+}
