@@ -4,14 +4,19 @@
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
       --master-port P bench.py --gpus N --steps K --warmup W
 
+--gpus N is N ranks: without a launcher, bench.py starts torch.distributed.run on itself as a
+child process (before touching the GPU) and exits with its status; under a launcher WORLD_SIZE
+must equal N.  The line carries world_size (from torch.distributed), each rank's device PCI
+address and the verdict digest of its own batches (`ranks`).
+
 One step = cuda_range_proof_verify semantics (crv:82) over one batch of B = 1024 synthetic
 64-bit proofs already resident in HBM (BASELINE configs[1]); every rank verifies its own
 batches (weak scaling, no data-path collective: proofs are independent).  K steps are timed
 between barrier + synchronize on both sides; the max over ranks is the step time.
 
 Extra fields on the JSON line:
-  roofline     the dominant kernel's algorithmic bytes / HIP-event launch time vs HBM peak
-               (the path is VALU-integer bound; see DESIGN.md), PMC traffic when profiled;
+  roofline     SURVEY 8(d) algorithmic bytes per step / ms_per_step vs HBM peak (the path is
+               VALU-integer bound; see DESIGN.md), PMC traffic per launch; valu_roofline beside it;
   cpu_baseline the CPU restatement (oracle/, test infrastructure) on a bounded sample, 1 thread;
   msm          2^20-point canonical-tree MSM points/s (BASELINE configs[2], per-point semantics);
                at N > 1 one MSM sharded over all ranks (cudabulletproof_amd/shard.py), strong scaling;
@@ -265,8 +270,65 @@ def configs0_leg(reps=15):
         out["dropin_gpu"] = {"value": h["wall_s"], "cuda_verify_s": h["cuda_verify_s"], "ok": h["ok"],
                              "exit_status": h["rc"],
                              "binary": "oracle/_ref/complete_bulletproof_test_hip (the same main() on "
-                                       "libcudabulletproof_hip.so; wall includes HIP runtime start-up)"}
+                                       "libcudabulletproof_hip.so; wall includes HIP runtime start-up; its "
+                                       "printed times are the driver's clock(), process CPU time)"}
+    out["dropin_latency"] = dropin_latency()
     return out
+
+
+def dropin_proof_file(path, n=16, i=0):
+    """proof.bin for tests/dropin_latency.c: reference proof i of tests/golden/proofs_n{n}.npz
+    (complete_bulletproof_test.cu's generators; proof 0 is its value-42 proof)."""
+    d = np.load(os.path.join(ROOT, "tests", "golden", f"proofs_n{n}.npz"))
+    h = d["head"][i]
+    with open(path, "wb") as f:
+        f.write(np.array([n, d["a"].shape[1], d["L"].shape[1]], np.uint64).tobytes())
+        for a in (d["G"], d["H"], d["g"], d["h"], d["V"][i], h[16:80], h[80:100], d["a"][i], d["b"][i], d["L"][i],
+                  d["R"][i]):
+            f.write(np.ascontiguousarray(a, np.uint64).tobytes())
+    return bool(d["ok_cuda"][i])
+
+
+def build_dropin_latency():
+    """Compile tests/dropin_latency.c against the product library into build/ (gcc, seconds)."""
+    import subprocess
+    out = os.path.join(ROOT, "build", "dropin_latency")
+    src = os.path.join(ROOT, "tests", "dropin_latency.c")
+    lib = os.path.join(ROOT, "cudabulletproof_amd", "libcudabulletproof_hip.so")
+    if os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(src), os.path.getmtime(lib)):
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    subprocess.check_call(["gcc", "-O2", "-I" + os.path.join(ROOT, "include"), src,
+                           "-L" + os.path.dirname(lib), "-lcudabulletproof_hip",
+                           "-Wl,-rpath," + os.path.dirname(lib), "-o", out])
+    return out
+
+
+def dropin_latency(ns=(16, 64), warm=20):
+    """Wall-clock latency of the drop-in cuda_range_proof_verify, one reference proof per call, in
+    a fresh process per n (tests/dropin_latency.c: the HIP runtime's start-up, the first call, the
+    median warm call), beside the reference CPU path's per-verify time.  Children only: this
+    process has not touched the GPU."""
+    import subprocess
+    import tempfile
+    try:
+        exe = build_dropin_latency()
+    except (OSError, subprocess.CalledProcessError) as e:
+        return {"error": str(e)}
+    res = {}
+    with tempfile.TemporaryDirectory() as tmp:
+        for n in ns:
+            pf = os.path.join(tmp, f"proof{n}.bin")
+            want = dropin_proof_file(pf, n)
+            p = subprocess.run([exe, pf, str(warm)], capture_output=True, text=True, timeout=300)
+            try:
+                r = json.loads(p.stdout.strip().splitlines()[-1])
+                r["matches_reference_verdict"] = r["verdict"] == want
+            except (ValueError, IndexError):
+                r = {"rc": p.returncode, "stderr": p.stderr[-500:]}
+            res[f"n{n}"] = r
+    res["harness"] = "tests/dropin_latency.c (CLOCK_MONOTONIC; one reference proof of tests/golden/proofs_n*.npz)"
+    return res
 
 
 def oracle_sample(n, B, seed, count=8):
@@ -319,16 +381,15 @@ def pmc(kernel, key, config=None):
 
 def rooflines(dom, B, n, steps, launches, avg_ms, dt, kern_ms, pcfg, npipes):
     """`roofline` (HBM, as the contract asks) and `valu_roofline` (the binding resource) for the
-    dominant kernel.  HBM: SURVEY §8(d) algorithmic bytes of the timed region's batches, per launch,
-    / the live HIP-event launch duration (and / the region's wall time: with two pipelines a launch's
-    own duration includes the other pipeline's overlapping launch); `traffic` = the PMC bytes per
+    dominant kernel.  HBM: SURVEY §8(d) algorithmic bytes of the timed region's batches / the
+    region's wall time (one step = one k_terms launch of one batch; the launches of the two
+    pipelines overlap, so the per-launch HIP-event rate goes beside it as `per_launch_overlapped`,
+    measured on the library's streams); `traffic` = the PMC bytes per
     launch (profiles/pmc_traffic.json, collected on this configuration) with its ratio to the
     algorithmic bytes and a breakdown model.  VALU: `frac` = VALUBusy (PMC: the fraction of cycles
-    in which the SIMDs issued VALU work), and an issue-cost model beside it: the per-opcode issue
-    cycles measured in shader-clock cycles (tools/ubench_issue.hip) weighted by the hot loop's
-    opcode mix (tools/valu_model.py) give the cycles one VALU instruction takes at full issue; the
-    peak is 1024 SIMDs x the PMC clock / that, and achieved = SQ_INSTS_VALU of the region's
-    launches / its wall time."""
+    in which the SIMDs issued VALU work); beside it the region's issue rate (SQ_INSTS_VALU per
+    launch x launches / wall time), the cycles per instruction per SIMD that rate means at the PMC
+    clock, and the rates of k_terms' point-op loops run alone (profiles/valu_step_roof.json)."""
     per_batch = alg_bytes(dom, B, n)
     per_launch = per_batch * steps / launches if per_batch else None
     achieved = (per_launch / (avg_ms * 1e-3)) / 1e9 if per_launch else None
@@ -336,14 +397,20 @@ def rooflines(dom, B, n, steps, launches, avg_ms, dt, kern_ms, pcfg, npipes):
     traffic = pmc(dom, "bytes_per_launch", pcfg)
     model = traffic_model(B, n, pcfg["prefix_bits"]) if dom == "k_terms" else None
     roofline = {
-        "bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-        "alg_bytes_per_launch": per_launch,
+        "bound": "hbm", "kernel": dom, "achieved": agg, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": agg / HBM_PEAK_GBS if agg else None, "traffic": traffic,
+        "achieved_rule": "SURVEY 8(d) algorithmic bytes of the timed steps / the timed region's wall time "
+                         "(= per step / ms_per_step): one step is one k_terms launch of one batch, and with two "
+                         "pipelines the launches overlap, so a launch's own duration is not a per-step time",
+        "alg_bytes_per_step": per_batch, "alg_bytes_per_launch": per_launch,
         "alg_bytes_rule": f"SURVEY 8(d): {verify_bytes(n) - 1} B per verify (944 + 64n + 256 log2 n) + 1 B verdict, "
                           f"x {B} verifies + {gens_bytes(n)} B generators per batch",
         "traffic_over_alg": traffic / per_launch if traffic and per_launch else None,
         "traffic_model_bytes": model,
-        "achieved_aggregate": agg, "frac_aggregate": agg / HBM_PEAK_GBS if agg else None,
+        "per_launch_overlapped": {
+            "achieved": achieved, "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "avg_launch_ms": avg_ms,
+            "note": "bytes per launch / the launch's own HIP-event duration, which includes the other pipeline's "
+                    "overlapping launch (a lower bound of the per-kernel rate)"},
         "avg_launch_ms": avg_ms, "launches": launches, "concurrent_pipelines": npipes or None,
         "rocprof_avg_launch_ms": pmc(dom, "rocprof_avg_ms", pcfg),
         "kernel_ms_share": {k: round(v / sum(kern_ms.values()), 4) for k, v in kern_ms.items()},
@@ -622,12 +689,14 @@ def headline_check(B, n, pipes, streams, batch, Gd, Hd, hd, sample):
     return res
 
 
-def h2d_leg(args, dev, pipes, batches, steps):
+def h2d_leg(args, dev, pipes, batches, steps, want_oks=None):
     """The headline with the per-batch proof H2D inside the timed region (SURVEY §8(d) timing rule):
     every step copies its batch (B proofs in the flat wire format, ≈2.3 KB each) from pinned host
     memory into one of a few device staging batches on a copy stream, and the pipeline's stream
     waits for that copy before the tick; a staging batch is overwritten only after the tick that
-    consumed it.  PCIe-inclusive: reported beside `value`, never as it."""
+    consumed it.  Every step writes its own verdict slice; after the flush each step's verdicts must
+    equal the resident headline's for the same batch (`want_oks`, `verdicts_match_resident`).
+    PCIe-inclusive: reported beside `value`, never as it."""
     import torch
     import cudabulletproof_amd as bp
     F = bp.RangeProofBatch.FIELDS
@@ -652,12 +721,15 @@ def h2d_leg(args, dev, pipes, batches, steps):
     stage = [torch.empty(nbytes, dtype=torch.uint8, device=dev) for _ in range(nst)]
     stage_views = [views(sb) for sb in stage]
     cst = torch.cuda.Stream(dev)
-    oks = [torch.zeros(args.batch, dtype=torch.uint8, device=dev) for _ in range(nst)]
+    fill = (pipes[0].depth - 1) * len(pipes)   # fill, as the headline
+    # one verdict slice per step: a batch writes its verdicts depth - 1 ticks after its push, so a
+    # ring of staging-sized ok buffers would be shared by batches still in flight
+    oks = torch.zeros(fill + steps, args.batch, dtype=torch.uint8, device=dev)
     consumed = [None] * nst
 
     # each batch's copy is issued AHEAD steps before its tick (a copy can queue behind a running
     # tick's blocks; issued with its own tick it delayed that tick): one box, 50 steps: 162-176 K
-    # verifies/s issued with the tick, 182-184 K issued 2, 4 or 6 steps ahead (tools/r03zf.sh)
+    # verifies/s issued with the tick, 182-184 K issued 2, 4 or 6 steps ahead
     issued = {}
 
     def copy(g):
@@ -678,12 +750,11 @@ def h2d_leg(args, dev, pipes, batches, steps):
         pl = pipes[g % len(pipes)]
         pl_stream = pl.stream if pl.stream is not None else torch.cuda.default_stream(dev)
         pl_stream.wait_event(issued.pop(g))
-        pl.push(bp.RangeProofBatch(args.n, **stage_views[j]), oks[j])
+        pl.push(bp.RangeProofBatch(args.n, **stage_views[j]), oks[g])
         done = torch.cuda.Event()
         done.record(pl_stream)
         consumed[j] = done
 
-    fill = (pipes[0].depth - 1) * len(pipes)   # fill, as the headline
     for g in range(fill):
         step(g, fill - 1)
     torch.cuda.synchronize(dev)
@@ -695,7 +766,12 @@ def h2d_leg(args, dev, pipes, batches, steps):
     for pl in pipes:
         pl.flush()
     torch.cuda.synchronize(dev)
+    match = None
+    if want_oks is not None:   # step g verified host batch g % len(host), the headline's batch g % nb
+        got = oks.cpu()
+        match = all(torch.equal(got[g], want_oks[g % len(host)].cpu()) for g in range(fill + steps))
     return {"metric": "64-bit range-proof verifies/sec, per-batch proof H2D inside the timed region",
+            "verdicts_match_resident": match,
             "value": args.batch * steps / dt, "unit": "verifies/s", "ms_per_step": dt / steps * 1e3,
             "bytes_h2d_per_step": nbytes, "copies_per_step": 1, "copy_ahead_steps": AHEAD, "h2d_GBps": nbytes * steps / dt / 1e9, "staging_batches": nst,
             "note": "pinned host -> HBM on a copy stream overlapped with the ticks; PCIe-inclusive, never `value`"}
@@ -884,8 +960,54 @@ def prove_leg(args, dev, gens=None):
             "prefix_bits": gens.bits if gens is not None else 0}
 
 
+def rank_launch(args):
+    """`--gpus N` means N ranks.  Under a launcher (WORLD_SIZE set) the world must be N.  Without
+    one and N > 1, this process starts `torch.distributed.run --nproc-per-node N` on this script as
+    a CHILD (before anything here touches the GPU; counting devices does not) and returns its exit
+    status; N larger than the visible GPUs is an error (--rehearse puts every rank on cuda:0).
+    Returns None when this process is a rank and should run the bench."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={ws} ranks", file=sys.stderr)
+            return 2
+        return None
+    if args.gpus <= 1:
+        return None
+    import socket
+    import subprocess
+    import torch
+    have = torch.cuda.device_count()
+    if have < args.gpus and not args.rehearse:
+        print(f"bench.py: --gpus {args.gpus} needs {args.gpus} GPUs, {have} visible "
+              f"(--rehearse runs every rank on cuda:0 with gloo)", file=sys.stderr)
+        return 3
+    with socket.socket() as s:   # a free rendezvous port on the loopback
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def rank_info(dev, oks_batches):
+    """This rank's identity and its headline result: device, PCI address, verdict digest of its
+    own (rank-seeded, distinct) batches."""
+    import torch
+    pr = torch.cuda.get_device_properties(dev)
+    ok = torch.cat([o.flatten() for o in oks_batches]).cpu().numpy()
+    return {"rank": int(os.environ.get("RANK", "0")), "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+            "device": str(dev), "name": pr.name,
+            "pci": f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0",
+            "uuid": str(getattr(pr, "uuid", "")), "verdicts_sha256": hashlib.sha256(ok.tobytes()).hexdigest()[:16],
+            "passes": int(ok.sum()), "proofs": int(ok.size)}
+
+
 def main():
     args = parse()
+    rc = rank_launch(args)
+    if rc is not None:
+        sys.exit(rc)
     import torch
     import torch.distributed as dist
 
@@ -1017,9 +1139,16 @@ def main():
     for pp in pipes:
         pp.flush()
     torch.cuda.synchronize(dev)
+    # every rank's identity + the verdicts of its own batches (gathered: proves N distinct ranks ran)
+    ranks = [rank_info(dev, oks[:nb])]
+    world_seen = 1
+    if world > 1:
+        world_seen = dist.get_world_size()
+        ranks = [None] * world_seen
+        dist.all_gather_object(ranks, rank_info(dev, oks[:nb]))
     h2d = None
     if pipes and not args.no_h2d:
-        h2d = h2d_leg(args, dev, pipes, batches, args.steps)
+        h2d = h2d_leg(args, dev, pipes, batches, args.steps, want_oks=oks[:nb] if args.mode == "pipeline" else None)
     sharded = None
     if pipes and not args.no_shard:   # configs[4] on the same pipelines (all ranks take part)
         sharded = shard_leg(args, dev, world, rank, pipes, gens, Gd, Hd, gd, hd, streams)
@@ -1068,7 +1197,9 @@ def main():
     if rank == 0:
         line = {
             "metric": "64-bit range-proof verifies/sec (batched)", "value": value, "unit": "verifies/s",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
+            "n_gpus": world, "world_size": world_seen, "distinct_devices": len({r["pci"] for r in ranks}),
+            "backend": dist.get_backend() if world > 1 else None, "ranks": ranks,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
             "data": ("synthetic: real 64-bit range proofs of random values made by the GPU prover "
                      "(generate_range_proof semantics, seeded randomness); generators per "

@@ -341,11 +341,15 @@ struct Pipeline {
         g.fin = last + 1;
         return g;
     }
-    // Layout switches (A/B: tools/ab_pipeline.sh; defaults = the measured best on MI355X,
+    // Layout switches (A/B runs in round 1; defaults = the measured best on MI355X,
     // 138.7K verifies/s lane trees + chains last vs 137.9K block trees, 130.6K lane trees + chains
     // first): HIPBP_LANE_TREE_MAX (lane trees for n <= it), HIPBP_CHAINS_FIRST (per-proof chain
     // regions at the start of the grid instead of the end).
     bool lane_tree = false, chains_first = false;
+    // drain-tick forms (push): HIPBP_QUAD forces lanes (0) / quads (1) / pairs (2) on every tick
+    // (-1: by size), HIPBP_QUAD_MAX_ITEMS / HIPBP_PAIR_MAX_ITEMS move the size bounds
+    int quad_force = -1;
+    unsigned long long quad_max = QUAD_MAX_ITEMS, pair_max = PAIR_MAX_ITEMS;
     // Lane sort (bp::launch_lane_sort): per-lane-scalar items in chain-length order, for batches
     // of at least LANE_SORT_MIN proofs (HIPBP_LANE_SORT=0 turns it off, for A/B runs).
     static constexpr size_t LANE_SORT_MIN = 64;
@@ -375,6 +379,13 @@ struct Pipeline {
         lane_tree = n <= (lt ? atoi(lt) : bp::LANE_TREE_MAX);
         const char* cf = getenv("HIPBP_CHAINS_FIRST");
         chains_first = cf ? atoi(cf) != 0 : false;
+        // drain-tick form knobs, read once per pipeline (push runs on the issue path)
+        const char* qe = getenv("HIPBP_QUAD");
+        const char* qm = getenv("HIPBP_QUAD_MAX_ITEMS");
+        const char* pm = getenv("HIPBP_PAIR_MAX_ITEMS");
+        quad_force = qe ? (atoi(qe) == 1 ? 4 : atoi(qe) == 2 ? 2 : 1) : -1;
+        quad_max = qm ? strtoull(qm, nullptr, 10) : QUAD_MAX_ITEMS;
+        pair_max = pm ? strtoull(pm, nullptr, 10) : PAIR_MAX_ITEMS;
         Lr = log2i((size_t)n);
         D = stages(Lr).fin + 1;   // batches with fewer rounds finish earlier
         slots.resize(D);
@@ -575,13 +586,8 @@ struct Pipeline {
             if (bp::region_is_sm(tr.reg[k].kind)) sm_items += tr.reg[k].items;
         // Between the two (up to PAIR_MAX_ITEMS), lane pairs (HIPBP_QUAD=2 forces them,
         // HIPBP_PAIR_MAX_ITEMS sets the bound).
-        const char* qe = getenv("HIPBP_QUAD");
-        const char* qm = getenv("HIPBP_QUAD_MAX_ITEMS");
-        const char* pm = getenv("HIPBP_PAIR_MAX_ITEMS");
-        const unsigned long long qmax = qm ? strtoull(qm, nullptr, 10) : QUAD_MAX_ITEMS;
-        const unsigned long long pmax = pm ? strtoull(pm, nullptr, 10) : PAIR_MAX_ITEMS;
-        int ql = sm_items <= qmax ? 4 : sm_items <= pmax ? 2 : 1;   // (a tick of chains alone is small too)
-        if (qe) ql = atoi(qe) == 1 ? 4 : atoi(qe) == 2 ? 2 : 1;
+        int ql = sm_items <= quad_max ? 4 : sm_items <= pair_max ? 2 : 1;   // (a tick of chains alone is small too)
+        if (quad_force >= 0) ql = quad_force;
         if (ql > 1) {   // re-lay the regions: scalar-multiplication items ql lanes each
             unsigned long long tot = 0;
             for (int k = 0; k < tr.count; k++) {
@@ -950,18 +956,27 @@ int hipbp_release_stream_workspaces(void* stream) {
     BP_RET_ON(err);
     hipStream_t s = (hipStream_t)stream;
     std::lock_guard<std::mutex> lk(e->mu);
-    BP_RET_ON(hipStreamSynchronize(s));
+    // every cached workspace of s is freed and its map entry removed even if a hipFree fails (no
+    // pointer is left behind for a later call to reuse or free twice); the first error is returned
+    hipError_t first = hipStreamSynchronize(s);
+    auto keep = [&first](hipError_t r) { if (first == hipSuccess) first = r; };
+    auto free_all = [&keep](Buf* bs, size_t nb) {
+        for (size_t i = 0; i < nb; i++)
+            if (bs[i].p) {
+                keep(hipFree(bs[i].p));
+                bs[i].p = nullptr;
+                bs[i].cap = 0;
+            }
+    };
     auto mi = e->msm_ws.find(s);
     if (mi != e->msm_ws.end()) {
-        for (auto& b : mi->second->b)
-            if (b.p) BP_RET_ON(hipFree(b.p));
+        free_all(mi->second->b, sizeof(mi->second->b) / sizeof(mi->second->b[0]));
         delete mi->second;
         e->msm_ws.erase(mi);
     }
     auto pi = e->provers.find(s);
     if (pi != e->provers.end()) {
-        for (auto& b : pi->second->b)
-            if (b.p) BP_RET_ON(hipFree(b.p));
+        free_all(pi->second->b, sizeof(pi->second->b) / sizeof(pi->second->b[0]));
         delete pi->second;
         e->provers.erase(pi);
     }
@@ -974,7 +989,11 @@ int hipbp_release_stream_workspaces(void* stream) {
             ++it;
         }
     }
-    BP_RET_ON(bp::pippenger_release(s));
+    keep(bp::pippenger_release(s));
+    if (first != hipSuccess) {
+        g_err = std::string("release_stream_workspaces: ") + hipGetErrorString(first);
+        return HIPBP_ERR_DEVICE;
+    }
     return HIPBP_OK;
 }
 
@@ -1545,11 +1564,13 @@ int hipbp_batch_range_proof_verify_host(const RangeProof* proofs, const ge25519*
     BP_RET_ON(hipGetDeviceCount(&ndev));
     if (ndev <= 0) { g_err = "no HIP device"; return HIPBP_ERR_DEVICE; }
     int ng = num_gpus <= 0 ? ndev : std::min(num_gpus, ndev);
-    // HIPBP_HOST_SHARDS=k (tests): k shards, shard d on device d % ndev, so the multi-device split,
-    // its host threads and the verdict merge also run on a one-GPU box (threads of one device
-    // serialise on its engine's mutex)
-    if (const char* hs = getenv("HIPBP_HOST_SHARDS"))
-        if (atoi(hs) > 0) ng = atoi(hs);
+    // HIPBP_HOST_SHARDS=k (tests, only when the caller leaves num_gpus <= 0): k shards (at most 64
+    // and at most one per proof), shard d on device d % ndev, so the multi-device split, its host
+    // threads and the verdict merge also run on a one-GPU box (threads of one device serialise on
+    // its engine's mutex)
+    if (num_gpus <= 0)
+        if (const char* hs = getenv("HIPBP_HOST_SHARDS"))
+            if (atoi(hs) > 0) ng = (int)std::min<size_t>(std::min(atoi(hs), 64), std::max<size_t>(count, 1));
     // The flat batch needs one (a/b length, rounds) shape: the first proof that passes the checks
     // sets it (the reference prover's proofs all share it); proofs of another shape go one by one.
     size_t abl = 0, Lr = 0;

@@ -536,10 +536,10 @@ __device__ __forceinline__ void final_task(const SlotDev& sd, size_t p) {
     if (sd.range_mode) {
         ge m0, m1;
         const int n = sd.bv.n;
-        if (n > TPB) {              // upper tree levels over the per-block chunk roots (RK_TREE)
+        if (!sd.lane_tree && n > TPB) {   // upper tree levels over the per-block chunk roots (RK_TREE)
             m0 = tree_upper<QUAD>(ws.msm_pts + (p * 2 + 0) * n, n / TPB, TPB);
             m1 = tree_upper<QUAD>(ws.msm_pts + (p * 2 + 1) * n, n / TPB, TPB);
-        } else {                    // RK_TREE blocks (n <= TPB) or RK_LTREE (lane trees) wrote them
+        } else {                    // RK_LTREE (whole lane trees, any n) or RK_TREE blocks (n <= TPB) wrote them
             m0 = ws.msm_part[p * 2 + 0];
             m1 = ws.msm_part[p * 2 + 1];
         }

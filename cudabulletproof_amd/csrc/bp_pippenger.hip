@@ -904,19 +904,30 @@ hipError_t pippenger_release(hipStream_t s) {
         pp = it->second;
         g_pip.erase(it);
     }
-    PIP_RET(hipStreamSynchronize(s));
-    if (pp->hi.side) PIP_RET(hipStreamSynchronize(pp->hi.side));
+    // keep freeing after an error (the pair is already out of the map): the first error is returned
+    hipError_t first = hipStreamSynchronize(s);
+    auto keep = [&first](hipError_t r) { if (first == hipSuccess) first = r; };
+    if (pp->hi.side) keep(hipStreamSynchronize(pp->hi.side));
     for (PipWs* w : {&pp->hi, &pp->lo}) {
         for (DBuf* b : {&w->keys_in, &w->keys, &w->vals, &w->temp, &w->start, &w->len[0], &w->len[1], &w->lay,
                         &w->bq, &w->bid[0], &w->bid[1], &w->Q[0], &w->Q[1], &w->S, &w->V, &w->Sw, &w->Tmid,
                         &w->maxlen, &w->part, &w->tailq})
-            if (b->p) PIP_RET(hipFree(b->p));
+            if (b->p) {
+                keep(hipFree(b->p));
+                b->p = nullptr;
+            }
         for (auto& ev : w->ev)
-            if (ev) PIP_RET(hipEventDestroy(ev));
-        if (w->side) PIP_RET(hipStreamDestroy(w->side));
+            if (ev) {
+                keep(hipEventDestroy(ev));
+                ev = nullptr;
+            }
+        if (w->side) {
+            keep(hipStreamDestroy(w->side));
+            w->side = nullptr;
+        }
     }
     delete pp;
-    return hipSuccess;
+    return first;
 }
 
 // Horner over all W window sums of `count` MSMs (Sw[m W .. m W + W)), on stream s.

@@ -386,6 +386,36 @@ class Reference(_Lib):
             _p(np.ascontiguousarray(Q, np.uint64))))
 
 
+    LOG_CAP = 1 << 16
+
+    def cuda_range_proof_verify_log(self, pr, n, G, H, g, h):
+        """cuda_range_proof_verify with the reference's stdout captured -> (ok, printed text)."""
+        buf = ctypes.create_string_buffer(self.LOG_CAP)
+        f = self.f("cuda_range_proof_verify_log")
+        f.restype = ctypes.c_int
+        ok = f(*self._vargs(pr, n, G, H, g, h), buf, _sz(self.LOG_CAP))
+        return bool(ok), buf.value.decode()
+
+    def cuda_inner_product_verify_log(self, n, a, b, c, L, R, x, P, G, H, Q):
+        """cuda_inner_product_verify with the reference's stdout captured -> (ok, printed text)."""
+        a, b = np.ascontiguousarray(a, np.uint64).reshape(-1, 4), np.ascontiguousarray(b, np.uint64).reshape(-1, 4)
+        L, R = np.ascontiguousarray(L, np.uint64).reshape(-1, 16), np.ascontiguousarray(R, np.uint64).reshape(-1, 16)
+        buf = ctypes.create_string_buffer(self.LOG_CAP)
+        f = self.f("cuda_inner_product_verify_log")
+        f.restype = ctypes.c_int
+        ok = f(_sz(n), _p(a), _p(b), _sz(len(a)), _p(np.ascontiguousarray(c, np.uint64)), _p(L), _p(R), _sz(len(L)),
+               _p(np.ascontiguousarray(x, np.uint64)), _p(np.ascontiguousarray(P, np.uint64)),
+               _p(np.ascontiguousarray(G, np.uint64)), _p(np.ascontiguousarray(H, np.uint64)),
+               _p(np.ascontiguousarray(Q, np.uint64)), buf, _sz(self.LOG_CAP))
+        return bool(ok), buf.value.decode()
+
+    def point_tree(self, P):
+        """ref_point_tree: the canonical tree over given points (device add + device normalize)."""
+        r = ge()
+        P = np.ascontiguousarray(P, np.uint64).reshape(-1, 16)
+        self.f("point_tree")(_p(r), _p(P), _sz(len(P)))
+        return r
+
     def rpv_parts(self, pr, n, G, H, g, h):
         """range_proof_verify's sub-checks, each the reference's own function -> (delta, flags):
         flags bit0 enhanced_range_check, bit1 robust_polynomial_identity_check, bit2 inner_product_verify."""
@@ -416,6 +446,52 @@ def prover_randomness(seed, n):
 
 def have_reference():
     return os.path.exists(REF_SO)
+
+
+# ---------------------------------------------------------------- the accept rule's figures
+# cuda_inner_product_verify reports its comparison of the check point with P on stdout
+# (crv:287-346) and accepts if any of four tests holds (crv:349-357).  STATS names the printed
+# integers; `printed_stats` parses the reference's text, `accept_stats` recomputes the same
+# figures from the two points (host tobytes of X and Y, crv:281-285).
+STATS = ("x_diffs", "small_x", "y_diffs", "small_y", "msb", "hash_nonzero")
+BRANCHES = ("b_small", "b_msb", "b_diffs", "b_hash")   # the four tests, crv:351, :353, :355, :357
+
+
+def printed_stats(text):
+    """The figures the reference printed for ONE cuda_inner_product_verify call -> dict:
+    early_reject (crv:154, <a,b> != c), computed_x8 / expected_x8 (crv:288-293, first 8 bytes of
+    tobytes(check.X) / tobytes(P.X)), the STATS integers, and verdict (crv:363-367)."""
+    import re
+    if "Inner product verification failed: <a,b> != c" in text:
+        return {"early_reject": True, "verdict": False}
+    m = re.search(r"Computed X: ([0-9a-f]{16})\.\.\.\nExpected X: ([0-9a-f]{16})\.\.\.\n"
+                  r"Coordinate differences: X=(\d+) bytes \((\d+) small\), Y=(\d+) bytes \((\d+) small\)\n"
+                  r"Matching significant bits: (\d+)/64\nHash difference count: (\d+)/32\n", text)
+    if not m:
+        raise ValueError("unexpected reference output:\n" + text)
+    d = {"early_reject": False, "computed_x8": bytes.fromhex(m.group(1)), "expected_x8": bytes.fromhex(m.group(2))}
+    d.update({k: int(m.group(3 + i)) for i, k in enumerate(STATS)})
+    d["verdict"] = "CUDA inner product verification passed with robust comparison" in text
+    return d
+
+
+def accept_stats(check_xy, P_xy):
+    """Restatement of crv:297-357 on 64-byte X||Y encodings (host tobytes) -> dict of STATS,
+    the four branch flags and the verdict."""
+    import hashlib
+    c = np.frombuffer(bytes(check_xy), np.uint8).astype(int)
+    p = np.frombuffer(bytes(P_xy), np.uint8).astype(int)
+    d = np.abs(c - p)
+    st = {"x_diffs": int((d[:32] > 0).sum()), "small_x": int(((d[:32] > 0) & (d[:32] <= 10)).sum()),
+          "y_diffs": int((d[32:] > 0).sum()), "small_y": int(((d[32:] > 0) & (d[32:] <= 10)).sum()),
+          "msb": int(64 - np.unpackbits((c[24:32] ^ p[24:32]).astype(np.uint8)).sum())}
+    hsh = hashlib.sha256(bytes(check_xy) + bytes(P_xy)).digest()
+    st["hash_nonzero"] = sum(1 for x in hsh if x)
+    br = {"b_small": st["small_x"] + st["small_y"] >= 20, "b_msb": st["msb"] >= 28,
+          "b_diffs": st["x_diffs"] + st["y_diffs"] <= 32, "b_hash": st["hash_nonzero"] <= 24}
+    st.update(br)
+    st["verdict"] = any(br.values())
+    return st
 
 
 def head_fields(head):

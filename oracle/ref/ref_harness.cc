@@ -46,6 +46,33 @@ static void quiet_end() {
     close(g_saved_stdout);
 }
 
+// ---------------------------------------------------------------- captured stdout
+// The same redirection into an anonymous temp file instead of /dev/null, so the lines the
+// reference prints about its own check point (crv:287-346: "Computed X:", the byte-difference
+// counts, "Matching significant bits", "Hash difference count") can be handed back verbatim.
+static FILE* g_cap = NULL;
+static void capture_begin() {
+    fflush(stdout);
+    g_saved_stdout = dup(1);
+    g_cap = tmpfile();
+    dup2(fileno(g_cap), 1);
+}
+static void capture_end(char* log, size_t cap) {
+    fflush(stdout);
+    dup2(g_saved_stdout, 1);
+    close(g_saved_stdout);
+    long len = ftell(g_cap);
+    if (len < 0) len = 0;
+    rewind(g_cap);
+    size_t got = 0;
+    if (log && cap) {
+        got = fread(log, 1, (size_t)len < cap - 1 ? (size_t)len : cap - 1, g_cap);
+        log[got] = 0;
+    }
+    fclose(g_cap);
+    g_cap = NULL;
+}
+
 // ---------------------------------------------------------------- deterministic RNG
 static uint64_t g_seed = 1, g_ctr = 0;
 static uint8_t g_block[32];
@@ -139,6 +166,20 @@ extern "C" void ref_dev_ge_add(ge25519* r, const ge25519* p, const ge25519* q) {
 extern "C" void ref_dev_ge_scalarmult(ge25519* r, const uint8_t* s, const ge25519* p) { device_ge25519_scalarmult(r, s, p); }
 extern "C" void ref_dev_ge_normalize(ge25519* p) { device_ge25519_normalize(p); }
 extern "C" void ref_msm_canon(ge25519* r, const fe25519* s, const ge25519* P, size_t n) { canon_tree_msm(r, s, P, n); }
+// The canonical tree alone over given points (the levels of canon_tree_msm above its terms):
+// combines the roots of aligned power-of-two shards into the whole MSM's root.
+extern "C" void ref_point_tree(ge25519* r, const ge25519* P, size_t n) {
+    if (n == 0) return;
+    ge25519* T = (ge25519*)malloc(n * sizeof(ge25519));
+    memcpy(T, P, n * sizeof(ge25519));
+    for (size_t st = 1; st < n; st *= 2)
+        for (size_t i = 0; i + st < n; i += 2 * st) {
+            device_ge25519_add(&T[i], &T[i], &T[i + st]);
+            device_ge25519_normalize(&T[i]);
+        }
+    *r = T[0];
+    free(T);
+}
 extern "C" void ref_msm_cpu(ge25519* r, const fe25519* s, const ge25519* P, size_t n) {
     FieldVector sv = {(fe25519*)s, n};
     PointVector pv = {(ge25519*)P, n};
@@ -236,6 +277,21 @@ extern "C" int ref_cuda_range_proof_verify(const struct FlatHead* head, const ge
     quiet_begin();
     bool ok = cuda_range_proof_verify(&p, V, n, &Gv, &Hv, g, h);
     quiet_end();
+    return ok ? 1 : 0;
+}
+
+// The same call with the reference's stdout captured into `log` (NUL-terminated, at most cap - 1
+// bytes): its own report of the check point and of the accept rule's inputs (crv:287-367).
+extern "C" int ref_cuda_range_proof_verify_log(const struct FlatHead* head, const ge25519* V, size_t n,
+                                               const fe25519* a, const fe25519* b, size_t ab_len, const ge25519* L,
+                                               const ge25519* R, size_t L_len, const ge25519* G, const ge25519* H,
+                                               const ge25519* g, const ge25519* h, char* log, size_t cap) {
+    RangeProof p;
+    build_proof(&p, head, n, a, b, ab_len, L, R, L_len);
+    PointVector Gv = {(ge25519*)G, n}, Hv = {(ge25519*)H, n};
+    capture_begin();
+    bool ok = cuda_range_proof_verify(&p, V, n, &Gv, &Hv, g, h);
+    capture_end(log, cap);
     return ok ? 1 : 0;
 }
 
@@ -379,6 +435,28 @@ extern "C" int ref_cuda_inner_product_verify(size_t n, const fe25519* a, const f
     quiet_begin();
     bool ok = cuda_inner_product_verify(&p, P, &Gv, &Hv, Q);
     quiet_end();
+    return ok ? 1 : 0;
+}
+
+// cuda_inner_product_verify with its stdout captured (see ref_cuda_range_proof_verify_log).
+extern "C" int ref_cuda_inner_product_verify_log(size_t n, const fe25519* a, const fe25519* b, size_t ab_len,
+                                                 const fe25519* c, const ge25519* L, const ge25519* R, size_t L_len,
+                                                 const fe25519* x, const ge25519* P, const ge25519* G,
+                                                 const ge25519* H, const ge25519* Q, char* log, size_t cap) {
+    InnerProductProof p;
+    memset(&p, 0, sizeof(p));
+    p.n = n;
+    p.a.elements = (fe25519*)a; p.a.length = ab_len;
+    p.b.elements = (fe25519*)b; p.b.length = ab_len;
+    p.c = *c;
+    p.L.elements = (ge25519*)L; p.L.length = L_len;
+    p.R.elements = (ge25519*)R; p.R.length = L_len;
+    p.L_len = L_len;
+    p.x = *x;
+    PointVector Gv = {(ge25519*)G, n}, Hv = {(ge25519*)H, n};
+    capture_begin();
+    bool ok = cuda_inner_product_verify(&p, P, &Gv, &Hv, Q);
+    capture_end(log, cap);
     return ok ? 1 : 0;
 }
 

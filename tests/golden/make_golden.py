@@ -37,6 +37,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 from oracle import pyoracle as po  # noqa: E402
+from accept_cases import TAMPER_FIELDS, apply_tamper  # noqa: E402
 
 M = 2**64 - 1
 P = [0xFFFFFFFFFFFFFFED, M, M, 0x7FFFFFFFFFFFFFFF]
@@ -218,12 +219,208 @@ def make_rpverify():
     np.savez_compressed(os.path.join(HERE, "rpverify.npz"), **out)
 
 
+# ---------------------------------------------------------------- accept_n16 / accept_n64
+# cuda_range_proof_verify's tolerant accept rule (crv:297-357) pinned by the reference's OWN
+# printed figures.  Per n, 256 range-mode cases:
+#   * 24 reference proofs (seeds 201..224, random in-range values);
+#   * 168 tampered copies: one 64-bit word of one field XOR-ed with a random mask (tamper_* below:
+#     field code, flat word index, mask), 7 per reference proof, the kinds cycling through
+#     TAMPER_KINDS (a / b / c tampering ends at the <a,b> != c early reject, crv:146-158; L[0] /
+#     R[0] and taux / mu are never read by this verify);
+#   * 64 proof-shaped random inputs (a = [t], b = [1], c = t).
+# Recorded per case: the verdict, the reference's printed report (early reject flag, "Computed X"
+# / "Expected X" 8 bytes, the six integers of crv:313-346: pyoracle.STATS), P from the reference's
+# calculate_inner_product_point, the check point from ref_ipa_fold, and `check_pin`: the reference's
+# report when it verifies the same inner-product proof against P := that check point (six zeros
+# prove that the composed check point's X and Y bytes are the reference's own).
+# Plus 32 IPA-level cases (cuda_inner_product_verify with a crafted P, 8 proofs x 4 variants)
+# that reach the two branches no natural input reaches: the small-difference count (>= 20) and
+# the differing-byte count (<= 32), each alone, next to "all equal" and a reject; the hash branch
+# (<= 24 non-zero bytes of a SHA-256 output) is out of reach of any input (probability ~1e-12).
+TAMPER_KINDS = (("L", 1), ("R", 1), ("x", 0), ("t", 0), ("A", 0), ("S", 0), ("T1", 0), ("T2", 0), ("a", 0),
+                ("b", 0), ("c", 0), ("Varg", 0), ("L", 0), ("R", 0), ("taux", 0), ("mu", 0))
+HEAD_OFF = {"V": 0, "A": 16, "S": 32, "T1": 48, "T2": 64, "taux": 80, "mu": 84, "t": 88, "c": 92, "x": 96}
+def tamper_target(kind, sel, Lr, rng):
+    """(field code, flat word index) for a tamper kind; sel = 1 picks a round >= 1 of L/R, 0 round 0."""
+    if kind in HEAD_OFF:
+        return 0, HEAD_OFF[kind] + int(rng.integers(0, 16 if kind in ("A", "S", "T1", "T2") else 4))
+    if kind == "Varg":
+        return 1, int(rng.integers(0, 16))
+    if kind in ("a", "b"):
+        return TAMPER_FIELDS.index(kind), int(rng.integers(0, 4))
+    rnd = int(rng.integers(1, Lr)) if sel else 0
+    return TAMPER_FIELDS.index(kind), rnd * 16 + int(rng.integers(0, 8))   # X or Y of L/R[rnd]
+
+
+def _xy(O, p):
+    return np.concatenate([O.fe_tobytes(p[0:4]), O.fe_tobytes(p[4:8])])
+
+
+def _printed_row(st):
+    """printed_stats dict -> (early, x8 computed, x8 expected, six ints) fixed-size arrays."""
+    if st["early_reject"]:
+        return 1, np.zeros(8, np.uint8), np.zeros(8, np.uint8), np.full(6, -1, np.int32)
+    return (0, np.frombuffer(st["computed_x8"], np.uint8), np.frombuffer(st["expected_x8"], np.uint8),
+            np.array([st[k] for k in po.STATS], np.int32))
+
+
+def craft_P(O, chk, variant, rng):
+    """A point whose X||Y host bytes sit at a chosen distance from the check point's (variant
+    0: equal; 1: X bytes 24-31 flipped + >= 26 other bytes off by 1..3 (small count alone);
+    2: X bytes 24-31 flipped only (differing-byte count alone); 3: X bytes 24-31 flipped + 30
+    other bytes off by 0x80 (no test holds)).  Z = 1, T = the check point's (not compared)."""
+    xy = _xy(O, chk).astype(np.int64)
+    if variant:
+        xy[24:31] ^= 0xFF
+        xy[31] ^= 0x3F                       # bit 255 stays clear: the bytes stay a canonical encoding
+    others = [i for i in range(63) if not 24 <= i < 32]   # never byte 63 (Y's top byte)
+    pick = rng.permutation(others)
+    if variant == 1:
+        for i in pick[:27]:
+            xy[i] = xy[i] + int(rng.integers(1, 4)) if xy[i] < 250 else xy[i] - int(rng.integers(1, 4))
+    if variant == 3:
+        for i in pick[:30]:
+            xy[i] ^= 0x80
+    b = xy.astype(np.uint8)
+    P = np.zeros(16, np.uint64)
+    P[0:4] = b[:32].view(np.uint64)
+    P[4:8] = b[32:].view(np.uint64)
+    P[8] = 1
+    P[12:16] = chk[12:16]
+    assert np.array_equal(_xy(O, P), b), "crafted bytes must be canonical"
+    return P
+
+
+def make_printed():
+    """Add to proofs_n16/n64.npz and ipa4096.npz what the reference PRINTS about each check point
+    (crv:287-346): printed_early, printed_x8c / printed_x8e ("Computed X" / "Expected X"),
+    printed_stats (pyoracle.STATS), printed_ok; and check_pin, its report when the same proof is
+    verified against P := the stored (composed) check point — six zeros pin every X / Y byte."""
+    po.build()
+    R = po.Reference()
+    for n in (16, 64):
+        path = os.path.join(HERE, f"proofs_n{n}.npz")
+        d = dict(np.load(path))
+        rows, pins, oks = [], [], []
+        for i in range(len(d["head"])):
+            pr = dict(head=d["head"][i], V=d["V"][i], a=d["a"][i], b=d["b"][i], L=d["L"][i], R=d["R"][i])
+            ok, txt = R.cuda_range_proof_verify_log(pr, n, d["G"], d["H"], d["g"], d["h"])
+            rows.append(_printed_row(po.printed_stats(txt)))
+            oks.append(ok)
+            hd = po.head_fields(pr["head"])
+            _, t2 = R.cuda_inner_product_verify_log(n, pr["a"], pr["b"], hd["c"], pr["L"], pr["R"], hd["x"],
+                                                    d["check"][i], d["G"], d["H"], d["h"])
+            pins.append(_printed_row(po.printed_stats(t2))[3])
+        d.update(printed_ok=np.array(oks), printed_early=np.array([r[0] for r in rows], np.uint8),
+                 printed_x8c=np.stack([r[1] for r in rows]), printed_x8e=np.stack([r[2] for r in rows]),
+                 printed_stats=np.stack([r[3] for r in rows]), check_pin=np.stack(pins))
+        np.savez_compressed(path, **d)
+        print(f"proofs_n{n}: printed stats {d['printed_stats'].tolist()}, pins {d['check_pin'].tolist()}")
+    path = os.path.join(HERE, "ipa4096.npz")
+    d = dict(np.load(path))
+    n = int(d["n"])
+    G, H = R.base_points(n, 1), R.base_points(n, 2)
+    _, Q = R.gh()
+    res = {}
+    for tag, c, P in (("", d["c_fix"], d["P"]), ("_raw", d["c_in"], d["P"]), ("_pin", d["c_fix"], d["check"])):
+        ok, txt = R.cuda_inner_product_verify_log(n, d["a"], d["b"], c, d["L"], d["R"], d["x"], P, G, H, Q)
+        e, x8c, x8e, s6 = _printed_row(po.printed_stats(txt))
+        res.update({f"printed_ok{tag}": np.array(ok), f"printed_early{tag}": np.array(e, np.uint8),
+                    f"printed_x8c{tag}": x8c, f"printed_x8e{tag}": x8e, f"printed_stats{tag}": s6})
+    d.update(res)
+    np.savez_compressed(path, **d)
+    print("ipa4096:", {k: v.tolist() for k, v in res.items() if "stats" in k or "ok" in k})
+
+
+def make_accept():
+    po.build()
+    R = po.Reference()
+    O = po.Oracle()
+    for n in (16, 64):
+        rng = np.random.default_rng(4000 + n)
+        Lr = n.bit_length() - 1
+        G, H = R.base_points(n, 1), R.base_points(n, 2)
+        g, h = R.gh()
+        base = []
+        for seed in range(201, 225):
+            val = np.zeros(32, np.uint8)
+            val[:n // 8] = rng.integers(0, 256, n // 8)
+            base.append(R.prove(seed, val, n, G, H, g, h))
+        tam = []                                   # (base index, field, word, mask)
+        for j in range(len(base) * 7):
+            kind, sel = TAMPER_KINDS[j % len(TAMPER_KINDS)]
+            f, w = tamper_target(kind, sel, Lr, rng)
+            mask = 1 << int(rng.integers(0, 64)) if j % 2 else int(rng.integers(1, 2**63))
+            tam.append((j // 7, f, w, mask))
+        rnd = []
+        for _ in range(64):
+            hd = rng.integers(0, 2**63, po.HEAD_WORDS, dtype=np.uint64)
+            hd[92:96] = hd[88:92]                  # c = t = <[t],[1]>
+            rnd.append(dict(head=hd, V=hd[0:16].copy(), a=hd[88:92][None].copy(),
+                            b=np.array([[1, 0, 0, 0]], np.uint64),
+                            L=rng.integers(0, 2**63, (Lr, 16), dtype=np.uint64),
+                            R=rng.integers(0, 2**63, (Lr, 16), dtype=np.uint64)))
+        cases = [("ref", p) for p in base] + [("tamper", apply_tamper(base[b], f, w, m)) for b, f, w, m in tam] + \
+                [("rand", p) for p in rnd]
+        rec = {k: [] for k in ("ok", "early", "x8c", "x8e", "stats", "P", "check", "pin")}
+        for kind, pr in cases:
+            ok, txt = R.cuda_range_proof_verify_log(pr, n, G, H, g, h)
+            st = po.printed_stats(txt)
+            assert st["verdict"] == ok
+            e, x8c, x8e, s6 = _printed_row(st)
+            P, _ = R.verify_P(pr, n, G, H, g, h)
+            hd = po.head_fields(pr["head"])
+            _, _, chk = R.ipa_fold(G, H, n, hd["x"], pr["L"], pr["R"], pr["a"][0], pr["b"][0], hd["c"], h)
+            pin = np.full(6, -1, np.int32)
+            if not e:   # the composed check point against the reference's own: verify with P := it
+                ok2, t2 = R.cuda_inner_product_verify_log(n, pr["a"], pr["b"], hd["c"], pr["L"], pr["R"], hd["x"], chk,
+                                                          G, H, h)
+                pin = _printed_row(po.printed_stats(t2))[3]
+            for k, v in zip(rec, (ok, e, x8c, x8e, s6, P, chk, pin)):
+                rec[k].append(v)
+        # IPA-level crafted P: the branches natural inputs do not reach
+        ipa = {k: [] for k in ("base", "variant", "P", "ok", "stats")}
+        for b in range(8):
+            pr = base[b]
+            hd = po.head_fields(pr["head"])
+            _, _, chk = R.ipa_fold(G, H, n, hd["x"], pr["L"], pr["R"], pr["a"][0], pr["b"][0], hd["c"], h)
+            for v in range(4):
+                Pc = craft_P(O, chk, v, rng)
+                ok, txt = R.cuda_inner_product_verify_log(n, pr["a"], pr["b"], hd["c"], pr["L"], pr["R"], hd["x"], Pc,
+                                                          G, H, h)
+                st = po.printed_stats(txt)
+                for k, val in zip(ipa, (b, v, Pc, ok, _printed_row(st)[3])):
+                    ipa[k].append(val)
+        out = dict(G=G, H=H, g=g, h=h,
+                   base_head=np.stack([p["head"] for p in base]), base_V=np.stack([p["V"] for p in base]),
+                   base_a=np.stack([p["a"] for p in base]), base_b=np.stack([p["b"] for p in base]),
+                   base_L=np.stack([p["L"] for p in base]), base_R=np.stack([p["R"] for p in base]),
+                   tamper=np.array([t[:3] for t in tam], np.int64),
+                   tamper_mask=np.array([t[3] for t in tam], np.uint64),
+                   rand_head=np.stack([p["head"] for p in rnd]), rand_L=np.stack([p["L"] for p in rnd]),
+                   rand_R=np.stack([p["R"] for p in rnd]),
+                   ok=np.array(rec["ok"]), early=np.array(rec["early"], np.uint8), x8c=np.stack(rec["x8c"]),
+                   x8e=np.stack(rec["x8e"]), stats=np.stack(rec["stats"]), P=np.stack(rec["P"]),
+                   check=np.stack(rec["check"]), check_pin=np.stack(rec["pin"]),
+                   ipa_base=np.array(ipa["base"], np.int64), ipa_variant=np.array(ipa["variant"], np.int64),
+                   ipa_P=np.stack(ipa["P"]), ipa_ok=np.array(ipa["ok"]), ipa_stats=np.stack(ipa["stats"]))
+        np.savez_compressed(os.path.join(HERE, f"accept_n{n}.npz"), **out)
+        print(f"accept n={n}: {len(cases)} cases, {int(out['ok'].sum())} accepts, {int(out['early'].sum())} early "
+              f"rejects; ipa crafted ok {out['ipa_ok'].astype(int).tolist()}")
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["ipa4096"]:
         make_ipa4096()
     elif sys.argv[1:] == ["rpverify"]:
         make_rpverify()
+    elif sys.argv[1:] == ["accept"]:
+        make_accept()
+    elif sys.argv[1:] == ["printed"]:
+        make_printed()
     else:
         main()
         make_ipa4096()
+        make_printed()
         make_rpverify()
+        make_accept()

@@ -33,8 +33,12 @@ def test_rooflines_without_matching_pmc(monkeypatch):
     r, v = bench.rooflines("k_terms", 1024, 64, 20, 20, 9.0, 0.108, {"k_terms": 180.0},
                            {"batch_per_gpu": 1024, "n": 64, "prefix_bits": 22, "pipelines": 2}, 2)
     per = 1024 * 6577 + 16640
-    assert r["alg_bytes_per_launch"] == per
-    assert abs(r["achieved"] - per / 9e-3 / 1e9) < 1e-9
+    assert r["alg_bytes_per_launch"] == per and r["alg_bytes_per_step"] == per
+    # the headline frac is driver-consistent: bytes per step / (wall time / steps), 20 steps in 0.108 s
+    assert abs(r["achieved"] - per * 20 / 0.108 / 1e9) < 1e-9
+    assert abs(r["frac"] - r["achieved"] / bench.HBM_PEAK_GBS) < 1e-15
+    # the overlapped per-launch figure only beside it
+    assert abs(r["per_launch_overlapped"]["achieved"] - per / 9e-3 / 1e9) < 1e-9
     assert r["frac"] < 1e-3 and r["traffic"] is None and r["traffic_over_alg"] is None
     assert v["frac"] is None and v["achieved_aggregate"] is None
 
@@ -54,3 +58,39 @@ def test_cpu_share(monkeypatch):
     assert nproc >= aff >= 1 and used == min(aff, 3)
     monkeypatch.delenv("OMP_NUM_THREADS")
     assert bench.cpu_share()[2] == aff
+
+
+def _run_bench(args, env_extra=None, timeout=240):
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                          timeout=timeout, env=env, cwd=ROOT)
+
+
+def test_gpus_flag_mismatch_with_launcher_world_fails():
+    # under a launcher the world must be the --gpus N asked for (no silent 1-rank line)
+    p = _run_bench(["--gpus", "8"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert p.returncode == 2 and "WORLD_SIZE=1" in p.stderr
+
+
+def test_gpus_flag_more_than_visible_fails(monkeypatch):
+    # --gpus 2 with fewer visible GPUs (none in this container): an error, not an N = 1 line
+    p = _run_bench(["--gpus", "2"])
+    assert p.returncode == 3 and "needs 2 GPUs" in p.stderr and not p.stdout.strip()
+
+
+def test_rank_launch_command(monkeypatch):
+    # --gpus N without a launcher: torch.distributed.run --nproc-per-node N on bench.py itself, as a child
+    import subprocess
+    seen = {}
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(subprocess, "call", lambda cmd: seen.setdefault("cmd", cmd) and 0)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--rehearse", "--steps", "3"])
+    a = argparse.Namespace(gpus=4, rehearse=True)
+    assert bench.rank_launch(a) == 0
+    cmd = seen["cmd"]
+    assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"] and "--nproc-per-node=4" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-5:] == ["--gpus", "4", "--rehearse", "--steps", "3"] and cmd[-6].endswith("bench.py")
+    assert bench.rank_launch(argparse.Namespace(gpus=1, rehearse=False)) is None

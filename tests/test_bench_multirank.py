@@ -28,13 +28,18 @@ def test_bench_two_ranks_rehearsal_matches_one_rank():
     one = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + SMALL, capture_output=True, text=True,
                          timeout=600, cwd=ROOT, env=env)
     assert one.returncode == 0, one.stderr[-2000:]
-    two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                          "--master-addr", "127.0.0.1", "--master-port", "29561", os.path.join(ROOT, "bench.py"),
-                          "--gpus", "2", "--rehearse"] + SMALL[:-2] + LEGS, capture_output=True, text=True, timeout=600, cwd=ROOT,
-                         env=env)
+    # no outer launcher: `--gpus 2` makes bench.py start the 2 ranks itself (torch.distributed.run child)
+    two = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--rehearse"] + SMALL[:-2]
+                         + LEGS, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
     assert two.returncode == 0, two.stderr[-2000:]
     l1, l2 = _line(one.stdout), _line(two.stdout)
     assert l1["n_gpus"] == 1 and l2["n_gpus"] == 2
+    # the line proves who ran: the torch.distributed world, one entry per rank, each rank's own batches
+    assert l1["world_size"] == 1 and l2["world_size"] == 2 and l2["backend"] == "gloo"
+    assert [r["rank"] for r in l2["ranks"]] == [0, 1] and len(l1["ranks"]) == 1
+    assert l2["ranks"][0]["verdicts_sha256"] == l1["ranks"][0]["verdicts_sha256"]   # rank 0's seeds whatever N
+    assert l2["ranks"][1]["verdicts_sha256"] != l2["ranks"][0]["verdicts_sha256"]   # distinct batches per rank
+    assert all(r["pci"] and r["proofs"] == 4 * 128 for r in l2["ranks"])
     assert l2["msm"]["scaling"] == "strong" and l2["scaling"] == "weak"
     assert l1["msm"]["result_sha256"] == l2["msm"]["result_sha256"]
     # Pippenger with its windows split over the 2 ranks == the single-GPU Pippenger
@@ -49,3 +54,14 @@ def test_bench_two_ranks_rehearsal_matches_one_rank():
     assert l1["repeats"]["n"] == l2["repeats"]["n"] == 5
     assert l2["config"]["passes_in_warmup_batch"] >= l1["config"]["passes_in_warmup_batch"]
     assert l2["ipa"]["n_gpus"] == 1 and l2["prove"]["n_gpus"] == 1 and l2["prove"]["valid"] == 256
+
+
+@pytest.mark.gpu
+def test_bench_more_gpus_than_visible_fails():
+    """`bench.py --gpus 2` on a one-GPU box must fail, not print a one-GPU line labelled N = 2."""
+    import torch
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("more than one GPU visible")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + SMALL, capture_output=True,
+                       text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 3 and "needs 2 GPUs" in p.stderr and not p.stdout.strip()

@@ -114,3 +114,27 @@ def test_reference_driver_runs_on_our_library():
     assert p.stderr.count("Vector lengths must match for inner product verification") == 1, p.stderr[-2000:]
     assert "HIP error" not in p.stderr
     assert p.returncode == -signal.SIGSEGV, (p.returncode, p.stderr[-2000:])
+
+
+def test_dropin_latency_harness_builds():
+    """tests/dropin_latency.c compiles against include/cudabulletproof_hip.h and links the library."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    exe = bench.build_dropin_latency()
+    assert "libcudabulletproof_hip.so" in subprocess.check_output(["ldd", exe], text=True)
+
+
+@pytest.mark.gpu
+def test_dropin_latency_wall_clock():
+    """The drop-in cuda_range_proof_verify, one reference proof per call, timed by wall clock in a
+    fresh process (tests/dropin_latency.c): every call returns the reference's verdict; the first
+    call (engine set-up included, the HIP runtime's own start-up timed apart) and the warm calls
+    are reported (bench.py configs0.dropin_latency carries the same figures)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    r = bench.dropin_latency(ns=(16,), warm=10)["n16"]
+    assert r["same_verdict_every_call"] and r["matches_reference_verdict"], r
+    assert r["devices"] >= 1 and 0 < r["warm_median_ms"] < 1000 and r["first_call_ms"] < 10000, r
+    print(r)

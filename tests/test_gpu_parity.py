@@ -1250,6 +1250,27 @@ def test_pipeline_quad_ticks_same_bits(bp, oracle, monkeypatch, n, B, mode, K, p
         _sample_vs_oracle(oracle, n, B, arrays, o[0].numpy().astype(bool), o[1].numpy().view(np.uint64), G, H, g, h)
 
 
+@pytest.mark.parametrize("n,B,lt", [(512, 3, "1024"), (512, 3, "512"), (256, 4, "4096"), (64, 5, "0")])
+def test_pipeline_lane_tree_knob_same_bits(bp, oracle, monkeypatch, n, B, lt):
+    """HIPBP_LANE_TREE_MAX only moves the MSM trees between RK_LTREE (one lane / quad per proof)
+    and RK_TREE blocks: with the lane trees on for n > 256 (above the block size) P and the
+    verdicts are the default layout's and the oracle's (advisor r03: final_task once re-reduced
+    the finished lane-tree root with the chunk roots there)."""
+    from cudabulletproof_amd import synth
+    import torch
+    G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+    g, h = oracle.gh()
+    arrays = synth.proofs(B, n, seed=900 + n)
+    monkeypatch.delenv("HIPBP_LANE_TREE_MAX", raising=False)
+    want = _pipeline_outputs(bp, n, B, 1, arrays, G, H, g, h, None)
+    monkeypatch.setenv("HIPBP_LANE_TREE_MAX", lt)
+    got = _pipeline_outputs(bp, n, B, 1, arrays, G, H, g, h, None)
+    for a, b in zip(want[-1], got[-1]):
+        assert torch.equal(a, b)
+    _sample_vs_oracle(oracle, n, B, arrays, got[-1][0].numpy().astype(bool), got[-1][1].numpy().view(np.uint64),
+                      G, H, g, h, step=1)
+
+
 @pytest.mark.parametrize("n,B,K", [(16, 70, 22), (64, 40, 20)])
 def test_pipeline_headline_table_width_same_bits(bp, oracle, n, B, K):
     """The headline's table width (bench.py: K = 22 at n = 64, 70 GB): prefix tables of K = 20-22
