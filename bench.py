@@ -782,7 +782,7 @@ def shard_push_batch(args, shard_size, npipe):
     and its last ticks (fold rounds 3..5, final terms, final assembly) are latency-bound, so a small
     shard (8192 proofs per rank at N = 8) goes through in one push per pipeline of at most 4096
     proofs: the two pipelines' latency-bound drain ticks then run side by side (tools/shard_probe.py,
-    DESIGN §5: 4096+4096 169.4 K, 2048 x 4 162.5 K, decreasing schedules 150-156 K)."""
+    profiles/NOTES.md §5: 4096+4096 169.4 K, 2048 x 4 162.5 K, decreasing schedules 150-156 K)."""
     if args.shard_batch > 0:
         return args.shard_batch
     per = -(-shard_size // npipe)

@@ -36,7 +36,7 @@ for k, (n, t) in sorted(tot.items(), key=lambda x: -x[1][1]):
     out.append(f"| {k} | {n} | {t / 1e6:.3f} | {t / n / 1e6:.4f} | {t / nmsm / 1e6:.4f} | {100 * t / all_ns:.1f} |")
 out.append(f"| **all kernels** |  | {all_ns / 1e6:.3f} |  | {all_ns / nmsm / 1e6:.3f} | 100 |")
 out += ["", "Per MSM, the kernel time adds to more than the wall time of one call because the top part's chunks, "
-        "window trees and Horner run on the side stream beside the bottom part's bucket trees (DESIGN §7c)."]
+        "window trees and Horner run on the side stream beside the bottom part's bucket trees (DESIGN §9, profiles/NOTES.md §7c)."]
 # PMC passes (profile_pip.sh): per kernel, summed over its launches in the 3-MSM probe runs,
 # per MSM; HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE (KB; gfx950 FETCH_SIZE x2 correction)
 def counters(name):
