@@ -331,11 +331,28 @@ def dropin_latency(ns=(16, 64), warm=20):
     return res
 
 
-def oracle_sample(n, B, seed, count=8):
+def oracle_sample(n, B, seed, count=64, procs=0):
     """The checker for the headline's self-check (bench `verify_check`): the first `count` proofs of
     the bench's batch 0 made by the CPU restatement's prover from the same inputs
     (synth.prove_inputs(B, n, seed) rows 0..count-1) and verified by it (crv:82 semantics): their
-    verdicts and IPA points P.  Test infrastructure, run before the GPU is touched."""
+    verdicts and IPA points P.  Test infrastructure, run before the GPU is touched, in worker
+    processes over the job's CPU share."""
+    count = min(count, B)
+    procs = max(1, min(procs or cpu_share()[2], 16, count))
+    cuts = [count * k // procs for k in range(procs + 1)]
+    jobs = [(n, B, seed, a, b) for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
+    if len(jobs) == 1:
+        parts = [_oracle_sample_rows(jobs[0])]
+    else:
+        import multiprocessing as mp
+        with mp.get_context("spawn").Pool(len(jobs)) as pool:
+            parts = pool.map(_oracle_sample_rows, jobs)
+    return {k: np.concatenate([p[k] for p in parts]) for k in ("ok", "P", "A")}
+
+
+def _oracle_sample_rows(args):
+    """oracle_sample's rows [lo, hi): the restatement's prover + verifier (one worker process)."""
+    n, B, seed, lo, hi = args
     from oracle import pyoracle
     from cudabulletproof_amd import synth
     O = pyoracle.Oracle()
@@ -343,7 +360,7 @@ def oracle_sample(n, B, seed, count=8):
     g, h = O.gh()
     pi = synth.prove_inputs(B, n, seed=seed)
     oks, Ps, heads = [], [], []
-    for p in range(count):
+    for p in range(lo, hi):
         sLR = np.concatenate([pi["sL"][p].view(np.uint8).reshape(n, 32), pi["sR"][p].view(np.uint8).reshape(n, 32)],
                              axis=1)
         pr = O.generate_range_proof(pi["v"][p].view(np.uint8), pi["gamma"][p].view(np.uint8), sLR,

@@ -114,6 +114,7 @@ EXPORTS = [
     "hipbp_sync", "hipbp_timing_enable",
     "hipbp_timing_collect", "hipbp_kernel_count", "hipbp_kernel_name", "hipbp_pipeline_create",
     "hipbp_pipeline_push", "hipbp_pipeline_flush", "hipbp_pipeline_depth", "hipbp_pipeline_destroy",
+    "hipbp_pipeline_defer_msm",
     "hipbp_release_stream_workspaces",
 ]
 
@@ -609,6 +610,11 @@ class VerifyPipeline:
         """hipbp_pipeline_use_gens: generators and prefix tables from a Generators set."""
         _chk(lib().hipbp_pipeline_use_gens(_c(self.h), _c(gens.h)))
         self._gens = gens
+
+    def defer_msm(self, on=True):
+        """hipbp_pipeline_defer_msm: split stage 0 for the batches pushed from now on (the MSM
+        terms, t*h and c*Q in one launch on an internal stream beside the fold rounds); same bits."""
+        _chk(lib().hipbp_pipeline_defer_msm(_c(self.h), ctypes.c_int(1 if on else 0)))
 
     def prefix_tables(self, bits):
         """hipbp_pipeline_prefix_tables: fixed-base prefix tables of the generators (same bits,

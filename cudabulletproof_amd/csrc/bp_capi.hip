@@ -149,7 +149,13 @@ struct Engine {
     }
     // prover workspaces (hipbp_batch_generate_range_proof), one per stream so batches on
     // different streams overlap (one batch's latency-bound stages under another's term launch)
-    struct ProverBufs { Buf b[19]; };
+    // + a high-priority side stream for the batch's latency-bound tail (chain0 .. final; created on
+    // first use) and the two events that order it after terms0 and before the caller's next work
+    struct ProverBufs {
+        Buf b[19];
+        hipStream_t tail = nullptr;
+        hipEvent_t ev_t0 = nullptr, ev_done = nullptr;
+    };
     std::map<hipStream_t, ProverBufs*> provers;
     hipEvent_t prove_gate = nullptr;   // HIPBP_PROVE_GATE: recorded after the last prover terms0
     // pinned host staging for the single-proof entry points (a pageable source of an
@@ -305,6 +311,7 @@ struct Gens {
 // point operation from ~1700 to ~750 for 4x the lanes, pairs to ~1140 for 2x: with both pipelines'
 // drains together, a 65,536-item tick is fastest on lanes, 32,768 on pairs, 16,384 on quads
 // (configs[4] shard: 173.8 K verifies/s vs 172.1 K with the round-3 bounds 49,152 / 98,304).
+constexpr unsigned long long ROW_MAX_ITEMS = 2048;   // 16-lane rows (sm_row) up to this many items
 constexpr unsigned long long QUAD_MAX_ITEMS = 16384;
 constexpr unsigned long long PAIR_MAX_ITEMS = 32768;
 
@@ -346,10 +353,21 @@ struct Pipeline {
     // first): HIPBP_LANE_TREE_MAX (lane trees for n <= it), HIPBP_CHAINS_FIRST (per-proof chain
     // regions at the start of the grid instead of the end).
     bool lane_tree = false, chains_first = false;
+    // Split stage 0 ("deferred MSM terms", hipbp_pipeline_defer_msm / HIPBP_DEFER_MSM=1): a batch
+    // pushed with it on runs only fold round 0 (+ the polynomial terms) in its stage-0 tick; the
+    // MSM terms, t*h and c*Q (read only by the final assembly) go to ONE RK_MSMT launch on the bulk
+    // stream `sb`, issued right after the batch's challenge tick and lane sort, and the batch's
+    // lane-tree tick (moved to stage FIN - 1) waits for it.  The fold chain then reaches its
+    // latency-bound last rounds sooner, with the MSM work running beside them: for a finite batch
+    // (configs[4]'s shards) the drain overlaps bulk work.  Needs the lane trees (n <= 64).
+    bool defer_msm = false;
+    hipStream_t sb = nullptr;
+    hipEvent_t ev_go = nullptr;
+    std::vector<hipEvent_t> ev_bulk;   // per slot: its RK_MSMT launch finished
     // drain-tick forms (push): HIPBP_QUAD forces lanes (0) / quads (1) / pairs (2) on every tick
     // (-1: by size), HIPBP_QUAD_MAX_ITEMS / HIPBP_PAIR_MAX_ITEMS move the size bounds
     int quad_force = -1;
-    unsigned long long quad_max = QUAD_MAX_ITEMS, pair_max = PAIR_MAX_ITEMS;
+    unsigned long long row_max = ROW_MAX_ITEMS, quad_max = QUAD_MAX_ITEMS, pair_max = PAIR_MAX_ITEMS;
     // Lane sort (bp::launch_lane_sort): per-lane-scalar items in chain-length order, for batches
     // of at least LANE_SORT_MIN proofs (HIPBP_LANE_SORT=0 turns it off, for A/B runs).
     static constexpr size_t LANE_SORT_MIN = 64;
@@ -383,9 +401,13 @@ struct Pipeline {
         const char* qe = getenv("HIPBP_QUAD");
         const char* qm = getenv("HIPBP_QUAD_MAX_ITEMS");
         const char* pm = getenv("HIPBP_PAIR_MAX_ITEMS");
-        quad_force = qe ? (atoi(qe) == 1 ? 4 : atoi(qe) == 2 ? 2 : 1) : -1;
+        quad_force = qe ? (atoi(qe) == 1 ? 4 : atoi(qe) == 2 ? 2 : atoi(qe) == 3 ? 16 : 1) : -1;
+        const char* rm = getenv("HIPBP_ROW_MAX_ITEMS");
+        row_max = rm ? strtoull(rm, nullptr, 10) : ROW_MAX_ITEMS;
         quad_max = qm ? strtoull(qm, nullptr, 10) : QUAD_MAX_ITEMS;
         pair_max = pm ? strtoull(pm, nullptr, 10) : PAIR_MAX_ITEMS;
+        const char* dm = getenv("HIPBP_DEFER_MSM");
+        defer_msm = dm && atoi(dm) != 0;
         Lr = log2i((size_t)n);
         D = stages(Lr).fin + 1;   // batches with fewer rounds finish earlier
         slots.resize(D);
@@ -416,6 +438,11 @@ struct Pipeline {
         if (sort_s) (void)hipStreamDestroy(sort_s);
         if (ev_tick) (void)hipEventDestroy(ev_tick);
         if (ev_sorted) (void)hipEventDestroy(ev_sorted);
+        if (sb) (void)hipStreamSynchronize(sb);
+        if (sb) (void)hipStreamDestroy(sb);
+        if (ev_go) (void)hipEventDestroy(ev_go);
+        for (auto ev : ev_bulk)
+            if (ev) (void)hipEventDestroy(ev);
         if (sort_bins.p) (void)hipFree(sort_bins.p);
         if (sort_offs.p) (void)hipFree(sort_offs.p);
         if (ptab.p) (void)hipFree(ptab.p);
@@ -474,6 +501,19 @@ struct Pipeline {
         for (auto& sl : slots) if (sl.active) return true;
         return false;
     }
+    bool defer_ok() const { return range_mode != 0 && lane_tree; }
+    hipError_t ensure_bulk() {
+        if (sb) return hipSuccess;
+        hipError_t r;
+        if ((r = hipStreamCreateWithFlags(&sb, hipStreamNonBlocking)) != hipSuccess) return r;
+        if ((r = hipEventCreateWithFlags(&ev_go, hipEventDisableTiming)) != hipSuccess) return r;
+        ev_bulk.assign(D, nullptr);
+        for (auto& ev : ev_bulk)
+            if ((r = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return r;
+        return hipSuccess;
+    }
+    // the stage of a batch's lane-tree region (RK_LTREE)
+    int ltree_stage(const Slot& sl, const Stages& g) const { return sl.dev.defer ? g.fin - 1 : std::min(3, g.fin - 1); }
     hipError_t carve(Slot& sl, size_t B, size_t Lb) {
         hipError_t r;
         size_t Lc = Lb ? Lb : 1;
@@ -524,6 +564,8 @@ struct Pipeline {
             nw.dev.lane_tree = lane_tree ? 1 : 0;
             nw.dev.ptab = pbits ? tables() : nullptr;
             nw.dev.pbits = pbits;
+            nw.dev.defer = (defer_msm && defer_ok()) ? 1 : 0;
+            if (nw.dev.defer) BP_RET_ON(ensure_bulk());
             BP_RET_ON(plan_sort(nw, head));
             BP_RET_ON(hipEventSynchronize(nw.copied));   // staging slot free again
             host_dev[head] = nw.dev;
@@ -537,6 +579,8 @@ struct Pipeline {
         }
         bp::RegionList tr{};
         bool overflow = false;
+        int wait_bulk[32];   // slots whose RK_MSMT launch this tick's lane-tree region must wait for
+        int nwait = 0;
         auto add = [&overflow](bp::RegionList& rl, int kind, int slot, int r, unsigned long long items, unsigned align) {
             if (!items) return;
             if (rl.count == bp::MAX_REGIONS) { overflow = true; return; }
@@ -562,12 +606,16 @@ struct Pipeline {
                     if (st == g.fin) add(tr, bp::RK_FINAL, idx, 0, B, 64);
                     // the lane MSM trees need only stage 0's terms: a few ticks before the final one,
                     // so a drain's last tick is the short P / check-point assembly alone
-                    if (range_mode && lane_tree && st == std::min(3, g.fin - 1)) add(tr, bp::RK_LTREE, idx, 0, B, 64);
+                    if (range_mode && lane_tree && st == ltree_stage(sl, g)) {
+                        add(tr, bp::RK_LTREE, idx, 0, B, 64);
+                        if (sl.dev.defer && nwait < 32) wait_bulk[nwait++] = idx;
+                    }
                     if (st == 2 && range_mode == 2) add(tr, bp::RK_POLY, idx, 0, B, 64);
                     if (st == 0) add(tr, bp::RK_PREP, idx, 0, range_mode ? 2 * B : B, 64);
                 } else if (pass == 2) {
                     if (st == 1) {
-                        add(tr, bp::RK_STAGE0, idx, 0, bp::stage0_lanes(B, n, L, range_mode).total, 64);
+                        add(tr, bp::RK_STAGE0, idx, 0,
+                            bp::stage0_lanes(B, n, L, range_mode, sl.dev.defer ? bp::S0_CRIT : bp::S0_ALL).total, 64);
                     }
                     if (st >= 2 && st <= L) add(tr, bp::RK_ROUND, idx, st - 1, B * 4 * (n >> st), 64);
                     if (st == g.ft) add(tr, bp::RK_FINAL_TERMS, idx, 0, B * 2, 64);
@@ -586,7 +634,8 @@ struct Pipeline {
             if (bp::region_is_sm(tr.reg[k].kind)) sm_items += tr.reg[k].items;
         // Between the two (up to PAIR_MAX_ITEMS), lane pairs (HIPBP_QUAD=2 forces them,
         // HIPBP_PAIR_MAX_ITEMS sets the bound).
-        int ql = sm_items <= quad_max ? 4 : sm_items <= pair_max ? 2 : 1;   // (a tick of chains alone is small too)
+        int ql = sm_items <= row_max ? 16 : sm_items <= quad_max ? 4 : sm_items <= pair_max ? 2 : 1;
+        if (!sm_items) ql = 4;   // a tick of chains alone: the chains on quads
         if (quad_force >= 0) ql = quad_force;
         if (ql > 1) {   // re-lay the regions: scalar-multiplication items ql lanes each
             unsigned long long tot = 0;
@@ -600,6 +649,7 @@ struct Pipeline {
             tr.total = tot;
         }
         if (tr.total >= (1ull << 32)) { g_err = "pipeline tick exceeds 2^32 lanes (batch too large for n)"; return HIPBP_ERR_ARG; }
+        for (int k = 0; k < nwait; k++) BP_RET_ON(hipStreamWaitEvent(s, ev_bulk[wait_bulk[k]], 0));
         if (tm) tm->mark(bp::KT_TERMS, false, s);
         bp::launch_terms(tr, slots_dev, G, H, g ? g : h, h, e->dtab, e->two_i, s, ql);
         if (tm) tm->mark(bp::KT_TERMS, true, s);
@@ -617,12 +667,42 @@ struct Pipeline {
                 BP_RET_ON(hipGetLastError());
             }
         }
+        if (has && nw.dev.defer) {
+            const int rc = launch_bulk(head);
+            if (rc != HIPBP_OK) return rc;
+        }
         for (auto& sl : slots) {
             if (!sl.active) continue;
             if (sl.stage == stages(sl.dev.bv.L_len).fin) sl.active = false;
             else sl.stage++;
         }
         head = (head + 1) % D;
+        return HIPBP_OK;
+    }
+    // The split stage 0's deferred part of the batch in slot idx (its challenges ran in the tick
+    // just enqueued on s, its lane order after it): ONE RK_MSMT launch on the bulk stream.
+    int launch_bulk(int idx) {
+        Slot& sl = slots[idx];
+        const unsigned long long B = sl.dev.bv.B;
+        bp::RegionList br{};
+        bp::Region& rg = br.reg[0];
+        br.count = 1;
+        rg.kind = bp::RK_MSMT;
+        rg.slot = idx;
+        rg.r = 0;
+        rg.begin = 0;
+        rg.items = bp::stage0_lanes(B, n, sl.dev.bv.L_len, range_mode, bp::S0_DEFER).total;
+        int ql = rg.items <= row_max ? 16 : rg.items <= quad_max ? 4 : rg.items <= pair_max ? 2 : 1;
+        if (quad_force >= 0) ql = quad_force;
+        rg.items *= ql;
+        br.total = (rg.items + 63) & ~63ull;
+        if (!rg.items) return HIPBP_OK;
+        if (br.total >= (1ull << 32)) { g_err = "pipeline bulk launch exceeds 2^32 lanes"; return HIPBP_ERR_ARG; }
+        BP_RET_ON(hipEventRecord(ev_go, s));
+        BP_RET_ON(hipStreamWaitEvent(sb, ev_go, 0));
+        bp::launch_terms(br, slots_dev, G, H, g ? g : h, h, e->dtab, e->two_i, sb, ql);
+        BP_RET_ON(hipGetLastError());
+        BP_RET_ON(hipEventRecord(ev_bulk[idx], sb));
         return HIPBP_OK;
     }
     int flush() {
@@ -976,6 +1056,13 @@ int hipbp_release_stream_workspaces(void* stream) {
     }
     auto pi = e->provers.find(s);
     if (pi != e->provers.end()) {
+        Engine::ProverBufs* pb = pi->second;
+        if (pb->tail) {
+            keep(hipStreamSynchronize(pb->tail));
+            keep(hipStreamDestroy(pb->tail));
+        }
+        if (pb->ev_t0) keep(hipEventDestroy(pb->ev_t0));
+        if (pb->ev_done) keep(hipEventDestroy(pb->ev_done));
         free_all(pi->second->b, sizeof(pi->second->b) / sizeof(pi->second->b[0]));
         delete pi->second;
         e->provers.erase(pi);
@@ -1074,17 +1161,45 @@ static int prove_run(const hipbp_prove_input* in, const ge25519* G, const ge2551
     }
     run(bp::PS_TERMS0, 0);
     if (gate) BP_RET_ON(hipEventRecord(e->prove_gate, s));
-    run(bp::PS_CHAIN0, 0);
-    run(bp::PS_COMMIT, 0);
-    run(bp::PS_TERMS1, 0);
-    run(bp::PS_TX, 0);
-    for (int r = 0; r < pin.L; r++) {
-        run(bp::PS_RTERMS, r);
-        run(bp::PS_RCHAIN, r);
-        run(bp::PS_ROUND, r);
+    // The tail (chain0 .. final: ~20 short dependent launches, mostly latency-bound) runs on a
+    // high-priority side stream of this workspace: with two caller streams, another batch's terms0
+    // holds every VGPR, and at equal priority the tail's blocks only got slots as that terms0
+    // drained (r03q trace: chain0 stretched to ~40 ms).  At high priority each freed slot goes to
+    // the tail first.  The caller's stream waits for the tail, so the call stays ordered on it.
+    // HIPBP_PROVE_TAIL_STREAM=0 keeps everything on the caller's stream (A/B).
+    static const bool tail_stream = !getenv("HIPBP_PROVE_TAIL_STREAM") || atoi(getenv("HIPBP_PROVE_TAIL_STREAM")) != 0;
+    hipStream_t ts = s;
+    if (tail_stream) {
+        if (!pb->tail) {
+            int lo_pr = 0, hi_pr = 0;
+            BP_RET_ON(hipDeviceGetStreamPriorityRange(&lo_pr, &hi_pr));
+            BP_RET_ON(hipStreamCreateWithPriority(&pb->tail, hipStreamNonBlocking, hi_pr));
+            BP_RET_ON(hipEventCreateWithFlags(&pb->ev_t0, hipEventDisableTiming));
+            BP_RET_ON(hipEventCreateWithFlags(&pb->ev_done, hipEventDisableTiming));
+        }
+        BP_RET_ON(hipEventRecord(pb->ev_t0, s));
+        BP_RET_ON(hipStreamWaitEvent(pb->tail, pb->ev_t0, 0));
+        ts = pb->tail;
     }
-    run(bp::PS_FINAL, 0);
+    auto run_t = [&](int stage, int r) {
+        bp::launch_prove(stage, r, pin, w, po, (const bp::ge*)G, (const bp::ge*)H, (const bp::ge*)g,
+                         (const bp::ge*)h, e->dtab, e->two_i, ts);
+    };
+    run_t(bp::PS_CHAIN0, 0);
+    run_t(bp::PS_COMMIT, 0);
+    run_t(bp::PS_TERMS1, 0);
+    run_t(bp::PS_TX, 0);
+    for (int r = 0; r < pin.L; r++) {
+        run_t(bp::PS_RTERMS, r);
+        run_t(bp::PS_RCHAIN, r);
+        run_t(bp::PS_ROUND, r);
+    }
+    run_t(bp::PS_FINAL, 0);
     BP_RET_ON(hipGetLastError());
+    if (tail_stream) {
+        BP_RET_ON(hipEventRecord(pb->ev_done, ts));
+        BP_RET_ON(hipStreamWaitEvent(s, pb->ev_done, 0));
+    }
     return HIPBP_OK;
 }
 
@@ -1167,6 +1282,18 @@ int hipbp_pipeline_use_gens(void* handle, void* gens) {
     pl->g = gs->g();
     pl->ext_tab = gs->bits ? gs->tab.as<bp::ge>() : nullptr;
     pl->pbits = gs->bits;
+    return HIPBP_OK;
+}
+
+int hipbp_pipeline_defer_msm(void* handle, int on) {
+    Pipeline* pl = (Pipeline*)handle;
+    if (!pl) { g_err = "null pipeline"; return HIPBP_ERR_ARG; }
+    if (on && !pl->defer_ok()) {
+        g_err = "defer_msm: needs cuda_range_proof_verify / range_proof_verify semantics and n <= the lane-tree limit";
+        return HIPBP_ERR_ARG;
+    }
+    std::lock_guard<std::mutex> lk(pl->e->mu);
+    pl->defer_msm = on != 0;   // applies to the batches pushed from now on
     return HIPBP_OK;
 }
 

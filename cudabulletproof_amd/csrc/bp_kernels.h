@@ -79,6 +79,10 @@ struct SlotDev {
     // table is ptab[b << pbits ..], b = k for G_k, n + k for H_k, 2n for h (= Q), 2n + 1 for g.
     const ge* ptab;
     int pbits;
+    // 1: stage 0 is split (Pipeline "deferred MSM terms"): RK_STAGE0 runs only the items later
+    // stages wait for (fold round 0, mode-2 polynomial terms); the two MSMs' terms and t*h, c*Q,
+    // which only the final assembly reads, run as an RK_MSMT launch on the pipeline's bulk stream
+    int defer;
 };
 
 // Stage-0 lane layout (host and device).  stage0_task's items by class — the <sG,G>/<sH,H>
@@ -94,15 +98,20 @@ struct Stage0Lanes {
     unsigned long long total;             // region lanes
     unsigned long long pl;                // per-lane items (perm0 length)
 };
-__host__ __device__ inline Stage0Lanes stage0_lanes(unsigned long long B, int n, int L, int range_mode) {
+// sel: S0_ALL every stage-0 item; S0_CRIT the split stage 0's RK_STAGE0 part (fold round 0 and
+// the polynomial terms); S0_DEFER its RK_MSMT part (the MSM terms, t*h and c*Q).  The per-lane
+// classes keep their S0_ALL positions in perm0 (the lane sort always orders all of them).
+enum Stage0Sel { S0_ALL = 0, S0_CRIT = 1, S0_DEFER = 2 };
+__host__ __device__ inline Stage0Lanes stage0_lanes(unsigned long long B, int n, int L, int range_mode, int sel = S0_ALL) {
     Stage0Lanes z;
     const unsigned long long msm = range_mode ? B * 2 * n : 0, fold = L > 0 ? B * 2 * n : 0;
     const bool uni = n >= 64;
-    z.U = uni ? msm / 2 + fold : 0;
-    z.size[0] = uni ? msm / 2 : msm;
-    z.size[1] = uni ? 0 : fold;
-    z.size[2] = B * 2;
-    z.size[3] = range_mode == 2 ? B * 7 : 0;
+    const bool m = sel != S0_CRIT, f = sel != S0_DEFER;   // MSM-side / fold-side items included
+    z.U = uni ? (m ? msm / 2 : 0) + (f ? fold : 0) : 0;
+    z.size[0] = m ? (uni ? msm / 2 : msm) : 0;
+    z.size[1] = f && !uni ? fold : 0;
+    z.size[2] = m ? B * 2 : 0;
+    z.size[3] = f && range_mode == 2 ? B * 7 : 0;
     unsigned long long o = z.U, pl = 0;
     for (int c = 0; c < 4; c++) {
         z.off[c] = o;
@@ -145,7 +154,8 @@ void launch_lane_sort(const LaneSortPlan& plan, unsigned* bins, unsigned* offs, 
 // (P, check point, accept).
 enum RegionKind { RK_STAGE0 = 0, RK_ROUND = 1, RK_FINAL_TERMS = 2, RK_FINAL = 4, RK_PREP = 5,
                   RK_TREE = 6, RK_POLY = 7, RK_M3 = 8,
-                  RK_LTREE = 9 /* the n <= LANE_TREE_MAX MSM trees, one lane (quad) per proof, into msm_part */ };
+                  RK_LTREE = 9 /* the n <= LANE_TREE_MAX MSM trees, one lane (quad) per proof, into msm_part */,
+                  RK_MSMT = 10 /* split stage 0's deferred part (SlotDev::defer), on the bulk stream */ };
 struct Region {
     int kind;
     int slot;
@@ -175,17 +185,17 @@ void launch_init_tables(ge* dtab, fe* two_i, int nmax, hipStream_t s);
 // left unwritten): tab[(2n + 2) << K].
 void launch_prefix_tables(ge* tab, const ge* G, const ge* H, const ge* h, const ge* g, int n, int K, hipStream_t s);
 // ql: lanes per scalar-multiplication item (1; 2: lane pairs; 4: lane quads, the drain-tick form,
-// whose chain regions take 4 lanes per proof too), k_terms<ql>
+// whose chain regions take 4 lanes per proof too; 16: 16-lane rows, chains on quads), k_terms<ql>
 void launch_terms(const RegionList& rl, const SlotDev* slots, const ge* G, const ge* H, const ge* g, const ge* h,
                   const ge* dtab, const fe* two_i, hipStream_t s, int ql = 1);
 inline bool region_is_sm(int kind) {
-    return kind == RK_STAGE0 || kind == RK_ROUND || kind == RK_FINAL_TERMS || kind == RK_M3;
+    return kind == RK_STAGE0 || kind == RK_ROUND || kind == RK_FINAL_TERMS || kind == RK_M3 || kind == RK_MSMT;
 }
 // lanes per item of a region in the form with ql lanes per scalar multiplication (the chain regions
 // go on quads in the quad form only)
 inline int region_lanes(int kind, int ql) {
     if (region_is_sm(kind)) return ql;
-    return (ql == 4 && (kind == RK_FINAL || kind == RK_LTREE)) ? 4 : 1;
+    return (ql >= 4 && (kind == RK_FINAL || kind == RK_LTREE)) ? 4 : 1;
 }
 
 // Generic canonical-tree MSM.  perm [m] / bins [MSM_BINS] (nullable): workspace of the

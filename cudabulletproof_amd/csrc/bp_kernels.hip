@@ -389,21 +389,23 @@ __device__ __forceinline__ uint32_t stage0_class_item(const SlotDev& sd, int c, 
     return nA + nB + 2 * B + j;
 }
 
-// Stage-0 lane -> stage0_task item, or SIZE_MAX for a padding lane (stage0_lanes).
-__device__ __forceinline__ uint32_t stage0_item(const SlotDev& sd, uint32_t l) {
+// Stage-0 lane -> stage0_task item, or SIZE_MAX for a padding lane (stage0_lanes; sel: the
+// part of a split stage 0 the region runs, Stage0Sel).
+__device__ __forceinline__ uint32_t stage0_item(const SlotDev& sd, uint32_t l, int sel = S0_ALL) {
     const uint32_t B = (uint32_t)sd.bv.B;
     const int n = sd.bv.n, ln = log2n(n);
-    const Stage0Lanes z = stage0_lanes(B, n, sd.bv.L_len, sd.range_mode);
+    const Stage0Lanes z = stage0_lanes(B, n, sd.bv.L_len, sd.range_mode, sel);
     if (l < (uint32_t)z.U) {
-        const uint32_t nG = sd.range_mode ? B << ln : 0;
+        const uint32_t nG = (sd.range_mode && sel != S0_CRIT) ? B << ln : 0;
         if (l < nG) return ((l >> ln) << (ln + 1)) + (l & (n - 1));   // <sG,G> segment of proof l / n
         return (sd.range_mode ? B << (ln + 1) : 0) + (l - nG);
     }
+    const Stage0Lanes za = sel == S0_ALL ? z : stage0_lanes(B, n, sd.bv.L_len, sd.range_mode);
     int c = 0;
-    uint32_t base = 0;   // class c's offset in perm0
+    uint32_t base = 0;   // class c's offset in perm0 (the S0_ALL class sizes)
 #pragma unroll
     for (int k = 1; k < 4; k++)
-        if (l >= (uint32_t)z.off[k]) { c = k; base += (uint32_t)z.size[k - 1]; }
+        if (l >= (uint32_t)z.off[k]) { c = k; base += (uint32_t)za.size[k - 1]; }
     const uint32_t j = l - (uint32_t)z.off[c];
     if (j >= (uint32_t)z.size[c]) return UINT32_MAX;
     return stage0_class_item(sd, c, sd.perm0 ? sd.perm0[base + j] : j);
@@ -811,8 +813,10 @@ void launch_lane_sort(const LaneSortPlan& plan, unsigned* bins, unsigned* offs, 
 // form; 4 (the drain ticks, too small to fill the SIMDs, whose time is one scalar-multiplication
 // chain's latency) a lane quad per item running sm_quad, 3 product latencies per point operation
 // instead of 9, and the chains (RK_LTREE, RK_FINAL) on quads too; 2 a lane pair per item running
-// sm_pair (5 product latencies, 10 products instead of 9), for ticks between the two.  Region items
-// are QL lanes each.  The same operations in every form, so the same bits.
+// sm_pair (5 product latencies, 10 products instead of 9), for ticks between the two; 16 (the
+// smallest ticks: a one-proof call) a 16-lane row per item running sm_row, each product split
+// over a quad, the chains on quads.  Region items are QL lanes each (chains 4 in the row form).
+// The same operations in every form, so the same bits.
 #ifdef BP_TERMS_WPE   // A/B: a register budget for more waves per SIMD than k_terms runs (room for other kernels' waves)
 #define BP_TERMS_BOUNDS __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(BP_TERMS_WPE, 8)))
 #else
@@ -858,10 +862,10 @@ __global__ BP_TERMS_BOUNDS void k_terms(RegionList rl, const SlotDev* __restrict
     } else if (rg.kind == RK_POLY) {
         poly_task(sd, l);
     } else if (rg.kind == RK_FINAL) {
-        if (QL == 4) final_task<true>(sd, l >> 2);
+        if (QL >= 4) final_task<true>(sd, l >> 2);   // the chains stay on quads in the row form
         else final_task<false>(sd, l);
     } else if (rg.kind == RK_LTREE) {
-        if (QL == 4) ltree_task<true>(sd, l >> 2);
+        if (QL >= 4) ltree_task<true>(sd, l >> 2);
         else ltree_task<false>(sd, l);
     } else {
         // the scalar-multiplication kinds: fill the job, then the one call site
@@ -869,10 +873,11 @@ __global__ BP_TERMS_BOUNDS void k_terms(RegionList rl, const SlotDev* __restrict
         jb.base = -1;
         bool live = true;
         uint32_t li = (uint32_t)l;   // < 2^32: Pipeline::push keeps a tick below 2^32 lanes
-        if (QL == 4) li >>= 2;       // the quad's / pair's item
+        if (QL == 16) li >>= 4;      // the row's / quad's / pair's item
+        if (QL == 4) li >>= 2;
         if (QL == 2) li >>= 1;
-        if (rg.kind == RK_STAGE0) {
-            const uint32_t it = stage0_item(sd, li);
+        if (rg.kind == RK_STAGE0 || rg.kind == RK_MSMT) {
+            const uint32_t it = stage0_item(sd, li, rg.kind == RK_MSMT ? S0_DEFER : sd.defer ? S0_CRIT : S0_ALL);
             live = it != UINT32_MAX && stage0_job(sd, it, G, H, g, h, jb);
         } else if (rg.kind == RK_M3) {
             m3_job(sd, li, jb);
@@ -886,7 +891,10 @@ __global__ BP_TERMS_BOUNDS void k_terms(RegionList rl, const SlotDev* __restrict
         }
         if (live) {
             const ge* pt = (sd.ptab && jb.base >= 0) ? sd.ptab + ((size_t)jb.base << sd.pbits) : nullptr;
-            if (QL == 4) {
+            if (QL == 16) {
+                const ge t = sm_row(jb.s, jb.P, dtab, pt, pt ? sd.pbits : 0);
+                if ((threadIdx.x & 15) == 0) *jb.dst = jb.dev_norm ? ge_norm_dev(t) : ge_norm_host(t);
+            } else if (QL == 4) {
                 const ge t = sm_quad(jb.s, jb.P, dtab, pt, pt ? sd.pbits : 0);
                 if ((threadIdx.x & 3) == 0) *jb.dst = jb.dev_norm ? ge_norm_dev(t) : ge_norm_host(t);
             } else if (QL == 2) {
@@ -907,7 +915,8 @@ void launch_terms(const RegionList& rl, const SlotDev* slots, const ge* G, const
     if (!rl.total) return;
     // A/B knob: unused dynamic LDS per block, to cap how many k_terms blocks share a CU
     static const unsigned pad = [] { const char* e = getenv("HIPBP_TERMS_LDS_PAD"); return e ? (unsigned)atoi(e) : 0u; }();
-    if (ql == 4) k_terms<4><<<nblk(rl.total), TPB, pad, s>>>(rl, slots, G, H, g, h, dtab, two_i);
+    if (ql == 16) k_terms<16><<<nblk(rl.total), TPB, pad, s>>>(rl, slots, G, H, g, h, dtab, two_i);
+    else if (ql == 4) k_terms<4><<<nblk(rl.total), TPB, pad, s>>>(rl, slots, G, H, g, h, dtab, two_i);
     else if (ql == 2) k_terms<2><<<nblk(rl.total), TPB, pad, s>>>(rl, slots, G, H, g, h, dtab, two_i);
     else k_terms<1><<<nblk(rl.total), TPB, pad, s>>>(rl, slots, G, H, g, h, dtab, two_i);
 }

@@ -511,17 +511,7 @@ __global__ __launch_bounds__(PTPB) void k_pip_window(const ge* __restrict__ V, i
 
 // ---- the Horner chain: one point operation per 16-lane row, one product per lane quad.
 // (fe_mul_q4, the product split over a lane quad: ge25519_quad.h)
-template <int SRC>   // lane SRC of each 16-lane row to the whole row
-__device__ __forceinline__ fe fe_row_bcast(const fe& a) {
-    fe r;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)a.v[i], 0x150 + SRC, 0xF, 0xF, true);
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(a.v[i] >> 32), 0x150 + SRC, 0xF, 0xF, true);
-        r.v[i] = (uint64_t)lo | ((uint64_t)hi << 32);
-    }
-    return r;
-}
+// (fe_row_bcast: lane SRC of each 16-lane row to the whole row, ge25519_quad.h)
 // DBL: add(p, p) (q ignored); else add(p, q).  p, q replicated over the row; result replicated.
 // Quad qi of the row forms product qi of each stage (A, B, T1 T2, Z1 Z2 / X3, Y3, Z3, T3).
 template <bool DBL>

@@ -141,7 +141,9 @@ __global__ __launch_bounds__(TPB) void k_prove_prep(ProveIn in, ProveWs ws, cons
 // The heavy items are random 255-bit scalars (sL, sR, gamma): a wave runs as long as its
 // longest chain, so the heavy list is counting-sorted by chain length (sm_ops) into slist,
 // longest first (the same scheme as the MSM's k_ops_*).
-constexpr int SORT_T = 1024;
+// 256-thread blocks: a 1024-thread block needs a whole CU's wave slots and waits behind the other
+// stream's running terms0 (in the r03q trace the scatter took 28 ms per launch that way)
+constexpr int SORT_T = 256;
 __global__ __launch_bounds__(TPB) void k_prove_sort_hist(ProveIn in, ProveWs ws) {
     __shared__ unsigned hb[MSM_BINS];
     for (int k = threadIdx.x; k < MSM_BINS; k += TPB) hb[k] = 0;
@@ -534,7 +536,10 @@ void launch_prove(int stage, int r, const ProveIn& in, const ProveWs& ws, const 
             // A/B knob: unused dynamic LDS per block, capping terms0 blocks per CU (room for the other
             // stream's chains)
             static const unsigned pad = [] { const char* e = getenv("HIPBP_PROVE_T0_PAD"); return e ? (unsigned)atoi(e) : 0u; }();
-            k_prove_terms0<<<nblk(B * (4 * (size_t)n + 4) + 2 * n), TPB, pad, s>>>(in, ws, G, H, g, h, dtab);
+            // the lists hold at most 2n + 4 items per proof (sL, sR, v, gamma, alpha, rho): every aL / aR
+            // term is a zero-scalar constant or a ctab entry (BP_GTAB), so the grid stops there
+            const size_t per_max = BP_GTAB ? 2 * (size_t)n + 4 : 4 * (size_t)n + 4;
+            k_prove_terms0<<<nblk(B * per_max + 2 * n), TPB, pad, s>>>(in, ws, G, H, g, h, dtab);
             break;
         }
         case PS_CHAIN0: k_prove_chain0<<<nblk(B * 4), TPB, 0, s>>>(in, ws); break;

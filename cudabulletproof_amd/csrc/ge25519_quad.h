@@ -232,6 +232,75 @@ __device__ __forceinline__ ge sm_quad(const fe& s, const ge& P, const ge* __rest
     return quad_of_point(r3);
 }
 
+// The same on a 16-lane ROW, in operand form: lane quad qi of the row takes role qi of sm_quad's
+// lanes (operands Y-X | T | Z | Y+X, stage-3 products X3 | T3 | Z3 | Y3), replicated over its four
+// lanes, and every product is split over the quad by rows (fe_mul_q4: four 64 x 256-bit partials,
+// two DPP levels, the fold on the quad's lane 0).  A step is then 3 quarter-products deep instead of
+// 3 products: for ticks of at most a few thousand items (a one-proof call, a small drain), whose
+// time is one scalar-multiplication chain's latency at one wave per SIMD.  The stage results go to
+// the row over row_newbcast; quads 0 and 3 swap X3 / Y3 over row_mirror (quad q <-> quad 3 - q;
+// the values are replicated over each quad, so the mirrored lane order within a quad is moot).
+// The same 512-bit products and the same add / sub / fold code, so the same bits.
+template <int SRC>   // lane SRC of each 16-lane row to the whole row (DPP row_newbcast)
+__device__ __forceinline__ fe fe_row_bcast(const fe& a) {
+    fe r;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)a.v[i], 0x150 + SRC, 0xF, 0xF, true);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(a.v[i] >> 32), 0x150 + SRC, 0xF, 0xF, true);
+        r.v[i] = (uint64_t)lo | ((uint64_t)hi << 32);
+    }
+    return r;
+}
+__device__ __forceinline__ fe ge_row_of_step(const fe& o, const fe& q) {
+    const int qi = (threadIdx.x >> 2) & 3;
+    const fe p1 = fe_mul_q4(o, q);   // role qi's stage-1 product, on the quad's lane 0
+    const fe A = fe_row_bcast<0>(p1), CT = fe_row_bcast<4>(p1), D0 = fe_row_bcast<8>(p1), B = fe_row_bcast<12>(p1);
+    const fe C = fe_quad_bcast<0>(fe_mul_q4(CT, k_const()));
+    const fe D = fe_add(D0, D0);
+    fe E, F, G, H;
+    fe_addsub(B, A, H, E);   // H = B + A, E = B - A
+    fe_addsub(D, C, G, F);   // G = D + C, F = D - C
+    return fe_quad_bcast<0>(fe_mul_q4(fe_sel(qi & 2, G, E), fe_sel(qi & 1, H, F)));
+}
+__device__ __forceinline__ fe row_of_next(const fe& r3) {   // quad 0: Y3 - X3, quad 3: X3 + Y3
+    const int qi = (threadIdx.x >> 2) & 3;
+    const fe sw = fe_dpp<0x140>(r3);   // row_mirror: quad q <- quad 3 - q
+    fe s, d;
+    fe_addsub(sw, r3, s, d);
+    return fe_sel(qi == 0, d, fe_sel(qi == 3, s, r3));
+}
+__device__ __forceinline__ fe row_of_form(const ge& r) {
+    return fe_sel4((threadIdx.x >> 2) & 3, fe_sub(r.Y, r.X), r.T, r.Z, fe_add(r.Y, r.X));
+}
+__device__ __forceinline__ ge row_of_point(const fe& r3) {   // X3 | T3 | Z3 | Y3 by quad -> replicated
+    return ge{fe_row_bcast<0>(r3), fe_row_bcast<12>(r3), fe_row_bcast<8>(r3), fe_row_bcast<4>(r3)};
+}
+__device__ __forceinline__ ge sm_row(const fe& s, const ge& P, const ge* __restrict__ dtab, const ge* ptab, int K) {
+    const fe qs = row_of_form(P);
+    const int lz = fe_clz256(s);
+    const bool pre = K > 0 && lz < K && ptab != nullptr;
+    const ge r0 = *(pre ? &ptab[prefix_index(s, K)] : &dtab[lz]);
+    int i = pre ? 255 - K : 255 - lz;   // index of the pending bit
+    if (i < 0) return r0;
+    BitStream bs = bs_init(s, i);
+    uint32_t bit = bs_next(bs);
+    bool add_phase = false;   // false: next op doubles; true: next op adds P
+    fe o = row_of_form(r0), r3;
+    while (true) {
+        r3 = ge_row_of_step(o, fe_sel(add_phase, qs, o));
+        if (!add_phase && bit) {
+            add_phase = true;
+        } else {
+            add_phase = false;
+            if (--i < 0) break;
+            bit = bs_next(bs);
+        }
+        o = row_of_next(r3);
+    }
+    return row_of_point(r3);
+}
+
 // The same on a lane PAIR, in operand form: lane 0 holds {Y-X, T}, lane 1 {Y+X, Z}; stage 1: lane 0
 // forms A and T1 T2, lane 1 B and Z1 Z2; the pair swaps them over DPP; stage 3: lane 0 X3 = E F and
 // T3 = E H, lane 1 Z3 = G F and Y3 = G H (one operand select: G over E on lane 1), so T3 and Z3 are

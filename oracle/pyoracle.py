@@ -448,6 +448,36 @@ def have_reference():
     return os.path.exists(REF_SO)
 
 
+def _verify_chunk(args):
+    n, heads, Vs, As, Bs, Ls, Rs, G, H, g, h = args
+    O = Oracle()
+    out = []
+    for i in range(len(heads)):
+        ok, P, chk, _, _ = O.cuda_range_proof_verify(heads[i], Vs[i], n, As[i], Bs[i], Ls[i], Rs[i], G, H, g, h)
+        out.append((ok, P, chk))
+    return out
+
+
+def cuda_range_proof_verify_many(n, heads, Vs, As, Bs, Ls, Rs, G, H, g, h, procs=None):
+    """The restatement's cuda_range_proof_verify over many proofs, in `procs` spawned worker
+    processes (children that never touch a GPU) -> (ok (m,) bool, P (m,16), check (m,16))."""
+    import multiprocessing as mp
+    m = len(heads)
+    if procs is None:
+        procs = min(16, os.cpu_count() or 1)
+    procs = max(1, min(procs, m))
+    cuts = [m * k // procs for k in range(procs + 1)]
+    jobs = [(n, heads[a:b], Vs[a:b], As[a:b], Bs[a:b], Ls[a:b], Rs[a:b], G, H, g, h)
+            for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
+    if procs == 1:
+        res = [_verify_chunk(j) for j in jobs]
+    else:
+        with mp.get_context("spawn").Pool(len(jobs)) as pool:
+            res = pool.map(_verify_chunk, jobs)
+    flat = [r for part in res for r in part]
+    return (np.array([r[0] for r in flat], bool), np.stack([r[1] for r in flat]), np.stack([r[2] for r in flat]))
+
+
 # ---------------------------------------------------------------- the accept rule's figures
 # cuda_inner_product_verify reports its comparison of the check point with P on stdout
 # (crv:287-346) and accepts if any of four tests holds (crv:349-357).  STATS names the printed

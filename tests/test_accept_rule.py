@@ -153,8 +153,8 @@ def _batch_arrays(cases):
 @pytest.mark.gpu
 @pytest.mark.parametrize("n", [16, 64])
 def test_gpu_accept_cases(bp, oracle, golden, monkeypatch, n):
-    """All 256 reference-emitted cases through the verify pipeline in one batch: lanes, quads and
-    pairs forced on every tick and the default tick forms, without prefix tables and with the
+    """All 256 reference-emitted cases through the verify pipeline in one batch: lanes, quads,
+    pairs and 16-lane rows forced on every tick and the default tick forms, without prefix tables and with the
     bench's K = 22 tables — every verdict and P, and the check point of every case that folds,
     equal the reference's.  The 32 crafted inner-product cases through the pipeline in
     inner-product mode (P given) and the four variants of one proof through the C ABI's
@@ -172,7 +172,7 @@ def test_gpu_accept_cases(bp, oracle, golden, monkeypatch, n):
     batch = bp.RangeProofBatch.from_numpy(n, arrays, dev)
     try:
         for tables in (False, True):
-            for q in (None, "0", "1", "2"):
+            for q in (None, "0", "1", "2", "3"):
                 if q is None:
                     monkeypatch.delenv("HIPBP_QUAD", raising=False)
                 else:

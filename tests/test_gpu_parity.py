@@ -1219,7 +1219,8 @@ def _sample_vs_oracle(oracle, n, B, arrays, ok, P, G, H, g, h, step=5):
                                                (1, 3, 1, 0, 1), (64, 1, 1, 0, 1)])
 def test_pipeline_quad_ticks_same_bits(bp, oracle, monkeypatch, n, B, mode, K, pushes):
     """The drain-tick forms — k_terms<4> (every scalar multiplication on a lane quad, sm_quad, the
-    chains too) and k_terms<2> (lane pairs, sm_pair) — forced on every tick (HIPBP_QUAD=1 / 2) give
+    chains too), k_terms<2> (lane pairs, sm_pair) and k_terms<16> (16-lane rows, sm_row, the chains
+    on quads) — forced on every tick (HIPBP_QUAD=1 / 2 / 3) give
     bit-identical verdicts, P, check points, mode-2 flags and polynomial sides to the lane form
     forced everywhere (HIPBP_QUAD=0): every region kind, with and without prefix tables, batches in
     flight together; a sample equals the oracle."""
@@ -1238,7 +1239,7 @@ def test_pipeline_quad_ticks_same_bits(bp, oracle, monkeypatch, n, B, mode, K, p
     import torch
     Pg = torch.from_numpy(oracle.base_points(B, 9).view(np.int64)).to("cuda:0")
     outs = []
-    for q in ("0", "1", "2"):   # lanes, quads, pairs on every tick
+    for q in ("0", "1", "2", "3"):   # lanes, quads, pairs, 16-lane rows on every tick
         monkeypatch.setenv("HIPBP_QUAD", q)
         outs.append(_pipeline_outputs(bp, n, B, mode, arrays, G, H, g, h, Pg, bits=K, pushes=pushes))
     for other in outs[1:]:
@@ -1248,6 +1249,79 @@ def test_pipeline_quad_ticks_same_bits(bp, oracle, monkeypatch, n, B, mode, K, p
     if mode == 1:
         o = outs[1][-1]
         _sample_vs_oracle(oracle, n, B, arrays, o[0].numpy().astype(bool), o[1].numpy().view(np.uint64), G, H, g, h)
+
+
+@pytest.mark.parametrize("n,B,mode,K,pushes,q", [(64, 70, 1, 12, 3, None), (16, 130, 1, 0, 2, None),
+                                                  (64, 9, 2, 5, 2, None), (16, 6, 2, 0, 1, "1"),
+                                                  (64, 40, 1, 0, 2, "2"), (4, 5, 1, 3, 1, None),
+                                                  (1, 3, 1, 0, 1, None), (64, 1, 1, 9, 1, "1")])
+def test_pipeline_deferred_msm_same_bits(bp, oracle, monkeypatch, n, B, mode, K, pushes, q):
+    """Split stage 0 (hipbp_pipeline_defer_msm: the MSM terms, t*h and c*Q in one launch on the
+    pipeline's bulk stream, the lane trees waiting for it at stage FIN - 1) gives the unsplit
+    pipeline's verdicts, P, check points, mode-2 flags and polynomial sides bit for bit: batches in
+    flight together, with and without prefix tables, each tick form; a sample equals the oracle."""
+    from cudabulletproof_amd import synth
+    import torch
+    G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+    g, h = oracle.gh()
+    arrays = synth.proofs(B, n, seed=1300 + n + B)
+    rng = np.random.default_rng(B + n)
+    arrays["taux"] = rand_fe(rng, B, top=False)
+    arrays["mu"] = rand_fe(rng, B, top=False)
+    arrays["t"][0] = 0
+    arrays["a"][:, 0] = arrays["t"]
+    arrays["c"][:] = arrays["t"]
+    if q is not None:
+        monkeypatch.setenv("HIPBP_QUAD", q)
+    monkeypatch.delenv("HIPBP_DEFER_MSM", raising=False)
+    want = _pipeline_outputs(bp, n, B, mode, arrays, G, H, g, h, None, bits=K, pushes=pushes)
+    monkeypatch.setenv("HIPBP_DEFER_MSM", "1")
+    got = _pipeline_outputs(bp, n, B, mode, arrays, G, H, g, h, None, bits=K, pushes=pushes)
+    for oa, ob in zip(want, got):
+        for a, b in zip(oa, ob):
+            assert torch.equal(a, b)
+    if mode == 1:
+        o = got[-1]
+        _sample_vs_oracle(oracle, n, B, arrays, o[0].numpy().astype(bool), o[1].numpy().view(np.uint64), G, H, g, h,
+                          step=7)
+
+
+def test_pipeline_defer_msm_api(bp, oracle):
+    """The C-ABI switch: refused where the split does not apply (inner-product mode; n above the
+    lane-tree limit), accepted in range mode, and a batch pushed with it verifies as without."""
+    import torch
+    from cudabulletproof_amd import synth
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    for n, mode, ok in ((64, 1, True), (64, 0, False), (128, 1, False), (16, 2, True)):
+        G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+        g, h = oracle.gh()
+        pl = bp.VerifyPipeline(8, n, T(G), T(H), T(h), range_mode=mode, g=T(g))
+        if ok:
+            pl.defer_msm(True)
+            pl.defer_msm(False)
+            pl.defer_msm(True)
+        else:
+            with pytest.raises(bp.BulletproofError):
+                pl.defer_msm(True)
+        pl.close()
+    n = 64
+    G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+    g, h = oracle.gh()
+    arrays = synth.proofs(8, n, seed=77)
+    batch = bp.RangeProofBatch.from_numpy(n, arrays, dev)
+    outs = []
+    for d in (False, True):
+        pl = bp.VerifyPipeline(8, n, T(G), T(H), T(h))
+        pl.defer_msm(d)
+        ok = torch.zeros(8, dtype=torch.uint8, device=dev)
+        P = torch.zeros(8, 16, dtype=torch.int64, device=dev)
+        pl.push(batch, ok, P)
+        pl.flush()
+        torch.cuda.synchronize()
+        pl.close()
+        outs.append((ok.cpu(), P.cpu()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
 
 @pytest.mark.parametrize("n,B,lt", [(512, 3, "1024"), (512, 3, "512"), (256, 4, "4096"), (64, 5, "0")])

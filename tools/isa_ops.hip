@@ -57,3 +57,7 @@ extern "C" __global__ void p_quad_dbl_of(fe* o, const fe* p) {
     const fe x = p[threadIdx.x];
     o[threadIdx.x] = quad_of_next(ge_quad_of_step<true>(x, x));
 }
+extern "C" __global__ void p_row_step_of(fe* o, const fe* p, const fe* qs, const int* u) {
+    const fe x = p[threadIdx.x];
+    o[threadIdx.x] = row_of_next(ge_row_of_step(x, fe_sel(u[threadIdx.x] != 0, qs[threadIdx.x], x)));
+}
