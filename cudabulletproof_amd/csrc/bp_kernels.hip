@@ -358,7 +358,7 @@ struct SmJob {
 
 // Lane and item indices of a tick are 32-bit (the host keeps a launch below 2^32 lanes) and n
 // is a power of two: index arithmetic is shifts and masks, no 64-bit division sequences.
-__device__ __forceinline__ int log2n(int n) { return __ffs(n) - 1; }
+// (log2n: bp_kernels.h)
 
 __device__ __forceinline__ void fold_job(const BatchView& bv, const VerifyWs& ws, int r, uint32_t p, uint32_t k,
                                          const ge* __restrict__ G, const ge* __restrict__ H, SmJob& jb) {
@@ -377,39 +377,7 @@ __device__ __forceinline__ void fold_job(const BatchView& bv, const VerifyWs& ws
     jb.dev_norm = 0;
 }
 
-// Per-lane class c item j -> stage0_task's item index (perm0 holds, per class range, the
-// items of that class in chain-length order: perm0[pl_base(c) + j]).
-__device__ __forceinline__ uint32_t stage0_class_item(const SlotDev& sd, int c, uint32_t j) {
-    const uint32_t B = (uint32_t)sd.bv.B;
-    const int n = sd.bv.n, ln = log2n(n);
-    const uint32_t nA = sd.range_mode ? B << (ln + 1) : 0, nB = sd.bv.L_len > 0 ? B << (ln + 1) : 0;
-    if (c == 0) return n >= 64 ? ((j >> ln) << (ln + 1)) + n + (j & (n - 1)) : j;
-    if (c == 1) return nA + j;
-    if (c == 2) return nA + nB + j;
-    return nA + nB + 2 * B + j;
-}
-
-// Stage-0 lane -> stage0_task item, or SIZE_MAX for a padding lane (stage0_lanes; sel: the
-// part of a split stage 0 the region runs, Stage0Sel).
-__device__ __forceinline__ uint32_t stage0_item(const SlotDev& sd, uint32_t l, int sel = S0_ALL) {
-    const uint32_t B = (uint32_t)sd.bv.B;
-    const int n = sd.bv.n, ln = log2n(n);
-    const Stage0Lanes z = stage0_lanes(B, n, sd.bv.L_len, sd.range_mode, sel);
-    if (l < (uint32_t)z.U) {
-        const uint32_t nG = (sd.range_mode && sel != S0_CRIT) ? B << ln : 0;
-        if (l < nG) return ((l >> ln) << (ln + 1)) + (l & (n - 1));   // <sG,G> segment of proof l / n
-        return (sd.range_mode ? B << (ln + 1) : 0) + (l - nG);
-    }
-    const Stage0Lanes za = sel == S0_ALL ? z : stage0_lanes(B, n, sd.bv.L_len, sd.range_mode);
-    int c = 0;
-    uint32_t base = 0;   // class c's offset in perm0 (the S0_ALL class sizes)
-#pragma unroll
-    for (int k = 1; k < 4; k++)
-        if (l >= (uint32_t)z.off[k]) { c = k; base += (uint32_t)za.size[k - 1]; }
-    const uint32_t j = l - (uint32_t)z.off[c];
-    if (j >= (uint32_t)z.size[c]) return UINT32_MAX;
-    return stage0_class_item(sd, c, sd.perm0 ? sd.perm0[base + j] : j);
-}
+// (stage0_class_item / stage0_item: bp_kernels.h, host-checked by tests/host_lanes_check.hip)
 
 // Stage 0: every scalar multiplication that depends only on the proof.  Item index space
 // (lanes reach it through stage0_item's class layout):
