@@ -80,6 +80,9 @@ def parse():
     ap.add_argument("--shard-batch", type=int, default=0,
                     help="configs[4]: proofs per pipeline push (0: auto from the rank's shard size)")
     ap.add_argument("--no-shard", action="store_true")
+    ap.add_argument("--shard-defer", type=int, default=0,
+                    help="configs[4]: split stage 0 in the shard's pipelines (hipbp_pipeline_defer_msm: the MSM "
+                         "terms beside the fold rounds, so the drain overlaps them); same bits")
     ap.add_argument("--host-count", type=int, default=32768, help="proofs per host-struct API call")
     ap.add_argument("--no-host", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip the headline self-check (verify_check)")
@@ -840,6 +843,10 @@ def shard_leg(args, dev, world, rank, pipes, gens, G, H, g, h, streams=None):
             for pp in own:
                 pp.use_gens(gens)
         pipes = own
+    defer = bool(args.shard_defer) and n <= 64   # (the split needs the lane trees: n <= 64)
+    for pp in pipes:   # the split stage 0 for the shard's batches (the headline pipelines get it back off)
+        pp.defer_msm(defer)
+
     def rows(j0, m):   # proofs [j0, j0 + m) of the global set: proof j is tile (j // B) % 4, row j % B
         parts, j = [], j0
         while j < j0 + m:
@@ -891,10 +898,14 @@ def shard_leg(args, dev, world, rank, pipes, gens, G, H, g, h, streams=None):
         times = [float(x) for x in t.tolist()]
     dt = statistics.median(times)
     import hashlib as _h
+    if defer:
+        for pp in pipes:
+            pp.defer_msm(False)
     for pp in own:
         pp.close()
     return {"metric": "2^16-proof 64-bit range-proof batch verify (BASELINE configs[4])", "value": total / dt,
-            "push_batch": Bs, "passes_timed": len(times), "value_min": total / max(times),
+            "push_batch": Bs, "defer_msm": defer, "passes_timed": len(times),
+            "value_min": total / max(times),
             "value_max": total / min(times), "same_verdicts_every_pass": len(digests) == 1,
             "unit": "verifies/s", "proofs": total, "n_gpus": world, "scaling": "strong", "ms": dt * 1e3,
             "passes": int(passes.item()), "verdicts_sha256": _h.sha256(allv.cpu().numpy().tobytes()).hexdigest()[:16],

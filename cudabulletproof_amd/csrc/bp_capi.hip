@@ -311,7 +311,7 @@ struct Gens {
 // point operation from ~1700 to ~750 for 4x the lanes, pairs to ~1140 for 2x: with both pipelines'
 // drains together, a 65,536-item tick is fastest on lanes, 32,768 on pairs, 16,384 on quads
 // (configs[4] shard: 173.8 K verifies/s vs 172.1 K with the round-3 bounds 49,152 / 98,304).
-constexpr unsigned long long ROW_MAX_ITEMS = 2048;   // 16-lane rows (sm_row) up to this many items
+constexpr unsigned long long ROW_MAX_ITEMS = 0;   // 16-lane rows (sm_row) up to this many items (0: off)
 constexpr unsigned long long QUAD_MAX_ITEMS = 16384;
 constexpr unsigned long long PAIR_MAX_ITEMS = 32768;
 
@@ -1166,8 +1166,8 @@ static int prove_run(const hipbp_prove_input* in, const ge25519* G, const ge2551
     // holds every VGPR, and at equal priority the tail's blocks only got slots as that terms0
     // drained (r03q trace: chain0 stretched to ~40 ms).  At high priority each freed slot goes to
     // the tail first.  The caller's stream waits for the tail, so the call stays ordered on it.
-    // HIPBP_PROVE_TAIL_STREAM=0 keeps everything on the caller's stream (A/B).
-    static const bool tail_stream = !getenv("HIPBP_PROVE_TAIL_STREAM") || atoi(getenv("HIPBP_PROVE_TAIL_STREAM")) != 0;
+    // HIPBP_PROVE_TAIL_STREAM=1 turns it on (A/B; off by default).
+    static const bool tail_stream = getenv("HIPBP_PROVE_TAIL_STREAM") && atoi(getenv("HIPBP_PROVE_TAIL_STREAM")) != 0;
     hipStream_t ts = s;
     if (tail_stream) {
         if (!pb->tail) {
