@@ -311,7 +311,9 @@ struct Gens {
 // point operation from ~1700 to ~750 for 4x the lanes, pairs to ~1140 for 2x: with both pipelines'
 // drains together, a 65,536-item tick is fastest on lanes, 32,768 on pairs, 16,384 on quads
 // (configs[4] shard: 173.8 K verifies/s vs 172.1 K with the round-3 bounds 49,152 / 98,304).
-constexpr unsigned long long ROW_MAX_ITEMS = 0;   // 16-lane rows (sm_row) up to this many items (0: off)
+// 16-lane rows (sm_row) up to this many items: a one-proof call's ticks (r04b, one MI355X, warm
+// cuda_range_proof_verify: n = 16 4.9 -> 4.0 ms, n = 64 6.7 -> 5.5 ms)
+constexpr unsigned long long ROW_MAX_ITEMS = 2048;
 constexpr unsigned long long QUAD_MAX_ITEMS = 16384;
 constexpr unsigned long long PAIR_MAX_ITEMS = 32768;
 
