@@ -80,7 +80,7 @@ def parse():
     ap.add_argument("--shard-batch", type=int, default=0,
                     help="configs[4]: proofs per pipeline push (0: auto from the rank's shard size)")
     ap.add_argument("--no-shard", action="store_true")
-    ap.add_argument("--shard-defer", type=int, default=0,
+    ap.add_argument("--shard-defer", type=int, default=1,
                     help="configs[4]: split stage 0 in the shard's pipelines (hipbp_pipeline_defer_msm: the MSM "
                          "terms beside the fold rounds, so the drain overlaps them); same bits")
     ap.add_argument("--host-count", type=int, default=32768, help="proofs per host-struct API call")

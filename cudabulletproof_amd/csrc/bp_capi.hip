@@ -356,16 +356,13 @@ struct Pipeline {
     // regions at the start of the grid instead of the end).
     bool lane_tree = false, chains_first = false;
     // Split stage 0 ("deferred MSM terms", hipbp_pipeline_defer_msm / HIPBP_DEFER_MSM=1): a batch
-    // pushed with it on runs only fold round 0 (+ the polynomial terms) in its stage-0 tick; the
-    // MSM terms, t*h and c*Q (read only by the final assembly) go to ONE RK_MSMT launch on the bulk
-    // stream `sb`, issued right after the batch's challenge tick and lane sort, and the batch's
-    // lane-tree tick (moved to stage FIN - 1) waits for it.  The fold chain then reaches its
-    // latency-bound last rounds sooner, with the MSM work running beside them: for a finite batch
-    // (configs[4]'s shards) the drain overlaps bulk work.  Needs the lane trees (n <= 64).
+    // pushed with it on runs only fold round 0 (+ the polynomial terms) in its stage-0 tick; its
+    // MSM terms, t*h and c*Q (read only by the lane trees and the final assembly) run as RK_MSMT
+    // chunks inside its fold-round ticks (stages 2 .. max(2, L - 1)), whose items shrink round by
+    // round, and the lane trees move to the stage after the last chunk.  For a finite batch
+    // (configs[4]'s shards) the rounds that would run half empty before the latency-bound last
+    // ticks carry the MSM work instead.  Needs the lane trees (n <= 64) and L >= 2.
     bool defer_msm = false;
-    hipStream_t sb = nullptr;
-    hipEvent_t ev_go = nullptr;
-    std::vector<hipEvent_t> ev_bulk;   // per slot: its RK_MSMT launch finished
     // drain-tick forms (push): HIPBP_QUAD forces lanes (0) / quads (1) / pairs (2) on every tick
     // (-1: by size), HIPBP_QUAD_MAX_ITEMS / HIPBP_PAIR_MAX_ITEMS move the size bounds
     int quad_force = -1;
@@ -440,11 +437,6 @@ struct Pipeline {
         if (sort_s) (void)hipStreamDestroy(sort_s);
         if (ev_tick) (void)hipEventDestroy(ev_tick);
         if (ev_sorted) (void)hipEventDestroy(ev_sorted);
-        if (sb) (void)hipStreamSynchronize(sb);
-        if (sb) (void)hipStreamDestroy(sb);
-        if (ev_go) (void)hipEventDestroy(ev_go);
-        for (auto ev : ev_bulk)
-            if (ev) (void)hipEventDestroy(ev);
         if (sort_bins.p) (void)hipFree(sort_bins.p);
         if (sort_offs.p) (void)hipFree(sort_offs.p);
         if (ptab.p) (void)hipFree(ptab.p);
@@ -503,19 +495,17 @@ struct Pipeline {
         for (auto& sl : slots) if (sl.active) return true;
         return false;
     }
-    bool defer_ok() const { return range_mode != 0 && lane_tree; }
-    hipError_t ensure_bulk() {
-        if (sb) return hipSuccess;
-        hipError_t r;
-        if ((r = hipStreamCreateWithFlags(&sb, hipStreamNonBlocking)) != hipSuccess) return r;
-        if ((r = hipEventCreateWithFlags(&ev_go, hipEventDisableTiming)) != hipSuccess) return r;
-        ev_bulk.assign(D, nullptr);
-        for (auto& ev : ev_bulk)
-            if ((r = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return r;
-        return hipSuccess;
+    bool defer_ok() const { return range_mode != 0 && lane_tree && Lr >= 2; }
+    // a split batch's MSM-term chunks: stages 2 .. msm_last(L), equal wave-aligned lane ranges
+    static int msm_last(int L) { return L - 1 > 2 ? L - 1 : 2; }
+    void msm_chunk(unsigned long long total, int L, int st, unsigned long long& lo, unsigned long long& hi) const {
+        const int m = msm_last(L) - 1, k = st - 2;   // m chunks, this is chunk k
+        lo = (total * (unsigned long long)k / m) & ~63ull;
+        hi = k + 1 == m ? total : (total * (unsigned long long)(k + 1) / m) & ~63ull;
     }
-    // the stage of a batch's lane-tree region (RK_LTREE)
-    int ltree_stage(const Slot& sl, const Stages& g) const { return sl.dev.defer ? g.fin - 1 : std::min(3, g.fin - 1); }
+    int ltree_stage(const Slot& sl, const Stages& g) const {
+        return sl.dev.defer ? msm_last(sl.dev.bv.L_len) + 1 : std::min(3, g.fin - 1);
+    }
     hipError_t carve(Slot& sl, size_t B, size_t Lb) {
         hipError_t r;
         size_t Lc = Lb ? Lb : 1;
@@ -566,8 +556,7 @@ struct Pipeline {
             nw.dev.lane_tree = lane_tree ? 1 : 0;
             nw.dev.ptab = pbits ? tables() : nullptr;
             nw.dev.pbits = pbits;
-            nw.dev.defer = (defer_msm && defer_ok()) ? 1 : 0;
-            if (nw.dev.defer) BP_RET_ON(ensure_bulk());
+            nw.dev.defer = (defer_msm && defer_ok() && (int)b->L_len >= 2) ? 1 : 0;
             BP_RET_ON(plan_sort(nw, head));
             BP_RET_ON(hipEventSynchronize(nw.copied));   // staging slot free again
             host_dev[head] = nw.dev;
@@ -581,8 +570,6 @@ struct Pipeline {
         }
         bp::RegionList tr{};
         bool overflow = false;
-        int wait_bulk[32];   // slots whose RK_MSMT launch this tick's lane-tree region must wait for
-        int nwait = 0;
         auto add = [&overflow](bp::RegionList& rl, int kind, int slot, int r, unsigned long long items, unsigned align) {
             if (!items) return;
             if (rl.count == bp::MAX_REGIONS) { overflow = true; return; }
@@ -610,7 +597,6 @@ struct Pipeline {
                     // so a drain's last tick is the short P / check-point assembly alone
                     if (range_mode && lane_tree && st == ltree_stage(sl, g)) {
                         add(tr, bp::RK_LTREE, idx, 0, B, 64);
-                        if (sl.dev.defer && nwait < 32) wait_bulk[nwait++] = idx;
                     }
                     if (st == 2 && range_mode == 2) add(tr, bp::RK_POLY, idx, 0, B, 64);
                     if (st == 0) add(tr, bp::RK_PREP, idx, 0, range_mode ? 2 * B : B, 64);
@@ -620,6 +606,11 @@ struct Pipeline {
                             bp::stage0_lanes(B, n, L, range_mode, sl.dev.defer ? bp::S0_CRIT : bp::S0_ALL).total, 64);
                     }
                     if (st >= 2 && st <= L) add(tr, bp::RK_ROUND, idx, st - 1, B * 4 * (n >> st), 64);
+                    if (sl.dev.defer && st >= 2 && st <= msm_last(L)) {   // a chunk of the split stage 0
+                        unsigned long long lo, hi;
+                        msm_chunk(bp::stage0_lanes(B, n, L, range_mode, bp::S0_DEFER).total, L, st, lo, hi);
+                        add(tr, bp::RK_MSMT, idx, (int)lo, hi - lo, 64);
+                    }
                     if (st == g.ft) add(tr, bp::RK_FINAL_TERMS, idx, 0, B * 2, 64);
                     if (st == g.m3) add(tr, bp::RK_M3, idx, 0, B * 2, 64);
                 }
@@ -651,7 +642,6 @@ struct Pipeline {
             tr.total = tot;
         }
         if (tr.total >= (1ull << 32)) { g_err = "pipeline tick exceeds 2^32 lanes (batch too large for n)"; return HIPBP_ERR_ARG; }
-        for (int k = 0; k < nwait; k++) BP_RET_ON(hipStreamWaitEvent(s, ev_bulk[wait_bulk[k]], 0));
         if (tm) tm->mark(bp::KT_TERMS, false, s);
         bp::launch_terms(tr, slots_dev, G, H, g ? g : h, h, e->dtab, e->two_i, s, ql);
         if (tm) tm->mark(bp::KT_TERMS, true, s);
@@ -669,42 +659,12 @@ struct Pipeline {
                 BP_RET_ON(hipGetLastError());
             }
         }
-        if (has && nw.dev.defer) {
-            const int rc = launch_bulk(head);
-            if (rc != HIPBP_OK) return rc;
-        }
         for (auto& sl : slots) {
             if (!sl.active) continue;
             if (sl.stage == stages(sl.dev.bv.L_len).fin) sl.active = false;
             else sl.stage++;
         }
         head = (head + 1) % D;
-        return HIPBP_OK;
-    }
-    // The split stage 0's deferred part of the batch in slot idx (its challenges ran in the tick
-    // just enqueued on s, its lane order after it): ONE RK_MSMT launch on the bulk stream.
-    int launch_bulk(int idx) {
-        Slot& sl = slots[idx];
-        const unsigned long long B = sl.dev.bv.B;
-        bp::RegionList br{};
-        bp::Region& rg = br.reg[0];
-        br.count = 1;
-        rg.kind = bp::RK_MSMT;
-        rg.slot = idx;
-        rg.r = 0;
-        rg.begin = 0;
-        rg.items = bp::stage0_lanes(B, n, sl.dev.bv.L_len, range_mode, bp::S0_DEFER).total;
-        int ql = rg.items <= row_max ? 16 : rg.items <= quad_max ? 4 : rg.items <= pair_max ? 2 : 1;
-        if (quad_force >= 0) ql = quad_force;
-        rg.items *= ql;
-        br.total = (rg.items + 63) & ~63ull;
-        if (!rg.items) return HIPBP_OK;
-        if (br.total >= (1ull << 32)) { g_err = "pipeline bulk launch exceeds 2^32 lanes"; return HIPBP_ERR_ARG; }
-        BP_RET_ON(hipEventRecord(ev_go, s));
-        BP_RET_ON(hipStreamWaitEvent(sb, ev_go, 0));
-        bp::launch_terms(br, slots_dev, G, H, g ? g : h, h, e->dtab, e->two_i, sb, ql);
-        BP_RET_ON(hipGetLastError());
-        BP_RET_ON(hipEventRecord(ev_bulk[idx], sb));
         return HIPBP_OK;
     }
     int flush() {
@@ -1291,7 +1251,7 @@ int hipbp_pipeline_defer_msm(void* handle, int on) {
     Pipeline* pl = (Pipeline*)handle;
     if (!pl) { g_err = "null pipeline"; return HIPBP_ERR_ARG; }
     if (on && !pl->defer_ok()) {
-        g_err = "defer_msm: needs cuda_range_proof_verify / range_proof_verify semantics and n <= the lane-tree limit";
+        g_err = "defer_msm: needs cuda_range_proof_verify / range_proof_verify semantics and 4 <= n <= the lane-tree limit";
         return HIPBP_ERR_ARG;
     }
     std::lock_guard<std::mutex> lk(pl->e->mu);

@@ -81,7 +81,7 @@ struct SlotDev {
     int pbits;
     // 1: stage 0 is split (Pipeline "deferred MSM terms"): RK_STAGE0 runs only the items later
     // stages wait for (fold round 0, mode-2 polynomial terms); the two MSMs' terms and t*h, c*Q,
-    // which only the final assembly reads, run as an RK_MSMT launch on the pipeline's bulk stream
+    // which only the lane trees and the final assembly read, run as RK_MSMT chunks in the fold ticks
     int defer;
 };
 
@@ -192,7 +192,7 @@ void launch_lane_sort(const LaneSortPlan& plan, unsigned* bins, unsigned* offs, 
 enum RegionKind { RK_STAGE0 = 0, RK_ROUND = 1, RK_FINAL_TERMS = 2, RK_FINAL = 4, RK_PREP = 5,
                   RK_TREE = 6, RK_POLY = 7, RK_M3 = 8,
                   RK_LTREE = 9 /* the n <= LANE_TREE_MAX MSM trees, one lane (quad) per proof, into msm_part */,
-                  RK_MSMT = 10 /* split stage 0's deferred part (SlotDev::defer), on the bulk stream */ };
+                  RK_MSMT = 10 /* a chunk of split stage 0's deferred part (SlotDev::defer); Region::r = its first lane */ };
 struct Region {
     int kind;
     int slot;

@@ -845,7 +845,9 @@ __global__ BP_TERMS_BOUNDS void k_terms(RegionList rl, const SlotDev* __restrict
         if (QL == 4) li >>= 2;
         if (QL == 2) li >>= 1;
         if (rg.kind == RK_STAGE0 || rg.kind == RK_MSMT) {
-            const uint32_t it = stage0_item(sd, li, rg.kind == RK_MSMT ? S0_DEFER : sd.defer ? S0_CRIT : S0_ALL);
+            // RK_MSMT: a chunk of the split stage 0's second part, lanes from rg.r on
+            const uint32_t it = rg.kind == RK_MSMT ? stage0_item(sd, (uint32_t)rg.r + li, S0_DEFER)
+                                                   : stage0_item(sd, li, sd.defer ? S0_CRIT : S0_ALL);
             live = it != UINT32_MAX && stage0_job(sd, it, G, H, g, h, jb);
         } else if (rg.kind == RK_M3) {
             m3_job(sd, li, jb);

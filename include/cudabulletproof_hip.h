@@ -199,11 +199,11 @@ void hipbp_gens_destroy(void* gens);
 /* The pipeline reads its generators and prefix tables from `gens` (same n; the pipeline must be
  * idle; the set must outlive the pipeline's use of it).  Results keep their bits. */
 int hipbp_pipeline_use_gens(void* pipeline, void* gens);
-/* Split stage 0 for the batches pushed from now on (on = 1; range_mode 1 or 2, n <= 64): a
+/* Split stage 0 for the batches pushed from now on (on = 1; range_mode 1 or 2, 4 <= n <= 64): a
  * batch's stage-0 tick runs only fold round 0 (and the range_proof_verify polynomial terms); its
- * two MSMs' terms, t*h and c*Q, which only the final assembly reads, run as one launch on an
- * internal stream right after the batch's challenge tick, beside the fold rounds.  A finite batch
- * then overlaps its latency-bound last ticks with that work.  Same bits either way. */
+ * two MSMs' terms, t*h and c*Q, which only the final assembly reads, run in chunks inside its
+ * fold-round ticks, whose own items shrink round by round.  A finite batch then fills the rounds
+ * before its latency-bound last ticks.  Same bits either way. */
 int hipbp_pipeline_defer_msm(void* pipeline, int on);
 void hipbp_pipeline_destroy(void* pipeline);
 
