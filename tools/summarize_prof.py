@@ -24,10 +24,10 @@ def short(name):
     name = name.split("(")[0].replace("bp::", "")
     if name.startswith("void "):
         name = name[5:]
-    # k_terms<1>: the pipeline tick (one lane per item); k_terms<2> / <4>: its drain-tick forms on a
-    # lane pair / quad
+    # k_terms<1>: the pipeline tick (one lane per item); k_terms<2> / <4> / <16>: its drain-tick forms
+    # on a lane pair / quad / 16-lane row
     return (name.replace("k_terms<1>", "k_terms").replace("k_terms<2>", "k_terms_pair")
-            .replace("k_terms<4>", "k_terms_quad"))
+            .replace("k_terms<4>", "k_terms_quad").replace("k_terms<16>", "k_terms_row"))
 
 
 def load_counters(d):
