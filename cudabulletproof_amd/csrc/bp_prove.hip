@@ -426,26 +426,30 @@ __global__ __launch_bounds__(TPB, 3) void k_prove_rterms(ProveIn in, ProveWs ws,
     const int n = in.n;
     const size_t per = 4 * (size_t)np + 2;
     uint32_t id;
-    if (!next_item(ws, gid(), id)) return;
-    size_t p = id / per;
-    int k = (int)(id % per);
-    fe s;
-    ge P;
-    int base;
-    const bool msm = k < 4 * np;
-    if (msm) {
-        int blk = k / np, j = k % np;
-        P = blk == 0 ? G[np + j] : blk == 1 ? H[j] : blk == 2 ? G[j] : H[np + j];
-        base = blk == 0 ? np + j : blk == 1 ? n + j : blk == 2 ? j : n + np + j;
-        s = ws.iscal[p * 2 * n + k];
-    } else {
-        P = *Q;
-        base = 2 * n;   // Q = h
-        s = ws.csc[p * 2 + (k - 4 * np)];
+    // grid-stride over the queued items: the lists hold ~2 non-zero items per proof when the prover
+    // takes its l = [t, 0..], r = [1, 0..] fallback, so a grid of B (4n' + 2) lanes would be almost
+    // all empty waves, and under another stream's running terms0 every one of them waits for a slot
+    for (size_t i = gid(); next_item(ws, i, id); i += (size_t)gridDim.x * TPB) {
+        size_t p = id / per;
+        int k = (int)(id % per);
+        fe s;
+        ge P;
+        int base;
+        const bool msm = k < 4 * np;
+        if (msm) {
+            int blk = k / np, j = k % np;
+            P = blk == 0 ? G[np + j] : blk == 1 ? H[j] : blk == 2 ? G[j] : H[np + j];
+            base = blk == 0 ? np + j : blk == 1 ? n + j : blk == 2 ? j : n + np + j;
+            s = ws.iscal[p * 2 * n + k];
+        } else {
+            P = *Q;
+            base = 2 * n;   // Q = h
+            s = ws.csc[p * 2 + (k - 4 * np)];
+        }
+        const ge* pt = prow(ws, base);
+        ge r = scalarmult<true>(s, P, &qs[threadIdx.x], dtab, pt, pt ? ws.pbits : 0);   // one call site (k_prove_terms0)
+        ws.iterm[p * (2 * (size_t)n + 2) + k] = msm ? ge_norm_host(r) : r;
     }
-    const ge* pt = prow(ws, base);
-    ge r = scalarmult<true>(s, P, &qs[threadIdx.x], dtab, pt, pt ? ws.pbits : 0);   // one call site (k_prove_terms0)
-    ws.iterm[p * (2 * (size_t)n + 2) + k] = msm ? ge_norm_host(r) : r;
 }
 
 __global__ __launch_bounds__(TPB) void k_prove_round(ProveIn in, ProveWs ws, ProveOut out, int r,
@@ -551,7 +555,10 @@ void launch_prove(int stage, int r, const ProveIn& in, const ProveWs& ws, const 
             break;
         case PS_RTERMS: {
             int np = n >> (r + 1);
-            k_prove_rterms<<<nblk(B * (4 * (size_t)np + 2)), TPB, 0, s>>>(in, ws, np, G, H, h, dtab);
+            // at most RTERMS_BLOCKS blocks (4 waves per SIMD over the GPU), grid-stride over the items
+            constexpr unsigned RTERMS_BLOCKS = 1024;
+            const unsigned nb = nblk(B * (4 * (size_t)np + 2));
+            k_prove_rterms<<<nb < RTERMS_BLOCKS ? nb : RTERMS_BLOCKS, TPB, 0, s>>>(in, ws, np, G, H, h, dtab);
             break;
         }
         case PS_RCHAIN: {
