@@ -535,14 +535,14 @@ __device__ __forceinline__ ge ge_op16(const ge& p, const ge& q) {
     return ge{fe_row_bcast<0>(r3), fe_row_bcast<4>(r3), fe_row_bcast<8>(r3), fe_row_bcast<12>(r3)};
 }
 
-#ifndef BP_HORNER16
-#define BP_HORNER16 1
+#ifndef BP_HORNER16   // 3: rows in operand form (default, r04j: one MSM 2.26/2.30 vs 2.33/2.34 ms with 1)
+#define BP_HORNER16 3
 #endif
 // Horner over windows w_top .. w_end (descending): T = Tin ? *Tin : S_{w_top} (then from
 // w_top - 1); per window c doublings, then + S_w.  A block (one wave) per MSM of the batch; each
-// 16-lane row of the wave runs the chain (ge_op16: a product per lane quad, 4 identical rows;
-// BP_HORNER16=0: ge_op_quad, 16 identical quads); lane 0 stores.  Split at any window, two calls
-// give the single chain's bits.
+// 16-lane row of the wave runs the chain (BP_HORNER16=3: the operand-form row step of sm_row;
+// 1: ge_op16, a product per lane quad on replicated points; 2: operand-form quads; 0: ge_op_quad,
+// 16 identical quads); lane 0 stores.  Split at any window, two calls give the single chain's bits.
 __global__ __launch_bounds__(64) void k_pip_horner(const ge* __restrict__ Sw, int W, int w_top, int w_end, int c,
                                                   const ge* __restrict__ Tin, ge* out) {
     Sw += (size_t)blockIdx.x * W;   // block m: MSM m of the batch
@@ -555,7 +555,21 @@ __global__ __launch_bounds__(64) void k_pip_horner(const ge* __restrict__ Sw, in
         T = Sw[w_top];
         w--;
     }
-    if (BP_HORNER16 == 2) {   // lane quads in operand form (ge25519_quad.h), squares for the doublings
+    if (BP_HORNER16 == 3) {   // 16-lane rows in operand form (ge25519_quad.h sm_row's step), 4 identical rows
+        fe o = row_of_form(T), r3;
+        bool pend = false;       // r3 holds the last operation's stage-3 products, o is stale
+        for (; w >= w_end; w--) {
+            for (int d = 0; d < c; d++) {
+                if (pend) o = row_of_next(r3);
+                r3 = ge_row_of_step(o, o);
+                pend = true;
+            }
+            if (pend) o = row_of_next(r3);
+            r3 = ge_row_of_step(o, row_of_form(Sw[w]));
+            pend = true;
+        }
+        if (pend) T = row_of_point(r3);
+    } else if (BP_HORNER16 == 2) {   // lane quads in operand form (ge25519_quad.h), squares for the doublings
         fe o = quad_of_form(T), r3;
         bool pend = false;       // r3 holds the last operation's stage-3 products, o is stale
         for (; w >= w_end; w--) {
