@@ -407,6 +407,14 @@ struct Pipeline {
         pair_max = pm ? strtoull(pm, nullptr, 10) : PAIR_MAX_ITEMS;
         const char* dm = getenv("HIPBP_DEFER_MSM");
         defer_msm = dm && atoi(dm) != 0;
+        if (const char* sp = getenv("HIPBP_DEFER_SPAN")) {
+            int a = 2, b = 1, c = 0;
+            if (sscanf(sp, "%d:%d:%d", &a, &b, &c) >= 1 && a >= 2) {
+                defer_first = a;
+                defer_last_off = b < 0 ? 0 : b;
+                defer_weight = c != 0;
+            }
+        }
         Lr = log2i((size_t)n);
         D = stages(Lr).fin + 1;   // batches with fewer rounds finish earlier
         slots.resize(D);
@@ -496,12 +504,21 @@ struct Pipeline {
         return false;
     }
     bool defer_ok() const { return range_mode != 0 && lane_tree && Lr >= 2; }
-    // a split batch's MSM-term chunks: stages 2 .. msm_last(L), equal wave-aligned lane ranges
-    static int msm_last(int L) { return L - 1 > 2 ? L - 1 : 2; }
+    // a split batch's MSM-term chunks: stages defer_first .. msm_last(L), wave-aligned lane ranges
+    // (HIPBP_DEFER_SPAN = "first:last_off:weight" for A/B runs: chunks at stages first .. L - last_off
+    // (at least first), weight 0 equal chunks, 1 chunk k weighted 2^k: later, emptier rounds get more)
+    int defer_first = 2, defer_last_off = 1, defer_weight = 0;
+    int msm_last(int L) const { return L - defer_last_off > defer_first ? L - defer_last_off : defer_first; }
     void msm_chunk(unsigned long long total, int L, int st, unsigned long long& lo, unsigned long long& hi) const {
-        const int m = msm_last(L) - 1, k = st - 2;   // m chunks, this is chunk k
-        lo = (total * (unsigned long long)k / m) & ~63ull;
-        hi = k + 1 == m ? total : (total * (unsigned long long)(k + 1) / m) & ~63ull;
+        const int m = msm_last(L) - defer_first + 1, k = st - defer_first;   // m chunks, this is chunk k
+        auto cut = [&](int j) -> unsigned long long {   // lanes before chunk j
+            if (j >= m) return total;
+            const unsigned long long num = defer_weight ? (1ull << j) - 1 : (unsigned long long)j;
+            const unsigned long long den = defer_weight ? (1ull << m) - 1 : (unsigned long long)m;
+            return (total / 64 * num / den) * 64;
+        };
+        lo = cut(k);
+        hi = cut(k + 1);
     }
     int ltree_stage(const Slot& sl, const Stages& g) const {
         return sl.dev.defer ? msm_last(sl.dev.bv.L_len) + 1 : std::min(3, g.fin - 1);
@@ -556,7 +573,9 @@ struct Pipeline {
             nw.dev.lane_tree = lane_tree ? 1 : 0;
             nw.dev.ptab = pbits ? tables() : nullptr;
             nw.dev.pbits = pbits;
-            nw.dev.defer = (defer_msm && defer_ok() && (int)b->L_len >= 2) ? 1 : 0;
+            // (the lane trees must land at least one tick before the final assembly)
+            nw.dev.defer = (defer_msm && defer_ok() && (int)b->L_len >= 2 &&
+                            msm_last((int)b->L_len) + 1 < stages((int)b->L_len).fin) ? 1 : 0;
             BP_RET_ON(plan_sort(nw, head));
             BP_RET_ON(hipEventSynchronize(nw.copied));   // staging slot free again
             host_dev[head] = nw.dev;
@@ -606,7 +625,7 @@ struct Pipeline {
                             bp::stage0_lanes(B, n, L, range_mode, sl.dev.defer ? bp::S0_CRIT : bp::S0_ALL).total, 64);
                     }
                     if (st >= 2 && st <= L) add(tr, bp::RK_ROUND, idx, st - 1, B * 4 * (n >> st), 64);
-                    if (sl.dev.defer && st >= 2 && st <= msm_last(L)) {   // a chunk of the split stage 0
+                    if (sl.dev.defer && st >= defer_first && st <= msm_last(L)) {   // a chunk of the split stage 0
                         unsigned long long lo, hi;
                         msm_chunk(bp::stage0_lanes(B, n, L, range_mode, bp::S0_DEFER).total, L, st, lo, hi);
                         add(tr, bp::RK_MSMT, idx, (int)lo, hi - lo, 64);
