@@ -287,7 +287,8 @@ def cuda_range_proof_verify(proof, V, n, G, H, g, h):
 def batch_range_proof_verify_host(proofs, V, n, G, H, g, h, num_gpus=0):
     """hipbp_batch_range_proof_verify_host: cuda_range_proof_verify over a list of proofs (the
     dicts cuda_range_proof_verify takes) packed as an array of the reference's RangeProof structs,
-    sharded over num_gpus devices (0: all).  Host arrays in, (count,) bool verdicts out."""
+    sharded over num_gpus devices (0: all) from the current device on.  Host arrays in, (count,) bool
+    verdicts out."""
     require_gpu()
     keep = []
     count = len(proofs)

@@ -1674,7 +1674,7 @@ int hipbp_batch_range_proof_verify_host(const RangeProof* proofs, const ge25519*
     if (ndev <= 0) { g_err = "no HIP device"; return HIPBP_ERR_DEVICE; }
     int ng = num_gpus <= 0 ? ndev : std::min(num_gpus, ndev);
     // HIPBP_HOST_SHARDS=k (tests, only when the caller leaves num_gpus <= 0): k shards (at most 64
-    // and at most one per proof), shard d on device d % ndev, so the multi-device split, its host
+    // and at most one per proof), shard d on device (current + d) % ndev, so the multi-device split, its host
     // threads and the verdict merge also run on a one-GPU box (threads of one device serialise on
     // its engine's mutex)
     if (num_gpus <= 0)
@@ -1709,8 +1709,8 @@ int hipbp_batch_range_proof_verify_host(const RangeProof* proofs, const ge25519*
         int rc = check_batch(&probe, 1);
         if (rc != HIPBP_OK) return rc;
     }
-    int dev0 = 0;
-    BP_RET_ON(hipGetDevice(&dev0));
+    int dev0 = 0;   // the caller's current device: shard d runs on device (dev0 + d) % ndev, so
+    BP_RET_ON(hipGetDevice(&dev0));   // num_gpus = 1 stays on it (one rank per GPU in a process group)
     const size_t M = main.size();
     std::vector<int> rcs(ng, HIPBP_OK);
     std::vector<std::string> errs(ng);
@@ -1719,7 +1719,7 @@ int hipbp_batch_range_proof_verify_host(const RangeProof* proofs, const ge25519*
         const size_t lo = M * d / ng, hi = M * (d + 1) / ng;
         if (hi == lo) continue;
         workers.emplace_back([&, d, lo, hi]() {
-            rcs[d] = host_shard(d % ndev, proofs, V, main.data() + lo, hi - lo, abl, Lr, n, G, H, h, ok);
+            rcs[d] = host_shard((dev0 + d) % ndev, proofs, V, main.data() + lo, hi - lo, abl, Lr, n, G, H, h, ok);
             if (rcs[d] != HIPBP_OK) errs[d] = g_err;   // g_err is per thread
         });
     }

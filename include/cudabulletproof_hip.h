@@ -133,7 +133,8 @@ int hipbp_device_count(void);
  * structs: ok[i] = cuda_range_proof_verify(&proofs[i], &V[i], n, G, H, g, h) for i < count, bit for
  * bit, with the reference's length check per proof (message on stderr, ok[i] = 0).  The proofs are
  * packed into the flat batch format, sharded in contiguous blocks over num_gpus devices (<= 0: all
- * visible), one host thread per device: 1024-proof chunks are packed into pinned staging, copied
+ * visible) starting at the calling thread's current device (shard d on device (current + d) mod the
+ * device count, so num_gpus = 1 stays on the current device), one host thread per device: 1024-proof chunks are packed into pinned staging, copied
  * and pushed as they are packed, alternating over two verify pipelines on two streams; one D2H of
  * the verdicts; no data-path exchange between devices.  Proofs whose a/b length or round
  * count differs from the first valid proof's go through the single-proof path.  Host pointers,
