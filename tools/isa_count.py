@@ -4,6 +4,7 @@ the field asm's exact forms for rare edges are skipped).
   python tools/isa_count.py [extra hipcc flags]
 """
 import collections
+import re
 import os
 import subprocess
 import sys
@@ -37,6 +38,17 @@ def main():
     for name in [l.split(":")[0] for l in s.split("\n") if l.startswith("p_") and l.split(":")[0].isidentifier()]:
         body = s[s.index("\n" + name + ":"):]
         body = body[:body.index("s_endpgm")]
+        if name.startswith("p_sm_"):   # a loop kernel: the last backward branch's body (one iteration)
+            lines = body.split("\n")
+            labels = {l.split(":")[0]: i for i, l in enumerate(lines) if re.match(r"^\.LBB\d+_\d+:", l)}
+            span = None
+            for i, l in enumerate(lines):
+                m = re.search(r"s_(?:cbranch_\w+|branch)\s+(\.LBB\d+_\d+)", l)
+                if m and m.group(1) in labels and labels[m.group(1)] < i:
+                    span = (labels[m.group(1)], i)
+            if span:
+                body = "\n".join(lines[span[0]:span[1] + 1])
+                name += " (loop body)"
         # the field asm's exact forms for rare edges sit between "s_branch 4f" and the "4:" label:
         # count the common path only (what a wave executes unless a lane is on a rare edge)
         ins, skip = [], False

@@ -61,3 +61,10 @@ extern "C" __global__ void p_row_step_of(fe* o, const fe* p, const fe* qs, const
     const fe x = p[threadIdx.x];
     o[threadIdx.x] = row_of_next(ge_row_of_step(x, fe_sel(u[threadIdx.x] != 0, qs[threadIdx.x], x)));
 }
+// the whole per-lane scalar-mult loop (the k_terms<1> hot loop): tools/isa_count.py --loop prints
+// the instructions of its loop body (one unified step + the bit bookkeeping)
+extern "C" __global__ void p_sm_lane_zone(ge* o, const fe* s, const ge* p, const ge* dtab) {
+    __shared__ geq qs[256];
+    qs[threadIdx.x] = ge_prep(p[threadIdx.x]);
+    o[threadIdx.x] = sm_lane_loop<true, true>(s[threadIdx.x], &qs[threadIdx.x], dtab, nullptr, 0);
+}
