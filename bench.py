@@ -63,7 +63,9 @@ def parse():
                     help="configs[3]: fixed-base prefix tables of G/H for fold round 0 (0 = none)")
     ap.add_argument("--prove-batch", type=int, default=65536, help="proofs per generate_range_proof batch")
     ap.add_argument("--prove-steps", type=int, default=4)
-    ap.add_argument("--prove-streams", type=int, default=2, help="HIP streams prover batches rotate over")
+    ap.add_argument("--prove-streams", type=int, default=4,
+                    help="HIP streams prover batches rotate over (4: 466-468 K vs 460-465 K with 2, "
+                         "profiles/ab/r04n_prove_schedules.txt)")
     ap.add_argument("--no-prove", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
