@@ -108,10 +108,15 @@ def main():
     base = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     out_md = os.path.join(ROOT, "profiles", f"rocprof_{tag}_summary.md")
     stats = list(csv.DictReader(open(os.path.join(base, "trace", "run_kernel_stats.csv"))))
+    try:   # the prefix-table width the bench ran with (its line's config)
+        kbits = json.loads(open(os.path.join(base, "bench_trace.json")).read().strip().splitlines()[-1])[
+            "config"]["prefix_tables"]["bits"]
+    except (OSError, ValueError, KeyError, IndexError):
+        kbits = "?"
     lines = [f"# rocprofv3 summary — {tag}", "",
              "Command: `tools/profile.sh " + tag + "` on one MI355X "
              "(bench.py --steps 20 --warmup 5 --no-cpu --no-ipa --no-prove --no-shard --no-host --no-check --no-h2d "
-             "--msm-log2 $MSM_LOG2 under rocprofv3: the headline configuration — B = 1024, n = 64, K = 22 prefix "
+             f"--msm-log2 $MSM_LOG2 under rocprofv3: the headline configuration — B = 1024, n = 64, K = {kbits} prefix "
              "tables, two pipelines — otherwise defaults).", "",
              "## Kernel trace (`rocprofv3 --kernel-trace --stats`)", "",
              "| kernel | calls | avg ms | min ms | max ms | % time |", "|---|---|---|---|---|---|"]
