@@ -966,8 +966,9 @@ def prove_leg(args, dev, gens=None):
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)
     Gd, Hd, gd, hd = T(G), T(H), T(g), T(h)
     pi = {k: T(v) for k, v in synth.prove_inputs(B, n).items()}
-    # two streams: one batch's latency-bound stages (T terms, IPA rounds, chains) run under the
-    # other batch's term launches (each stream has its own prover workspace in the engine)
+    # batches rotate over --prove-streams streams (default 4): one batch's latency-bound stages (T
+    # terms, IPA rounds, chains) run under the other batches' term launches (each stream has its own
+    # prover workspace in the engine)
     # (different priorities: HIP maps streams onto at most GPU_MAX_HW_QUEUES hardware queues and two
     # same-priority streams created after the verify legs' streams can share one, which serializes them)
     lo, hi = torch.cuda.Stream.priority_range()
