@@ -37,6 +37,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+DEFAULT_PREFIX_BITS = 23       # --prefix-bits default (tests/test_gpu_fullsize.py runs the same width)
 FE_B, GE_B = 32, 128
 
 
@@ -77,7 +78,7 @@ def parse():
     ap.add_argument("--proofs", choices=["prover", "synthetic"], default="prover",
                     help="verify inputs: proofs made by the GPU prover from random 64-bit values (default) "
                          "or proof-shaped random data")
-    ap.add_argument("--prefix-bits", type=int, default=23,
+    ap.add_argument("--prefix-bits", type=int, default=DEFAULT_PREFIX_BITS,
                     help="fixed-base prefix tables of the generators (hipbp_pipeline_prefix_tables; "
                          "0 = off): one-time setup, same bits (23: 139.6 GB at n = 64; +0.4 %% over 22, "
                          "profiles/ab/r04t_prefix_bits.txt)")
@@ -848,9 +849,30 @@ def shard_leg(args, dev, world, rank, pipes, gens, G, H, g, h, streams=None):
             for pp in own:
                 pp.use_gens(gens)
         pipes = own
-    defer = bool(args.shard_defer) and n <= 64   # (the split needs the lane trees: n <= 64)
-    for pp in pipes:   # the split stage 0 for the shard's batches (the headline pipelines get it back off)
-        pp.defer_msm(defer)
+    defer = False
+    if args.shard_defer:   # the split stage 0 for the shard's batches, where the C ABI accepts it
+        try:
+            for pp in pipes:
+                pp.defer_msm(True)
+            defer = True
+        except bp.BulletproofError:   # (n < 4 or above the lane-tree limit: the unsplit pipeline)
+            for pp in pipes:
+                pp.defer_msm(False)
+    try:
+        return _shard_run(args, dev, world, B, n, total, lo, hi, tiles, pipes, Bs, defer)
+    finally:
+        if defer:   # the headline pipelines get it back off whatever happened
+            for pp in pipes:
+                pp.defer_msm(False)
+        for pp in own:
+            pp.close()
+
+
+def _shard_run(args, dev, world, B, n, total, lo, hi, tiles, pipes, Bs, defer):
+    import torch
+    import torch.distributed as dist
+    import cudabulletproof_amd as bp
+    from cudabulletproof_amd import shard
 
     def rows(j0, m):   # proofs [j0, j0 + m) of the global set: proof j is tile (j // B) % 4, row j % B
         parts, j = [], j0
@@ -903,11 +925,6 @@ def shard_leg(args, dev, world, rank, pipes, gens, G, H, g, h, streams=None):
         times = [float(x) for x in t.tolist()]
     dt = statistics.median(times)
     import hashlib as _h
-    if defer:
-        for pp in pipes:
-            pp.defer_msm(False)
-    for pp in own:
-        pp.close()
     return {"metric": "2^16-proof 64-bit range-proof batch verify (BASELINE configs[4])", "value": total / dt,
             "push_batch": Bs, "defer_msm": defer, "passes_timed": len(times),
             "value_min": total / max(times),
@@ -1024,6 +1041,30 @@ def rank_launch(args):
     return subprocess.call(cmd)
 
 
+def device_pci(dev):
+    import torch
+    pr = torch.cuda.get_device_properties(dev)
+    return f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+
+
+def require_distinct_devices(dev, world, rank):
+    """A measured (non-rehearsal) N-rank run must have its N ranks on N distinct devices over RCCL:
+    every rank's PCI address is gathered before any leg runs, and a world that does not satisfy it
+    exits 4 on every rank without a line (a rehearsal says so with --rehearse)."""
+    import torch.distributed as dist
+    pcis = [None] * world
+    dist.all_gather_object(pcis, device_pci(dev))
+    backend = dist.get_backend()
+    if backend == "nccl" and len(set(pcis)) == world:
+        return
+    if rank == 0:
+        print(f"bench.py: {world} ranks on {len(set(pcis))} distinct device(s) {sorted(set(pcis))} over {backend}: "
+              f"a measured N-rank run needs N distinct GPUs over RCCL ('nccl'); --rehearse for a one-GPU rehearsal",
+              file=sys.stderr)
+    dist.destroy_process_group()
+    sys.exit(4)
+
+
 def rank_info(dev, oks_batches):
     """This rank's identity and its headline result: device, PCI address, verdict digest of its
     own (rank-seeded, distinct) batches."""
@@ -1031,8 +1072,7 @@ def rank_info(dev, oks_batches):
     pr = torch.cuda.get_device_properties(dev)
     ok = torch.cat([o.flatten() for o in oks_batches]).cpu().numpy()
     return {"rank": int(os.environ.get("RANK", "0")), "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
-            "device": str(dev), "name": pr.name,
-            "pci": f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0",
+            "device": str(dev), "name": pr.name, "pci": device_pci(dev),
             "uuid": str(getattr(pr, "uuid", "")), "verdicts_sha256": hashlib.sha256(ok.tobytes()).hexdigest()[:16],
             "passes": int(ok.sum()), "proofs": int(ok.size)}
 
@@ -1070,6 +1110,8 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if world > 1 and not args.rehearse:
+        require_distinct_devices(dev, world, rank)
     bp.lib()
     bp.require_gpu()
 

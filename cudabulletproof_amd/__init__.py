@@ -614,7 +614,10 @@ class VerifyPipeline:
 
     def defer_msm(self, on=True):
         """hipbp_pipeline_defer_msm: split stage 0 for the batches pushed from now on (the MSM
-        terms, t*h and c*Q in one launch on an internal stream beside the fold rounds); same bits."""
+        terms, t*h and c*Q as RK_MSMT chunks inside the batch's fold-round ticks, stages 2 .. L, on
+        the pipeline's own stream; the lane trees at the final-terms tick); same bits.  Raises
+        BulletproofError where the split does not apply (inner-product mode, n above the lane-tree
+        limit, n > 512)."""
         _chk(lib().hipbp_pipeline_defer_msm(_c(self.h), ctypes.c_int(1 if on else 0)))
 
     def prefix_tables(self, bits):

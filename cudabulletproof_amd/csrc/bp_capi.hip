@@ -149,15 +149,10 @@ struct Engine {
     }
     // prover workspaces (hipbp_batch_generate_range_proof), one per stream so batches on
     // different streams overlap (one batch's latency-bound stages under another's term launch)
-    // + a high-priority side stream for the batch's latency-bound tail (chain0 .. final; created on
-    // first use) and the two events that order it after terms0 and before the caller's next work
     struct ProverBufs {
         Buf b[19];
-        hipStream_t tail = nullptr;
-        hipEvent_t ev_t0 = nullptr, ev_done = nullptr;
     };
     std::map<hipStream_t, ProverBufs*> provers;
-    hipEvent_t prove_gate = nullptr;   // HIPBP_PROVE_GATE: recorded after the last prover terms0
     // pinned host staging for the single-proof entry points (a pageable source of an
     // async copy must outlive the copy; this one does, and the stream is synced after use)
     uint8_t* pinned = nullptr;
@@ -503,7 +498,11 @@ struct Pipeline {
         for (auto& sl : slots) if (sl.active) return true;
         return false;
     }
-    bool defer_ok() const { return range_mode != 0 && lane_tree && Lr >= 2; }
+    // A split batch adds one RK_MSMT region to each of its stages 2 .. L: in steady state a tick then
+    // holds up to 2 L + 5 regions (RK_STAGE0, L - 1 RK_ROUND + L - 1 RK_MSMT, RK_FINAL_TERMS, RK_M3,
+    // RK_FINAL, RK_LTREE, RK_POLY, RK_PREP), which must fit the kernel's region list (n <= 512 when
+    // HIPBP_LANE_TREE_MAX raises the lane-tree limit; the default limit is n <= 64, 17 regions).
+    bool defer_ok() const { return range_mode != 0 && lane_tree && Lr >= 2 && 2 * Lr + 5 <= bp::MAX_REGIONS; }
     // a split batch's MSM-term chunks: stages defer_first .. msm_last(L), wave-aligned lane ranges
     // (HIPBP_DEFER_SPAN = "first:last_off:weight" for A/B runs: chunks at stages first .. L - last_off
     // (at least first), weight 0 equal chunks, 1 chunk k weighted 2^k: later, emptier rounds get more)
@@ -1038,13 +1037,6 @@ int hipbp_release_stream_workspaces(void* stream) {
     }
     auto pi = e->provers.find(s);
     if (pi != e->provers.end()) {
-        Engine::ProverBufs* pb = pi->second;
-        if (pb->tail) {
-            keep(hipStreamSynchronize(pb->tail));
-            keep(hipStreamDestroy(pb->tail));
-        }
-        if (pb->ev_t0) keep(hipEventDestroy(pb->ev_t0));
-        if (pb->ev_done) keep(hipEventDestroy(pb->ev_done));
         free_all(pi->second->b, sizeof(pi->second->b) / sizeof(pi->second->b[0]));
         delete pi->second;
         e->provers.erase(pi);
@@ -1133,55 +1125,20 @@ static int prove_run(const hipbp_prove_input* in, const ge25519* G, const ge2551
     };
     run(bp::PS_PREP, 0);
     run(bp::PS_SORT0, 0);
-    // A/B knob (HIPBP_PROVE_GATE=1, off by default): terms0 of successive calls runs one after another
-    // across streams, so that each batch's latency-bound rest can run under the next batch's terms0
-    // (with HIPBP_PROVE_T0_PAD leaving it a wave slot).
-    static const bool gate = getenv("HIPBP_PROVE_GATE") && atoi(getenv("HIPBP_PROVE_GATE")) != 0;
-    if (gate) {
-        if (!e->prove_gate) BP_RET_ON(hipEventCreateWithFlags(&e->prove_gate, hipEventDisableTiming));
-        else BP_RET_ON(hipStreamWaitEvent(s, e->prove_gate, 0));
-    }
     run(bp::PS_TERMS0, 0);
-    if (gate) BP_RET_ON(hipEventRecord(e->prove_gate, s));
-    // The tail (chain0 .. final: ~20 short dependent launches, mostly latency-bound) runs on a
-    // high-priority side stream of this workspace: with two caller streams, another batch's terms0
-    // holds every VGPR, and at equal priority the tail's blocks only got slots as that terms0
-    // drained (r03q trace: chain0 stretched to ~40 ms).  At high priority each freed slot goes to
-    // the tail first.  The caller's stream waits for the tail, so the call stays ordered on it.
-    // HIPBP_PROVE_TAIL_STREAM=1 turns it on (A/B; off by default).
-    static const bool tail_stream = getenv("HIPBP_PROVE_TAIL_STREAM") && atoi(getenv("HIPBP_PROVE_TAIL_STREAM")) != 0;
-    hipStream_t ts = s;
-    if (tail_stream) {
-        if (!pb->tail) {
-            int lo_pr = 0, hi_pr = 0;
-            BP_RET_ON(hipDeviceGetStreamPriorityRange(&lo_pr, &hi_pr));
-            BP_RET_ON(hipStreamCreateWithPriority(&pb->tail, hipStreamNonBlocking, hi_pr));
-            BP_RET_ON(hipEventCreateWithFlags(&pb->ev_t0, hipEventDisableTiming));
-            BP_RET_ON(hipEventCreateWithFlags(&pb->ev_done, hipEventDisableTiming));
-        }
-        BP_RET_ON(hipEventRecord(pb->ev_t0, s));
-        BP_RET_ON(hipStreamWaitEvent(pb->tail, pb->ev_t0, 0));
-        ts = pb->tail;
-    }
-    auto run_t = [&](int stage, int r) {
-        bp::launch_prove(stage, r, pin, w, po, (const bp::ge*)G, (const bp::ge*)H, (const bp::ge*)g,
-                         (const bp::ge*)h, e->dtab, e->two_i, ts);
-    };
-    run_t(bp::PS_CHAIN0, 0);
-    run_t(bp::PS_COMMIT, 0);
-    run_t(bp::PS_TERMS1, 0);
-    run_t(bp::PS_TX, 0);
+    // the tail (chain0 .. final: ~20 short dependent launches) on the caller's stream; a side stream,
+    // a terms0 gate across streams and other tail schedules were measured and rejected
+    run(bp::PS_CHAIN0, 0);
+    run(bp::PS_COMMIT, 0);
+    run(bp::PS_TERMS1, 0);
+    run(bp::PS_TX, 0);
     for (int r = 0; r < pin.L; r++) {
-        run_t(bp::PS_RTERMS, r);
-        run_t(bp::PS_RCHAIN, r);
-        run_t(bp::PS_ROUND, r);
+        run(bp::PS_RTERMS, r);
+        run(bp::PS_RCHAIN, r);
+        run(bp::PS_ROUND, r);
     }
-    run_t(bp::PS_FINAL, 0);
+    run(bp::PS_FINAL, 0);
     BP_RET_ON(hipGetLastError());
-    if (tail_stream) {
-        BP_RET_ON(hipEventRecord(pb->ev_done, ts));
-        BP_RET_ON(hipStreamWaitEvent(s, pb->ev_done, 0));
-    }
     return HIPBP_OK;
 }
 
@@ -1271,7 +1228,8 @@ int hipbp_pipeline_defer_msm(void* handle, int on) {
     Pipeline* pl = (Pipeline*)handle;
     if (!pl) { g_err = "null pipeline"; return HIPBP_ERR_ARG; }
     if (on && !pl->defer_ok()) {
-        g_err = "defer_msm: needs cuda_range_proof_verify / range_proof_verify semantics and 4 <= n <= the lane-tree limit";
+        g_err = "defer_msm: needs cuda_range_proof_verify / range_proof_verify semantics, 4 <= n <= the lane-tree limit "
+                "and n <= 512 (a split tick's region list)";
         return HIPBP_ERR_ARG;
     }
     std::lock_guard<std::mutex> lk(pl->e->mu);
@@ -1672,7 +1630,11 @@ int hipbp_batch_range_proof_verify_host(const RangeProof* proofs, const ge25519*
     int ndev = 0;
     BP_RET_ON(hipGetDeviceCount(&ndev));
     if (ndev <= 0) { g_err = "no HIP device"; return HIPBP_ERR_DEVICE; }
-    int ng = num_gpus <= 0 ? ndev : std::min(num_gpus, ndev);
+    if (num_gpus > ndev) {   // asked for more devices than are visible: an error, not a silent fallback
+        g_err = "num_gpus = " + std::to_string(num_gpus) + " but " + std::to_string(ndev) + " HIP device(s) visible";
+        return HIPBP_ERR_ARG;
+    }
+    int ng = num_gpus <= 0 ? ndev : num_gpus;
     // HIPBP_HOST_SHARDS=k (tests, only when the caller leaves num_gpus <= 0): k shards (at most 64
     // and at most one per proof), shard d on device (current + d) % ndev, so the multi-device split, its host
     // threads and the verdict merge also run on a one-GPU box (threads of one device serialise on

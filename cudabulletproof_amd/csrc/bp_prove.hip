@@ -537,13 +537,10 @@ void launch_prove(int stage, int r, const ProveIn& in, const ProveWs& ws, const 
             }
             break;
         case PS_TERMS0: {
-            // A/B knob: unused dynamic LDS per block, capping terms0 blocks per CU (room for the other
-            // stream's chains)
-            static const unsigned pad = [] { const char* e = getenv("HIPBP_PROVE_T0_PAD"); return e ? (unsigned)atoi(e) : 0u; }();
             // the lists hold at most 2n + 4 items per proof (sL, sR, v, gamma, alpha, rho): every aL / aR
             // term is a zero-scalar constant or a ctab entry (BP_GTAB), so the grid stops there
             const size_t per_max = BP_GTAB ? 2 * (size_t)n + 4 : 4 * (size_t)n + 4;
-            k_prove_terms0<<<nblk(B * per_max + 2 * n), TPB, pad, s>>>(in, ws, G, H, g, h, dtab);
+            k_prove_terms0<<<nblk(B * per_max + 2 * n), TPB, 0, s>>>(in, ws, G, H, g, h, dtab);
             break;
         }
         case PS_CHAIN0: k_prove_chain0<<<nblk(B * 4), TPB, 0, s>>>(in, ws); break;

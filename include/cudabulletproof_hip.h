@@ -133,8 +133,9 @@ int hipbp_device_count(void);
  * structs: ok[i] = cuda_range_proof_verify(&proofs[i], &V[i], n, G, H, g, h) for i < count, bit for
  * bit, with the reference's length check per proof (message on stderr, ok[i] = 0).  The proofs are
  * packed into the flat batch format, sharded in contiguous blocks over num_gpus devices (<= 0: all
- * visible) starting at the calling thread's current device (shard d on device (current + d) mod the
- * device count, so num_gpus = 1 stays on the current device), one host thread per device: 1024-proof chunks are packed into pinned staging, copied
+ * visible; more than are visible: HIPBP_ERR_ARG, nothing verified) starting at the calling thread's
+ * current device (shard d on device (current + d) mod the device count, so num_gpus = 1 stays on
+ * the current device), one host thread per device: 1024-proof chunks are packed into pinned staging, copied
  * and pushed as they are packed, alternating over two verify pipelines on two streams; one D2H of
  * the verdicts; no data-path exchange between devices.  Proofs whose a/b length or round
  * count differs from the first valid proof's go through the single-proof path.  Host pointers,
@@ -204,7 +205,9 @@ int hipbp_pipeline_use_gens(void* pipeline, void* gens);
  * batch's stage-0 tick runs only fold round 0 (and the range_proof_verify polynomial terms); its
  * two MSMs' terms, t*h and c*Q, which only the final assembly reads, run in chunks inside its
  * fold-round ticks, whose own items shrink round by round.  A finite batch then fills the rounds
- * before its latency-bound last ticks.  Same bits either way. */
+ * before its latency-bound last ticks.  Same bits either way.  HIPBP_ERR_ARG where it does not
+ * apply: inner-product mode, n above the lane-tree limit (HIPBP_LANE_TREE_MAX), or n > 512 (a
+ * split tick's 2 log2 n + 5 regions must fit the kernel's region list). */
 int hipbp_pipeline_defer_msm(void* pipeline, int on);
 void hipbp_pipeline_destroy(void* pipeline);
 

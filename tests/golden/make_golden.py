@@ -24,7 +24,12 @@ oracle/build_ref.sh) and records inputs + reference outputs as .npz (no pickles)
               compute_precise_delta's delta and the enhanced_range_check /
               robust_polynomial_identity_check / inner_product_verify results.
 
-  python tests/golden/make_golden.py [ipa4096|rpverify]   (argument: regenerate only that fixture)
+  batch1024.npz BASELINE configs[1] at full batch: 1024 reference proofs of random 64-bit values
+              + 256 tampered copies, the reference's cuda_range_proof_verify outcome of each
+              (verdict, early reject, 8-byte digests of the proof, P and the check point).
+
+  python tests/golden/make_golden.py [ipa4096|rpverify|accept|printed|batch1024]
+              (argument: regenerate only that fixture)
 
 The survey's golden digests are reproduced by tests/test_oracle_golden.py.
 """
@@ -409,8 +414,98 @@ def make_accept():
               f"rejects; ipa crafted ok {out['ipa_ok'].astype(int).tolist()}")
 
 
+B1024_SEED0 = 5001   # seeds 5001 .. 6024 (disjoint from every other fixture's)
+
+
+def batch1024_value(seed):
+    """The 64-bit value of batch1024 proof `seed`: bytes 0..7 of SHA256("batch1024" || seed_le64)."""
+    v = np.zeros(32, np.uint8)
+    v[:8] = np.frombuffer(hashlib.sha256(b"batch1024" + int(seed).to_bytes(8, "little")).digest()[:8], np.uint8)
+    return v
+
+
+def proof_digest(pr):
+    """8-byte SHA-256 of a proof's words (head, V, a, b, L, R): the GPU prover's reproduction check."""
+    return hashlib.sha256(b"".join(np.ascontiguousarray(pr[k], np.uint64).tobytes()
+                                   for k in ("head", "V", "a", "b", "L", "R"))).digest()[:8]
+
+
+def point_digest(p):
+    return hashlib.sha256(np.ascontiguousarray(p, np.uint64).tobytes()).digest()[:8]
+
+
+def _b1024_rows(args):
+    """Worker (spawned, no GPU): reference proofs / tampered copies -> per-case outcomes."""
+    lo, hi, tam = args
+    R = po.Reference()
+    n = 64
+    G, H = R.base_points(n, 1), R.base_points(n, 2)
+    g, h = R.gh()
+    out = []
+    cache = {}
+
+    def proof(i):
+        if i not in cache:
+            cache[i] = R.prove(B1024_SEED0 + i, batch1024_value(B1024_SEED0 + i), n, G, H, g, h)
+        return cache[i]
+    jobs = [(i, None) for i in range(lo, hi)] + [(t[0], t) for t in tam]
+    for i, t in jobs:
+        pr = proof(i) if t is None else apply_tamper(proof(i), *t[1:])
+        ok, txt = R.cuda_range_proof_verify_log(pr, n, G, H, g, h)
+        early = po.printed_stats(txt)["early_reject"]   # crv:146-158: <a,b> != c, no check point formed
+        P, _ = R.verify_P(pr, n, G, H, g, h)
+        hd = po.head_fields(pr["head"])
+        _, _, chk = R.ipa_fold(G, H, n, hd["x"], pr["L"], pr["R"], pr["a"][0], pr["b"][0], hd["c"], h)
+        out.append((i, t is not None, proof_digest(pr), bool(ok), point_digest(P), point_digest(chk), bool(early)))
+    return out
+
+
+def make_batch1024(procs=8):
+    """BASELINE configs[1] at its full batch: 1024 reference proofs of random 64-bit values
+    (generate_range_proof, rp.cu:1159, seeds 5001.. under oracle/ref's deterministic RAND_bytes)
+    and 256 tampered copies (TAMPER_KINDS, one word XOR a mask), each verified by the reference's
+    own cuda_range_proof_verify (crv:82-127).  Stored per case: the seed index, the value, 8-byte
+    SHA-256 digests of the proof words, of P (calculate_inner_product_point) and of the check
+    point (crv:160-279), and the reference's verdict -> batch1024.npz (no proof data: the GPU
+    prover regenerates the proofs from seed and value, tests/test_gpu_fullsize.py)."""
+    import multiprocessing as mp
+    po.build()
+    B, Lr = 1024, 6
+    rng = np.random.default_rng(1024)
+    tam = []
+    for j in range(256):
+        kind, sel = TAMPER_KINDS[j % len(TAMPER_KINDS)]
+        f, w = tamper_target(kind, sel, Lr, rng)
+        mask = 1 << int(rng.integers(0, 64)) if j % 2 else int(rng.integers(1, 2**63))
+        tam.append((int(rng.integers(0, B)), f, w, mask))
+    cuts = [B * k // procs for k in range(procs + 1)]
+    jobs = [(cuts[k], cuts[k + 1], [t for t in tam if cuts[k] <= t[0] < cuts[k + 1]]) for k in range(procs)]
+    with mp.get_context("spawn").Pool(procs) as pool:
+        rows = [r for part in pool.map(_b1024_rows, jobs) for r in part]
+    orig = sorted([r for r in rows if not r[1]], key=lambda r: r[0])
+    tmap = {}
+    for r in rows:
+        if r[1]:
+            tmap.setdefault(r[0], []).append(r)
+    trows = []
+    for t in tam:   # the tampered rows in `tam` order (a worker ran its share in that order)
+        trows.append(tmap[t[0]].pop(0))
+    cat = lambda rs, k: np.stack([np.frombuffer(r[k], np.uint8) for r in rs])
+    out = dict(seed0=np.array(B1024_SEED0), value=np.stack([batch1024_value(B1024_SEED0 + i)[:8].view("<u8")[0]
+                                                             for i in range(B)]).astype(np.uint64),
+               proof_d8=cat(orig, 2), ok=np.array([r[3] for r in orig]), P_d8=cat(orig, 4), check_d8=cat(orig, 5),
+               early=np.array([r[6] for r in orig]),
+               tamper=np.array([t[:3] for t in tam], np.int64), tamper_mask=np.array([t[3] for t in tam], np.uint64),
+               t_proof_d8=cat(trows, 2), t_ok=np.array([r[3] for r in trows]), t_P_d8=cat(trows, 4),
+               t_check_d8=cat(trows, 5), t_early=np.array([r[6] for r in trows]))
+    np.savez_compressed(os.path.join(HERE, "batch1024.npz"), **out)
+    print(f"batch1024: {int(out['ok'].sum())}/{B} reference accepts, tampered {int(out['t_ok'].sum())}/256 accepts")
+
+
 if __name__ == "__main__":
-    if sys.argv[1:] == ["ipa4096"]:
+    if sys.argv[1:] == ["batch1024"]:
+        make_batch1024()
+    elif sys.argv[1:] == ["ipa4096"]:
         make_ipa4096()
     elif sys.argv[1:] == ["rpverify"]:
         make_rpverify()

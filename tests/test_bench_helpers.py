@@ -94,3 +94,37 @@ def test_rank_launch_command(monkeypatch):
     assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
     assert cmd[-5:] == ["--gpus", "4", "--rehearse", "--steps", "3"] and cmd[-6].endswith("bench.py")
     assert bench.rank_launch(argparse.Namespace(gpus=1, rehearse=False)) is None
+
+
+def _distinct_worker(rank, world, port, pcis, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    bench.device_pci = lambda dev: pcis[rank]
+    try:
+        bench.require_distinct_devices(None, world, rank)
+        q.put((rank, "ran"))
+        dist.destroy_process_group()
+    except SystemExit as e:
+        q.put((rank, f"exit {e.code}"))
+
+
+def test_measured_multirank_run_needs_distinct_devices_over_rccl():
+    """A non-rehearsal N-rank bench refuses (exit 4 on every rank, before any leg) when its ranks
+    share a device or the backend is not RCCL: here gloo ranks on two distinct and on one shared
+    PCI address — both refused, since gloo is not 'nccl'."""
+    import multiprocessing as mp
+    import socket
+    for pcis in (["0000:05:00.0", "0000:15:00.0"], ["0000:05:00.0", "0000:05:00.0"]):
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        procs = [ctx.Process(target=_distinct_worker, args=(r, 2, port, pcis, q)) for r in range(2)]
+        for p in procs:
+            p.start()
+        res = dict(q.get(timeout=120) for _ in range(2))
+        for p in procs:
+            p.join(timeout=60)
+        assert res == {0: "exit 4", 1: "exit 4"}, res

@@ -1,7 +1,8 @@
 """bench.py's N>1 path (torchrun, one process per rank) rehearsed on one GPU: every rank on cuda:0
-with gloo collectives (--rehearse).  The sharded MSM (shard roots + all_gather + canonical tree)
+with gloo collectives (--rehearse), N = 2, 4, 8.  The sharded MSM (shard roots + all_gather + canonical tree)
 and the window-sharded Pippenger (window sums + all_gather + Horner) must give the same points as
-the single-rank run, and the line must carry the N=2 fields."""
+the single-rank run, and the line must carry the N-rank fields.  A real (non-rehearsal) N > 1 run
+must refuse to measure when its ranks do not sit on N distinct devices or the backend is not RCCL."""
 import json
 import os
 import subprocess
@@ -22,30 +23,40 @@ def _line(out):
     return json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
 
 
-@pytest.mark.gpu
-def test_bench_two_ranks_rehearsal_matches_one_rank():
+@pytest.fixture(scope="module")
+def one_rank_line():
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     one = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + SMALL, capture_output=True, text=True,
                          timeout=600, cwd=ROOT, env=env)
     assert one.returncode == 0, one.stderr[-2000:]
-    # no outer launcher: `--gpus 2` makes bench.py start the 2 ranks itself (torch.distributed.run child)
-    two = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--rehearse"] + SMALL[:-2]
-                         + LEGS, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    return _line(one.stdout)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [2, 4, 8])
+def test_bench_ranks_rehearsal_matches_one_rank(one_rank_line, N):
+    """N = 2, 4, 8 ranks (all on cuda:0, gloo): the shard of configs[4] (shard.shard_bounds(3000, N, r)),
+    the sharded canonical MSM and the window-split Pippenger give the one-rank digests."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    l1 = one_rank_line
+    # no outer launcher: `--gpus N` makes bench.py start the N ranks itself (torch.distributed.run child)
+    two = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(N), "--rehearse"] + SMALL[:-2]
+                         + LEGS, capture_output=True, text=True, timeout=900, cwd=ROOT, env=env)
     assert two.returncode == 0, two.stderr[-2000:]
-    l1, l2 = _line(one.stdout), _line(two.stdout)
-    assert l1["n_gpus"] == 1 and l2["n_gpus"] == 2
+    l2 = _line(two.stdout)
+    assert l1["n_gpus"] == 1 and l2["n_gpus"] == N
     # the line proves who ran: the torch.distributed world, one entry per rank, each rank's own batches
-    assert l1["world_size"] == 1 and l2["world_size"] == 2 and l2["backend"] == "gloo"
-    assert [r["rank"] for r in l2["ranks"]] == [0, 1] and len(l1["ranks"]) == 1
+    assert l1["world_size"] == 1 and l2["world_size"] == N and l2["backend"] == "gloo"
+    assert [r["rank"] for r in l2["ranks"]] == list(range(N)) and len(l1["ranks"]) == 1
     assert l2["ranks"][0]["verdicts_sha256"] == l1["ranks"][0]["verdicts_sha256"]   # rank 0's seeds whatever N
-    assert l2["ranks"][1]["verdicts_sha256"] != l2["ranks"][0]["verdicts_sha256"]   # distinct batches per rank
+    assert len({r["verdicts_sha256"] for r in l2["ranks"]}) == N                    # distinct batches per rank
     assert all(r["pci"] and r["proofs"] == 4 * 128 for r in l2["ranks"])
     assert l2["msm"]["scaling"] == "strong" and l2["scaling"] == "weak"
     assert l1["msm"]["result_sha256"] == l2["msm"]["result_sha256"]
-    # Pippenger with its windows split over the 2 ranks == the single-GPU Pippenger
+    # Pippenger with its windows split over the N ranks == the single-GPU Pippenger
     ps = l2["msm"]["pippenger_sharded"]
     assert ps["scaling"] == "strong" and ps["result_sha256"] == l1["msm"]["pippenger"]["result_sha256"]
-    # configs[4]: the same proof set sharded over 1 or 2 ranks -> the same verdicts on every rank
+    # configs[4]: the same proof set sharded over 1 or N ranks -> the same verdicts on every rank
     s1, s2 = l1["sharded_2p16"], l2["sharded_2p16"]
     assert s1["proofs"] == s2["proofs"] == 3000 and s2["scaling"] == "strong"
     assert s1["passes"] == s2["passes"] > 0 and s1["verdicts_sha256"] == s2["verdicts_sha256"]

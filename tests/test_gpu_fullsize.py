@@ -99,6 +99,88 @@ def test_batch_2p16_tiled_verify(bp, oracle):
     assert np.array_equal(chk[0][folds], chkr[folds])
 
 
+def _proof_dicts(out, B):
+    """Per-proof dicts (head, V, a, b, L, R as the reference harness lays them out) from the GPU
+    prover's output tensors."""
+    o = {k: out[k].cpu().numpy().view(np.uint64) for k in ("V", "A", "S", "T1", "T2", "taux", "mu", "t", "c", "x",
+                                                          "a", "b", "L", "R")}
+    return [dict(head=np.concatenate([o[k][p] for k in ("V", "A", "S", "T1", "T2", "taux", "mu", "t", "c", "x")]),
+                 V=o["V"][p], a=o["a"][p], b=o["b"][p], L=o["L"][p], R=o["R"][p]) for p in range(B)]
+
+
+@pytest.mark.parametrize("split", [False, True])
+def test_batch1024_reference_outcomes(bp, oracle, golden, split):
+    """BASELINE configs[1] at its full batch against the REFERENCE's own outcomes
+    (tests/golden/batch1024.npz, make_golden.py make_batch1024): the GPU prover regenerates the
+    1024 reference proofs (seeds + values; each proof's digest must equal the reference prover's,
+    rp.cu:1159), and they go through the bench's exact configuration — ONE B = 1024 batch on one of
+    two pipelines on their own streams, the bench's default prefix-table width, split stage 0 off
+    and on — beside a second B = 1024 batch on the other pipeline whose first 256 proofs are the
+    fixture's tampered copies.  Every verdict and every P digest, and the check-point digest of
+    every case that folds, equal the reference's cuda_range_proof_verify (crv:82-127)."""
+    import torch
+    import bench
+    from test_gpu_parity import _prove_inputs
+    from test_accept_rule import _batch_arrays
+    from accept_cases import apply_tamper
+    d = golden("batch1024")
+    n, B = 64, 1024
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    seeds = [int(d["seed0"]) + i for i in range(B)]
+    values = [np.concatenate([np.frombuffer(np.uint64(x).tobytes(), np.uint8), np.zeros(24, np.uint8)])
+              for x in d["value"]]
+    v, gam, sL, sR, rnd, _ = _prove_inputs(seeds, values, n)
+    G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+    g, h = oracle.gh()
+    K = bench.DEFAULT_PREFIX_BITS
+    gens = bp.Generators(n, T(G), T(H), T(g), T(h), prefix_bits=K)
+    pipes = []
+    try:
+        out = bp.batch_generate_range_proof(n, T(v), T(gam), T(sL), T(sR), T(rnd), T(G), T(H), T(g), T(h), gens=gens)
+        torch.cuda.synchronize()
+        assert int(out["valid"].sum().item()) == B
+        proofs = _proof_dicts(out, B)
+        got = np.stack([np.frombuffer(hashlib.sha256(b"".join(np.ascontiguousarray(pr[k], np.uint64).tobytes()
+                                                              for k in ("head", "V", "a", "b", "L", "R"))).digest()[:8],
+                                      np.uint8) for pr in proofs])
+        assert np.array_equal(got, d["proof_d8"]), "GPU prover != reference prover"
+        batch0 = bp.RangeProofBatch(n, **{k: out[k] for k in bp.RangeProofBatch.FIELDS})
+        tcases = [apply_tamper(proofs[int(b)], f, w, m) for (b, f, w), m in zip(d["tamper"], d["tamper_mask"])]
+        batch1 = bp.RangeProofBatch.from_numpy(n, _batch_arrays(tcases + proofs[256:]), dev)
+        streams = [torch.cuda.Stream(dev) for _ in range(2)]
+        pipes = [bp.VerifyPipeline(B, n, T(G), T(H), T(h), stream=st) for st in streams]
+        res = []
+        for pp, b in zip(pipes, (batch0, batch1)):
+            pp.use_gens(gens)
+            pp.defer_msm(split)
+            ok = torch.zeros(B, dtype=torch.uint8, device=dev)
+            P = torch.zeros(B, 16, dtype=torch.int64, device=dev)
+            chk = torch.zeros(B, 16, dtype=torch.int64, device=dev)
+            pp.push(b, ok, P, chk)
+            res.append((ok, P, chk))
+        for pp in pipes:
+            pp.flush()
+        torch.cuda.synchronize()
+    finally:
+        for pp in pipes:
+            pp.close()
+        gens.close()
+        torch.cuda.empty_cache()
+    p8 = lambda P: np.stack([np.frombuffer(hashlib.sha256(r.tobytes()).digest()[:8], np.uint8)
+                             for r in P.cpu().numpy().view(np.uint64)])
+    want = [(d["ok"], d["P_d8"], d["check_d8"], d["early"]),
+            (np.concatenate([d["t_ok"], d["ok"][256:]]), np.concatenate([d["t_P_d8"], d["P_d8"][256:]]),
+             np.concatenate([d["t_check_d8"], d["check_d8"][256:]]), np.concatenate([d["t_early"], d["early"][256:]]))]
+    for k, ((ok, P, chk), (wok, wP, wchk, wearly)) in enumerate(zip(res, want)):
+        okh = ok.cpu().numpy().astype(bool)
+        assert np.array_equal(okh, wok.astype(bool)), (k, np.nonzero(okh != wok.astype(bool))[0][:10])
+        assert np.array_equal(p8(P), wP), k
+        folds = ~wearly.astype(bool)
+        assert np.array_equal(p8(chk)[folds], wchk[folds]), k
+    assert 0 < int(d["ok"].sum()) <= B and int(d["t_ok"].sum()) < 256
+
+
 def test_msm_pippenger_2p20_matches_oracle(bp, oracle):
     """hipbp_msm_pippenger (window 12, the labelled alternative) on the same 2^20 inputs equals
     orc_msm_pippenger's result (tests/golden/msm_2p20.json)."""

@@ -275,6 +275,10 @@ def test_batch_verify_host_structs(bp, golden, n):
     # the reference's length check (crv:140-143): generator vectors shorter than the proofs' n
     got = bp.batch_range_proof_verify_host(ref[:2], d["V"][:2], n, d["G"][:n // 2], d["H"][:n // 2], d["g"], d["h"])
     assert not got.any()
+    # more devices than are visible: an error with a message, not a silent one-device run
+    ndev = torch.cuda.device_count()
+    with pytest.raises(bp.BulletproofError, match=f"num_gpus = {ndev + 1} but {ndev} HIP device"):
+        bp.batch_range_proof_verify_host(ref, d["V"], n, d["G"], d["H"], d["g"], d["h"], num_gpus=ndev + 1)
 
 
 @pytest.mark.parametrize("n,B,ab_len", [(64, 48, 1), (16, 40, 3), (4, 17, 2), (1, 9, 1), (256, 4, 1), (512, 3, 1),
@@ -1256,10 +1260,11 @@ def test_pipeline_quad_ticks_same_bits(bp, oracle, monkeypatch, n, B, mode, K, p
                                                   (64, 40, 1, 0, 2, "2"), (4, 5, 1, 3, 1, None),
                                                   (1, 3, 1, 0, 1, None), (64, 1, 1, 9, 1, "1")])
 def test_pipeline_deferred_msm_same_bits(bp, oracle, monkeypatch, n, B, mode, K, pushes, q):
-    """Split stage 0 (hipbp_pipeline_defer_msm: the MSM terms, t*h and c*Q in one launch on the
-    pipeline's bulk stream, the lane trees waiting for it at stage FIN - 1) gives the unsplit
-    pipeline's verdicts, P, check points, mode-2 flags and polynomial sides bit for bit: batches in
-    flight together, with and without prefix tables, each tick form; a sample equals the oracle."""
+    """Split stage 0 (hipbp_pipeline_defer_msm: the MSM terms, t*h and c*Q as RK_MSMT chunks inside
+    the batch's own fold-round ticks, stages 2 .. L, on the pipeline's stream; the lane trees at
+    msm_last(L) + 1, the final-terms tick) gives the unsplit pipeline's verdicts, P, check points,
+    mode-2 flags and polynomial sides bit for bit: batches in flight together, with and without
+    prefix tables, each tick form; a sample equals the oracle."""
     from cudabulletproof_amd import synth
     import torch
     G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
@@ -1322,6 +1327,44 @@ def test_pipeline_defer_msm_api(bp, oracle):
         pl.close()
         outs.append((ok.cpu(), P.cpu()))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+def test_pipeline_defer_msm_largest_lane_tree_n(bp, oracle, monkeypatch):
+    """With the lane-tree limit raised (HIPBP_LANE_TREE_MAX = 4096) the split applies up to n = 512,
+    whose split ticks hold 2 log2 n + 5 = 23 regions (<= the kernel's 24), and verifies as without
+    it, 16 batches in flight; at n = 1024 (25 regions) the switch is refused with a message
+    instead of a push failing on the region list (advisor r04)."""
+    import torch
+    from cudabulletproof_amd import synth
+    monkeypatch.setenv("HIPBP_LANE_TREE_MAX", "4096")
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    n = 1024
+    G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+    g, h = oracle.gh()
+    pl = bp.VerifyPipeline(2, n, T(G), T(H), T(h))
+    with pytest.raises(bp.BulletproofError, match="n <= 512"):
+        pl.defer_msm(True)
+    pl.close()
+    n, B = 512, 2
+    G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+    outs = []
+    for d in (False, True):
+        pl = bp.VerifyPipeline(B, n, T(G), T(H), T(h))
+        pl.defer_msm(d)
+        res = []
+        for k in range(16):   # more batches than stages: steady-state ticks with every stage's regions
+            batch = bp.RangeProofBatch.from_numpy(n, synth.proofs(B, n, seed=900 + k), dev)
+            ok = torch.zeros(B, dtype=torch.uint8, device=dev)
+            P = torch.zeros(B, 16, dtype=torch.int64, device=dev)
+            pl.push(batch, ok, P)
+            res.append((ok, P, batch))
+        pl.flush()
+        torch.cuda.synchronize()
+        pl.close()
+        outs.append([(ok.cpu(), P.cpu()) for ok, P, _ in res])
+    for (a, b), (c, e) in zip(outs[0], outs[1]):
+        assert torch.equal(a, c) and torch.equal(b, e)
 
 
 @pytest.mark.parametrize("n,B,lt", [(512, 3, "1024"), (512, 3, "512"), (256, 4, "4096"), (64, 5, "0")])

@@ -148,6 +148,45 @@ def test_prover_against_reference(oracle, golden, n):
             assert np.array_equal(pr[k], d[k][i]), (i, k)
 
 
+def test_oracle_batch1024_sample(oracle, golden):
+    """batch1024.npz (BASELINE configs[1] at full batch, reference-emitted): a 24-case sample —
+    every 64th of the 1024 reference proofs and every 32nd tampered copy — through the CPU
+    restatement's prover and cuda_range_proof_verify: proof, P and check-point digests and the
+    verdicts equal the reference's (the GPU runs the whole fixture: test_gpu_fullsize.py)."""
+    import sys
+    from oracle.pyoracle import prover_randomness
+    sys.path.insert(0, GOLDEN)
+    from accept_cases import apply_tamper
+    d = golden("batch1024")
+    n = 64
+    G, H = oracle.base_points(n, 1), oracle.base_points(n, 2)
+    g, h = oracle.gh()
+    dig = lambda *arrs: np.frombuffer(hashlib.sha256(b"".join(np.ascontiguousarray(a, np.uint64).tobytes()
+                                                              for a in arrs)).digest()[:8], np.uint8)
+
+    def proof(i):
+        val = np.zeros(32, np.uint8)
+        val[:8] = np.frombuffer(np.uint64(d["value"][i]).tobytes(), np.uint8)
+        gamma, sLR, rnd4 = prover_randomness(int(d["seed0"]) + i, n)
+        return oracle.generate_range_proof(val, gamma, sLR, rnd4, n, G, H, g, h)
+
+    def check(pr, ok_w, P_w, chk_w, early):
+        ok, P, chk, _, _ = oracle.cuda_range_proof_verify(pr["head"], pr["V"], n, pr["a"], pr["b"], pr["L"], pr["R"],
+                                                          G, H, g, h)
+        assert ok == bool(ok_w) and np.array_equal(dig(P), P_w)
+        if not early:
+            assert np.array_equal(dig(chk), chk_w)
+    for i in range(0, 1024, 64):
+        pr = proof(i)
+        assert np.array_equal(dig(*(pr[k] for k in ("head", "V", "a", "b", "L", "R"))), d["proof_d8"][i]), i
+        check(pr, d["ok"][i], d["P_d8"][i], d["check_d8"][i], d["early"][i])
+    for j in range(0, 256, 32):
+        b, f, w = (int(x) for x in d["tamper"][j])
+        pr = apply_tamper(proof(b), f, w, int(d["tamper_mask"][j]))
+        assert np.array_equal(dig(*(pr[k] for k in ("head", "V", "a", "b", "L", "R"))), d["t_proof_d8"][j]), j
+        check(pr, d["t_ok"][j], d["t_P_d8"][j], d["t_check_d8"][j], d["t_early"][j])
+
+
 def test_prover_refuses_out_of_range(oracle):
     """validate_range_input (rp.cu:238): bit n or any higher byte set -> no proof."""
     from oracle.pyoracle import prover_randomness
