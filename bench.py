@@ -37,7 +37,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
-DEFAULT_PREFIX_BITS = 23       # --prefix-bits default (tests/test_gpu_fullsize.py runs the same width)
+# --prefix-bits default (tests/test_gpu_fullsize.py runs the same width): the smallest width within
+# 0.5 % of the best measured (profiles/ab/r05a_prefix_sweep.json, one MI355X, median of 2 runs each:
+# K 0 181.5 K, 16 188.0 K, 18 189.2 K, 20 190.0 K, 21 190.7 K, 22 191.0 K, 23 191.6 K verifies/s);
+# K = 21 takes 34.9 GB of the 288 GB HBM (K = 23: 139.6 GB)
+DEFAULT_PREFIX_BITS = 21
 FE_B, GE_B = 32, 128
 
 
@@ -80,8 +84,11 @@ def parse():
                          "or proof-shaped random data")
     ap.add_argument("--prefix-bits", type=int, default=DEFAULT_PREFIX_BITS,
                     help="fixed-base prefix tables of the generators (hipbp_pipeline_prefix_tables; "
-                         "0 = off): one-time setup, same bits (23: 139.6 GB at n = 64; +0.4 %% over 22, "
-                         "profiles/ab/r04t_prefix_bits.txt)")
+                         "0 = off): one-time setup, same bits (21: 34.9 GB at n = 64, within 0.5 %% of 23's "
+                         "139.6 GB, profiles/ab/r05a_prefix_sweep.json)")
+    ap.add_argument("--table-legs", default="0,16",
+                    help="prefix-table widths timed beside the headline on the same batches (`prefix_legs`: "
+                         "0 = the reference's plain double-and-add with no precompute); '' skips them")
     ap.add_argument("--shard-total", type=int, default=1 << 16, help="configs[4]: proofs in the sharded batch")
     ap.add_argument("--shard-batch", type=int, default=0,
                     help="configs[4]: proofs per pipeline push (0: auto from the rank's shard size)")
@@ -444,6 +451,7 @@ def rooflines(dom, B, n, steps, launches, avg_ms, dt, kern_ms, pcfg, npipes):
     }
     vi = pmc(dom, "valu_instr_per_launch", pcfg)
     busy = pmc(dom, "valu_busy_pct", pcfg)
+    alg_vi = alg_valu_per_verify(n, pcfg["prefix_bits"]) * B if dom == "k_terms" else None
     clk = pmc(dom, "eff_clock_ghz", pcfg)
     vagg = vi * launches / dt if vi else None   # all launches of the timed region / its wall time
     loops = step_roof()
@@ -459,8 +467,40 @@ def rooflines(dom, B, n, steps, launches, avg_ms, dt, kern_ms, pcfg, npipes):
         "isolated_loops_source": "profiles/valu_step_roof.json (tools/ubench_step.hip: k_terms' point-op loops "
                                  "from registers + LDS at its occupancy)",
         "valu_utilization_pct": pmc(dom, "valu_utilization_pct", pcfg), "pmc_config": pcfg,
+        "frac_alg": alg_vi / vi * busy / 100 if alg_vi and vi and busy else None,
+        "alg_product_valu_per_launch": alg_vi,
+        "frac_alg_rule": "minimum product VALU per launch (2 VALU per 32x32 limb product: 464 products per doubling "
+                         "with its squares, 512 per add with Z2 = 1; point ops per verify from bench.point_ops_model "
+                         "at this prefix width) / measured SQ_INSTS_VALU per launch x VALUBusy: the share of "
+                         "the SIMDs' issue cycles spent on the products the reference's formulas require",
     }
     return roofline, valu_roofline
+
+
+def point_ops_model(n, K):
+    """Expected point operations of one verify (crv:82 semantics), for scalars uniform below 2^255:
+    the 4n + 2 fixed-base scalar-mults (the two MSMs, fold round 0, t*h, c*Q) start after a K-bit
+    prefix-table entry (256 - K doublings, (255 - K) / 2 adds expected); the other sm_per_verify(n) -
+    (4n + 2) (fold rounds >= 1, a0 G', b0 H') run all 256 bits minus ~1 leading zero (254
+    doublings, 127 adds expected).  A model: the exact counts depend on the proofs' scalars."""
+    fixed = 4 * n + 2
+    other = sm_per_verify(n) - fixed
+    dbl = fixed * (256 - K) + other * 254 if K else (fixed + other) * 254
+    add = fixed * (255 - K) / 2 + other * 127 if K else (fixed + other) * 127
+    return dbl, add
+
+
+# 32x32-bit limb products per point operation the reference's formulas need at minimum: a doubling
+# (ge25519_add(r, r), curve25519_ops.cu:406) = 4 squares (36 products) + 5 general products (64);
+# an add with Z2 = 1 (the generators and normalized points) = 8 general products (Z1 Z2 = Z1)
+PRODUCTS_DBL, PRODUCTS_ADD = 4 * 36 + 5 * 64, 8 * 64
+
+
+def alg_valu_per_verify(n, K):
+    """Minimum product VALU of one verify in wave64 instructions: 2 VALU per 32x32 product (one
+    v_mad_u64_u32 + one carry count), per the point_ops_model, / 64 lanes."""
+    dbl, add = point_ops_model(n, K)
+    return 2 * (dbl * PRODUCTS_DBL + add * PRODUCTS_ADD) / 64
 
 
 def step_roof():
@@ -1011,6 +1051,61 @@ def prove_leg(args, dev, gens=None):
             "prefix_bits": gens.bits if gens is not None else 0}
 
 
+def prefix_leg(args, dev, world, bits, batches, oks, ref_oks, G, H, g, h, streams):
+    """The headline configuration at another prefix-table width (`prefix_legs`): fresh pipelines on
+    the same streams over the same resident batches, a generator set with `bits`-bit tables (none at
+    0: every scalar-mult is the reference's full 256-bit double-and-add, cuda_bulletproof_kernels.cu:26-41),
+    filled, then args.steps ticks timed between barrier + synchronize like `value` (max over ranks).
+    The verdicts of every batch must equal the headline's (`verdicts_match_headline`)."""
+    import torch
+    import torch.distributed as dist
+    import cudabulletproof_amd as bp
+    B, n, nb = args.batch, args.n, len(batches)
+    gens = None
+    torch.cuda.synchronize(dev)
+    tb = time.perf_counter()
+    if bits:
+        gens = bp.Generators(n, G, H, g, h, prefix_bits=bits)
+        torch.cuda.synchronize(dev)
+    build_s = time.perf_counter() - tb
+    npipe = max(1, args.pipes)
+    pipes = [bp.VerifyPipeline(B, n, G, H, h, stream=streams[i]) for i in range(npipe)]
+    try:
+        if gens is not None:
+            for pp in pipes:
+                pp.use_gens(gens)
+        step = lambda k: pipes[k % npipe].push(batches[k % nb], oks[k % nb])
+        for k in range((pipes[0].depth - 1) * npipe):
+            step(k)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            step(k)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        for pp in pipes:
+            pp.flush()
+        torch.cuda.synchronize(dev)
+        same = all(torch.equal(o, r) for o, r in zip(oks[:nb], ref_oks))
+    finally:
+        for pp in pipes:
+            pp.close()
+        if gens is not None:
+            gens.close()
+        torch.cuda.empty_cache()
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return {"prefix_bits": bits, "value": B * args.steps * world / dt, "ms_per_step": dt / args.steps * 1e3,
+            "steps": args.steps, "tables_GB": (2 * n + 2) * (1 << bits) * GE_B / 1e9 if bits else 0.0,
+            "tables_build_s": build_s if bits else None, "verdicts_match_headline": same}
+
+
 def rank_launch(args):
     """`--gpus N` means N ranks.  Under a launcher (WORLD_SIZE set) the world must be N.  Without
     one and N > 1, this process starts `torch.distributed.run --nproc-per-node N` on this script as
@@ -1215,6 +1310,11 @@ def main():
     for pp in pipes:
         pp.flush()
     torch.cuda.synchronize(dev)
+    prefix_legs = None
+    if pipes and args.table_legs.strip():   # the same workload at other table widths, e.g. none (K = 0)
+        ref_oks = [o.clone() for o in oks[:nb]]
+        prefix_legs = {f"k{b}": prefix_leg(args, dev, world, b, batches, oks, ref_oks, Gd, Hd, gd, hd, streams)
+                       for b in (int(x) for x in args.table_legs.split(",")) if b != args.prefix_bits}
     # every rank's identity + the verdicts of its own batches (gathered: proves N distinct ranks ran)
     ranks = [rank_info(dev, oks[:nb])]
     world_seen = 1
@@ -1286,8 +1386,10 @@ def main():
                        "batch_per_gpu": B, "n": n, "semantics": "cuda_range_proof_verify (crv:82)",
                        "parallelism": f"independent proof shards x{world}", "mode": args.mode,
                        "pipeline_depth": pipe.depth if pipe else None, "pipelines": len(pipes) or None,
-                       "prefix_tables": prefix,
+                       "prefix_tables": prefix, "prefix_bits": prefix["bits"] if prefix else 0,
+                       "prefix_tables_GB": round(prefix["GB"], 3) if prefix else 0.0,
                        "proof_bytes": proof_bytes(n, 1), "passes_in_warmup_batch": passes_warm},
+            "prefix_legs": prefix_legs,
             "repeats": ({"n": len(reps), "steps_each": args.steps,
                          "median": total / statistics.median(reps), "min": total / max(reps),
                          "max": total / min(reps), "unit": "verifies/s",
@@ -1297,6 +1399,9 @@ def main():
             "with_h2d": h2d, "configs0": configs0, "msm": msm, "ipa": ipa, "prove": prove,
             "sharded_2p16": sharded, "host_api": host_api,
         }
+        for k, leg in (prefix_legs or {}).items():   # scalars in `config` (the driver keeps config's scalars)
+            line["config"][f"{k}_value"] = leg["value"]
+            line["config"][f"{k}_ms_per_step"] = leg["ms_per_step"]
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()   # the other ranks wait out rank 0's single-GPU legs, then all leave together

@@ -254,7 +254,10 @@ BP_DEV void mul512(uint64_t t[8], const fe& f, const fe& g) {
         b[2 * i + 1] = (uint32_t)(g.v[i] >> 32);
     }
 #if BP_MUL_ASM && defined(__HIP_DEVICE_COMPILE__)   // host pass: the C form (host-side checks)
-    mul512_asm(w, a, b);
+    // bounded form (every column's first carry uncounted, mul512_asm.h) unless a lane's gating words
+    // a[0], b[7] exceed MUL_BOUNDED_WORD (wave-uniform test; ~2^-27 per lane): then the counting form
+    mul512_bounded_asm(w, a, b);
+    if (__builtin_expect(__any(max(a[0], b[7]) > MUL_BOUNDED_WORD), 0)) mul512_asm(w, a, b);
 #else
     uint64_t acc = 0;
     uint32_t c2 = 0;
@@ -295,7 +298,8 @@ BP_DEV void sqr512(uint64_t t[8], const fe& f) {
         a[2 * i + 1] = (uint32_t)(f.v[i] >> 32);
     }
 #if BP_MUL_ASM && defined(__HIP_DEVICE_COMPILE__)
-    sqr512_offdiag_asm(o, a);
+    sqr512_offdiag_bounded_asm(o, a);
+    if (__builtin_expect(__any(max(a[0], a[7]) > MUL_BOUNDED_WORD), 0)) sqr512_offdiag_asm(o, a);
 #else
     uint64_t acc = 0;
     uint32_t c2 = 0;

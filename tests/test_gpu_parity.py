@@ -694,6 +694,58 @@ def test_fold_corners_vs_reference_rule(bp):
         assert [int(x) for x in got[i]] == _ref_fold(t), (i, [hex(x) for x in t])
 
 
+@pytest.mark.parametrize("op", ["mul", "sq"])
+def test_bounded_product_gate(bp, oracle, op):
+    """mul512 / sqr512 run the bounded product (every column's first carry uncounted,
+    tools/gen_mul_asm.py BOUNDED) unless a lane's gating word — a[0] or b[7] (a[0] or a[7] for a
+    square) — exceeds 0xFFFFFFEF, when the wave runs the counting product.  Waves here: (1) every
+    gating word exactly at the bound with all other words 2^32 - 1 (the largest products the
+    bounded form meets); (2) one lane just above the bound (0xFFFFFFF0, 0xFFFFFFFF) at a rotating
+    position among bounded lanes; (3) all-ones operands.  Every lane equals the oracle's
+    fe25519_mul (== fe25519_sq, curve25519_ops.cu:93-149)."""
+    import torch
+    rng = np.random.default_rng(17 if op == "mul" else 18)
+    BOUND = 0xFFFFFFEF
+
+    def fe_words(words):
+        return np.array([words[2 * k] | (words[2 * k + 1] << 32) for k in range(4)], np.uint64)
+    a_l, b_l = [], []
+    for w in range(48):
+        for lane in range(64):
+            aw = [0xFFFFFFFF if rng.random() < 0.7 else int(rng.integers(0, 2**32)) for _ in range(8)]
+            bw = [0xFFFFFFFF if rng.random() < 0.7 else int(rng.integers(0, 2**32)) for _ in range(8)]
+            aw[0], bw[7] = BOUND - int(rng.integers(0, 3)), BOUND - int(rng.integers(0, 3))
+            if op == "sq":
+                aw[7] = BOUND - int(rng.integers(0, 3))
+            if w >= 16 and lane == (w * 37) % 64:   # one lane over the bound: the counting form
+                over = [0xFFFFFFF0, 0xFFFFFFFF][w % 2]
+                if w % 3 == 0:
+                    aw[0] = over
+                elif op == "mul":
+                    bw[7] = over
+                else:
+                    aw[7] = over
+            if w >= 40:
+                aw = [0xFFFFFFFF] * 8
+                bw = [0xFFFFFFFF] * 8
+            a_l.append(fe_words(aw))
+            b_l.append(fe_words(bw))
+    a, b = np.stack(a_l), np.stack(b_l)
+    if op == "sq":
+        b = a.copy()
+    dev = torch.device("cuda:0")
+    T = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(np.int64)).to(dev)
+    r = torch.empty(len(a), 4, dtype=torch.int64, device=dev)
+    if op == "sq":
+        bp.field_op("sq", r, T(a))
+    else:
+        bp.field_op("mul", r, T(a), T(b))
+    torch.cuda.synchronize()
+    got = r.cpu().numpy().view(np.uint64)
+    for i in range(len(a)):
+        assert np.array_equal(got[i], oracle.fe_mul(a[i], b[i])), i
+
+
 def _edge_cases(op, rng):
     """Operand pairs that put one lane on each rare edge the field asm tests for (fe_add_asm /
     fe_sub_asm / fe_fold_asm in field_asm.h): every exact-form branch taken by exactly the case

@@ -23,18 +23,24 @@ def offdiag(k):
     return [(i, k - i) for i in range(8) if i < k - i <= 7]
 
 
-def emit_column(k, prods=None, first=None):
+def emit_column(k, prods=None, first=None, bounded=False):
+    """One product-scanning column as asm lines.  bounded: the column's first product cannot carry
+    out of the 64-bit accumulator (the caller has checked the operand words that bound it, see
+    BOUNDED below), so only the later products' carries are counted.  Returns (prods, lines,
+    counted) with counted = the number of carries counted into c2 (0: c2 is not written)."""
     prods = column(k) if prods is None else prods
     first = (k == 0) if first is None else first
-    ins = []          # list of (text, writes_sgpr_idx or None, reads_sgpr_idx or None)
     need_carry = not first
-    pending = []      # (sgpr index, position written)
+    pending = []      # sgpr indices whose carry is still to be counted
     seq = []
+    counted = 0
     for t, (i, j) in enumerate(prods):
         s = t % 3
-        seq.append(("mad", i, j, s, t))
-        if need_carry:
+        skip = need_carry and bounded and t == 0
+        seq.append(("mad", i, j, "sd" if skip else f"s{s}", t))
+        if need_carry and not skip:
             pending.append(s)
+            counted += 1
         if len(pending) > 2:
             seq.append(("addc", pending.pop(0)))
     while need_carry and pending:
@@ -44,12 +50,13 @@ def emit_column(k, prods=None, first=None):
     first_addc = True
     for op in seq:
         if op[0] == "mad":
-            _, i, j, s, t = op
+            _, i, j, sname, t = op
             if first and t == 0:
-                lines.append(f"v_mad_u64_u32 %[acc], %[s{s}], %[a{i}], %[b{j}], 0")
+                lines.append(f"v_mad_u64_u32 %[acc], %[{sname}], %[a{i}], %[b{j}], 0")
             else:
-                lines.append(f"v_mad_u64_u32 %[acc], %[s{s}], %[a{i}], %[b{j}], %[acc]")
-            wpos[s] = pos
+                lines.append(f"v_mad_u64_u32 %[acc], %[{sname}], %[a{i}], %[b{j}], %[acc]")
+            if sname != "sd":
+                wpos[int(sname[1:])] = pos
             pos += 1
         else:
             s = op[1]
@@ -63,7 +70,59 @@ def emit_column(k, prods=None, first=None):
             else:
                 lines.append(f"v_addc_co_u32 %[c2], %[sd], %[c2], 0, %[s{s}]")
             pos += 1
-    return prods, lines
+    return prods, lines, counted
+
+
+# The bounded forms.  Column k's FIRST product is a_0 b_k (k <= 7) or a_(k-7) b_7 (k >= 8) (column()
+# and offdiag() list products in increasing i), and it is added to the previous column's carry-out
+# acc_start = hi + 2^32 c2 <= (2^32 - 1) + 2^32 (products of that column - 1) <= 2^35 - 1.  When the
+# gating words a_0 and b_7 (a_0 and a_7 for a square) are <= 0xFFFFFFEF, that product is at most
+# (2^32 - 1)(2^32 - 17) = 2^64 - 18 2^32 + 17, so acc_start + it < 2^64 - 10 2^32 + 17: no carry
+# out, and the column need not count it.  mul512 / sqr512 test the gating words wave-uniformly and
+# run the counting form when any lane exceeds the bound (probability ~2^-27 per lane).
+BOUNDED = 0xFFFFFFEF
+
+
+def emit_product(out, fname, sig, wname, cols, last, bounded=False, square=False, pre=()):
+    """One generated product function.  cols = [(k, prods, first)]: column k's words go to
+    wname[k]; `last` = the index of the final carry word (wname[last] = the accumulator's high part).
+    square: operand b is a (the off-diagonal half of a square)."""
+    out.append(f"__device__ __forceinline__ void {fname}({sig}) {{")
+    out.append("    uint64_t acc = 0, s0, s1, s2, sd;")
+    out.append("    uint32_t c2;")
+    out.extend(pre)
+    prev_counted = 0
+    for idx, (k, prods, first) in enumerate(cols):
+        _, lines, counted = emit_column(k, prods, first=first, bounded=bounded)
+        if idx > 0:   # the previous column's carry-out: (acc >> 32) + 2^32 (its counted carries)
+            out.append("    acc = (acc >> 32) | ((uint64_t)c2 << 32);" if prev_counted else "    acc >>= 32;")
+        ai = sorted({i for i, _ in prods} | ({j for _, j in prods} if square else set()))
+        bj = [] if square else sorted({j for _, j in prods})
+        body = "\\n\\t".join(lines)
+        if square:
+            body = body.replace("%[b", "%[a")
+        ops_in = ", ".join([f'[a{i}] "v"(a[{i}])' for i in ai] + [f'[b{j}] "v"(b[{j}])' for j in bj])
+        if first:
+            out.append(f'    asm volatile("{body}" : [acc] "=&v"(acc), [s0] "=&s"(s0) : {ops_in});')
+        elif counted:
+            out.append(f'    asm volatile("{body}"')
+            out.append(f'                 : [acc] "+v"(acc), [c2] "=&v"(c2), [s0] "=&s"(s0), [s1] "=&s"(s1), '
+                       f'[s2] "=&s"(s2), [sd] "=&s"(sd)')
+            out.append(f"                 : {ops_in});")
+        else:
+            out.append(f'    asm volatile("{body}"')
+            out.append(f'                 : [acc] "+v"(acc), [s0] "=&s"(s0), [s1] "=&s"(s1), [s2] "=&s"(s2), '
+                       f'[sd] "=&s"(sd)')
+            out.append(f"                 : {ops_in});")
+        out.append(f"    {wname}[{k}] = (uint32_t)acc;")
+        prev_counted = counted
+    out.append("    acc = (acc >> 32) | ((uint64_t)c2 << 32);" if prev_counted else "    acc >>= 32;")
+    out.append(f"    {wname}[{last}] = (uint32_t)acc;")
+    if square:
+        out.append(f"    {wname}[{last + 1}] = (uint32_t)(acc >> 32);")
+    out.append("    (void)s0; (void)s1; (void)s2; (void)sd; (void)c2;")
+    out.append("}")
+    out.append("")
 
 
 def main(path=OUT):
@@ -73,87 +132,28 @@ def main(path=OUT):
     out.append("#pragma once")
     out.append("#include <stdint.h>")
     out.append("namespace bp {")
-    out.append("__device__ __forceinline__ void mul512_asm(uint32_t w[16], const uint32_t a[8], const uint32_t b[8]) {")
-    out.append("    uint64_t acc = 0, s0, s1, s2, sd;")
-    out.append("    uint32_t c2;")
-    for k in range(15):
-        prods, lines = emit_column(k)
-        ai = sorted({i for i, _ in prods})
-        bj = sorted({j for _, j in prods})
-        body = "\\n\\t".join(lines)
-        ops_in = ", ".join([f'[a{i}] "v"(a[{i}])' for i in ai] + [f'[b{j}] "v"(b[{j}])' for j in bj])
-        if k == 0:
-            out.append(f'    asm volatile("{body}" : [acc] "=&v"(acc), [s0] "=&s"(s0) : {ops_in});')
-        else:
-            out.append(f'    asm volatile("{body}"')
-            out.append(f'                 : [acc] "+v"(acc), [c2] "=&v"(c2), [s0] "=&s"(s0), [s1] "=&s"(s1), '
-                       f'[s2] "=&s"(s2), [sd] "=&s"(sd)')
-            out.append(f"                 : {ops_in});")
-        out.append(f"    w[{k}] = (uint32_t)acc;")
-        if k == 0:
-            out.append("    acc >>= 32;")
-        else:
-            out.append("    acc = (acc >> 32) | ((uint64_t)c2 << 32);")
-    out.append("    w[15] = (uint32_t)acc;")
-    out.append("    (void)s0; (void)s1; (void)s2; (void)sd;")
-    out.append("}")
-    out.append("")
-    out.append("// Off-diagonal half of a square: o = sum_{i<j} a_i a_j 2^(32(i+j)), o[0] = 0 (columns 1..13).")
-    out.append("__device__ __forceinline__ void sqr512_offdiag_asm(uint32_t o[16], const uint32_t a[8]) {")
-    out.append("    uint64_t acc = 0, s0, s1, s2, sd;")
-    out.append("    uint32_t c2;")
-    out.append("    o[0] = 0;")
-    for k in range(1, 14):
-        prods = offdiag(k)
-        _, lines = emit_column(k, prods, first=(k == 1))
-        ai = sorted({i for i, _ in prods} | {j for _, j in prods})
-        body = "\\n\\t".join(lines)
-        ops_in = ", ".join([f'[a{i}] "v"(a[{i}])' for i in ai])
-        body = body.replace("%[b", "%[a")
-        if k == 1:
-            out.append(f'    asm volatile("{body}" : [acc] "=&v"(acc), [s0] "=&s"(s0) : {ops_in});')
-        else:
-            out.append(f'    asm volatile("{body}"')
-            out.append(f'                 : [acc] "+v"(acc), [c2] "=&v"(c2), [s0] "=&s"(s0), [s1] "=&s"(s1), '
-                       f'[s2] "=&s"(s2), [sd] "=&s"(sd)')
-            out.append(f"                 : {ops_in});")
-        out.append(f"    o[{k}] = (uint32_t)acc;")
-        if k == 1:
-            out.append("    acc >>= 32;")
-        else:
-            out.append("    acc = (acc >> 32) | ((uint64_t)c2 << 32);")
-    out.append("    o[14] = (uint32_t)acc;")
-    out.append("    o[15] = (uint32_t)(acc >> 32);")
-    out.append("    (void)s0; (void)s1; (void)s2; (void)sd;")
-    out.append("}")
-    out.append("")
+    out.append(f"// Gating-word bound of the *_bounded forms (tools/gen_mul_asm.py BOUNDED): every column's first")
+    out.append(f"// product is known not to carry out when the gating words are <= it, so it is not counted.")
+    out.append(f"constexpr uint32_t MUL_BOUNDED_WORD = 0x{BOUNDED:08X}u;")
+    full = [(k, column(k), k == 0) for k in range(15)]
+    for bounded, suffix in ((False, ""), (True, "_bounded")):
+        if bounded:
+            out.append("// The same product with the first carry of every column uncounted: valid when a[0] and b[7]")
+            out.append("// are <= MUL_BOUNDED_WORD (14 carry counts fewer).")
+        emit_product(out, f"mul512{suffix}_asm", "uint32_t w[16], const uint32_t a[8], const uint32_t b[8]", "w", full,
+                     15, bounded=bounded)
+    off = [(k, offdiag(k), k == 1) for k in range(1, 14)]
+    for bounded, suffix in ((False, ""), (True, "_bounded")):
+        out.append("// Off-diagonal half of a square: o = sum_{i<j} a_i a_j 2^(32(i+j)), o[0] = 0 (columns 1..13)"
+                   + (";" if bounded else "."))
+        if bounded:
+            out.append("// bounded: the first carry of every column uncounted, valid when a[0], a[7] <= MUL_BOUNDED_WORD.")
+        emit_product(out, f"sqr512_offdiag{suffix}_asm", "uint32_t o[16], const uint32_t a[8]", "o", off, 14,
+                     bounded=bounded, square=True, pre=("    o[0] = 0;",))
     out.append("// Two rows of the product for a lane quad that shares one multiplication: (a1 2^32 + a0) * b,")
     out.append("// the exact 320-bit partial as 10 words (columns 0..8 + the final carry word).")
-    out.append("__device__ __forceinline__ void mul2x8_asm(uint32_t w[10], const uint32_t a[2], const uint32_t b[8]) {")
-    out.append("    uint64_t acc = 0, s0, s1, s2, sd;")
-    out.append("    uint32_t c2;")
-    for k in range(9):
-        prods = [(i, k - i) for i in range(2) if 0 <= k - i <= 7]
-        _, lines = emit_column(k, prods, first=(k == 0))
-        ai = sorted({i for i, _ in prods})
-        bj = sorted({j for _, j in prods})
-        body = "\\n\\t".join(lines)
-        ops_in = ", ".join([f'[a{i}] "v"(a[{i}])' for i in ai] + [f'[b{j}] "v"(b[{j}])' for j in bj])
-        if k == 0:
-            out.append(f'    asm volatile("{body}" : [acc] "=&v"(acc), [s0] "=&s"(s0) : {ops_in});')
-        else:
-            out.append(f'    asm volatile("{body}"')
-            out.append(f'                 : [acc] "+v"(acc), [c2] "=&v"(c2), [s0] "=&s"(s0), [s1] "=&s"(s1), '
-                       f'[s2] "=&s"(s2), [sd] "=&s"(sd)')
-            out.append(f"                 : {ops_in});")
-        out.append(f"    w[{k}] = (uint32_t)acc;")
-        if k == 0:
-            out.append("    acc >>= 32;")
-        else:
-            out.append("    acc = (acc >> 32) | ((uint64_t)c2 << 32);")
-    out.append("    w[9] = (uint32_t)acc;")
-    out.append("    (void)s0; (void)s1; (void)s2; (void)sd;")
-    out.append("}")
+    rows2 = [(k, [(i, k - i) for i in range(2) if 0 <= k - i <= 7], k == 0) for k in range(9)]
+    emit_product(out, "mul2x8_asm", "uint32_t w[10], const uint32_t a[2], const uint32_t b[8]", "w", rows2, 9)
     out.append("}  // namespace bp")
     open(path, "w").write("\n".join(out) + "\n")
     print("wrote", path)
