@@ -254,8 +254,12 @@ BP_DEV void mul512(uint64_t t[8], const fe& f, const fe& g) {
         b[2 * i + 1] = (uint32_t)(g.v[i] >> 32);
     }
 #if BP_MUL_ASM && defined(__HIP_DEVICE_COMPILE__)   // host pass: the C form (host-side checks)
-    // bounded form (every column's first carry uncounted, mul512_asm.h) unless a lane's gating words
-    // a[0], b[7] exceed MUL_BOUNDED_WORD (wave-uniform test; ~2^-27 per lane): then the counting form
+    // bounded form (the first carry of every column uncounted, mul512_asm.h) unless a lane's gating
+    // words a[0], b[7] exceed MUL_BOUNDED_WORD (a wave-uniform test; ~2^-27 per lane): then the
+    // counting form recomputes the product (out of line).  (A form that also left the second carry
+    // of columns 7..13 uncounted, gated on top words <= 0x7FFFFFEF, ran at 123 K vs 202 K verifies/s:
+    // this arithmetic's values are not reduced below 2^255, so that gate failed in most waves,
+    // profiles/ab/r05d_bounded2.json.)
     mul512_bounded_asm(w, a, b);
     if (__builtin_expect(__any(max(a[0], b[7]) > MUL_BOUNDED_WORD), 0)) mul512_asm(w, a, b);
 #else

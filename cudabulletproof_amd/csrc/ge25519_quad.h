@@ -71,7 +71,8 @@ __device__ __forceinline__ fe fe_mul_q4(const fe& x, const fe& y) {
         b[2 * i] = (uint32_t)y.v[i];
         b[2 * i + 1] = (uint32_t)(y.v[i] >> 32);
     }
-    mul2x8_asm(w, a, b);
+    mul2x8_bounded_asm(w, a, b);   // the counting form when a lane's a[0] exceeds the bound (mul512_asm.h)
+    if (__builtin_expect(__any(a[0] > MUL_BOUNDED_WORD), 0)) mul2x8_asm(w, a, b);
     // lanes 0, 2: q = own partial + the next lane's partial at +2 words (12 words)
     uint32_t n1[10];
 #pragma unroll

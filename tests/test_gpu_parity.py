@@ -696,36 +696,36 @@ def test_fold_corners_vs_reference_rule(bp):
 
 @pytest.mark.parametrize("op", ["mul", "sq"])
 def test_bounded_product_gate(bp, oracle, op):
-    """mul512 / sqr512 run the bounded product (every column's first carry uncounted,
-    tools/gen_mul_asm.py BOUNDED) unless a lane's gating word — a[0] or b[7] (a[0] or a[7] for a
-    square) — exceeds 0xFFFFFFEF, when the wave runs the counting product.  Waves here: (1) every
-    gating word exactly at the bound with all other words 2^32 - 1 (the largest products the
-    bounded form meets); (2) one lane just above the bound (0xFFFFFFF0, 0xFFFFFFFF) at a rotating
-    position among bounded lanes; (3) all-ones operands.  Every lane equals the oracle's
-    fe25519_mul (== fe25519_sq, curve25519_ops.cu:93-149)."""
+    """mul512 / sqr512 run the bounded products (tools/gen_mul_asm.py: the first carry of every
+    column uncounted) unless a lane's gating words exceed 0xFFFFFFEF — mul: a[0] or b[7]; sq: a[0]
+    or a[7] — when the wave runs the counting product.
+    Waves here: (1) every gating word at or just under its bound with all other words 2^32 - 1 (the
+    largest products the bounded forms meet); (2) one lane just over a bound at a rotating position
+    among such lanes; (3) all-ones operands.  Every lane equals the oracle's fe25519_mul
+    (== fe25519_sq, curve25519_ops.cu:93-149)."""
     import torch
     rng = np.random.default_rng(17 if op == "mul" else 18)
-    BOUND = 0xFFFFFFEF
+    LOW = 0xFFFFFFEF
+    TOP = 0xFFFFFFEF
 
     def fe_words(words):
         return np.array([words[2 * k] | (words[2 * k + 1] << 32) for k in range(4)], np.uint64)
     a_l, b_l = [], []
-    for w in range(48):
+    for w in range(64):
         for lane in range(64):
             aw = [0xFFFFFFFF if rng.random() < 0.7 else int(rng.integers(0, 2**32)) for _ in range(8)]
             bw = [0xFFFFFFFF if rng.random() < 0.7 else int(rng.integers(0, 2**32)) for _ in range(8)]
-            aw[0], bw[7] = BOUND - int(rng.integers(0, 3)), BOUND - int(rng.integers(0, 3))
-            if op == "sq":
-                aw[7] = BOUND - int(rng.integers(0, 3))
-            if w >= 16 and lane == (w * 37) % 64:   # one lane over the bound: the counting form
-                over = [0xFFFFFFF0, 0xFFFFFFFF][w % 2]
-                if w % 3 == 0:
-                    aw[0] = over
-                elif op == "mul":
-                    bw[7] = over
+            aw[0] = LOW - int(rng.integers(0, 3))
+            aw[7], bw[7] = TOP - int(rng.integers(0, 3)), TOP - int(rng.integers(0, 3))
+            if 16 <= w < 56 and lane == (w * 37) % 64:   # one lane over a bound: the counting form
+                which = w % 3
+                if which == 0:
+                    aw[0] = [LOW + 1, 0xFFFFFFFF][w % 2]
+                elif which == 1:
+                    aw[7] = [TOP + 1, 0xFFFFFFFF][w % 2]
                 else:
-                    aw[7] = over
-            if w >= 40:
+                    bw[7] = [TOP + 1, 0xFFFFFFFF][w % 2]
+            if w >= 56:
                 aw = [0xFFFFFFFF] * 8
                 bw = [0xFFFFFFFF] * 8
             a_l.append(fe_words(aw))

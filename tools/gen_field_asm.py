@@ -195,9 +195,9 @@ def gen_add():
 
 
 def gen_fold():
-    """Two wave-uniform branches: (1) some x_i (i = 1..3) may be 2^64-1 (its low word is), so the
-    lossy carry can differ from the true one -> the exact chain + exact fix-up; else the plain
-    carry chain, then (2) fix_test -> fast or exact fix-up."""
+    """One wave-uniform branch after the plain carry chain: if some x_i (i = 1..3) may be 2^64-1
+    (its low word is: the lossy carry can differ from the true one) or fix_test's edge words are
+    all ones, the exact chain (from the inputs again) + exact fix-up; else the fast fix-up."""
     h = [f"h{i}" for i in range(8)]
     test1 = [V("v_max3_u32 %[vt3], %[x2], %[x4], %[x6]"),
              V("v_cmp_eq_u32 %[srare], -1, %[vt3]", ["srare"])]
@@ -216,14 +216,20 @@ def gen_fold():
                        ["sk1"], ["sk0"]))
         exact.append(S(f"s_and_b64 %[sq{i}], %[sq{i}], %[scy]", [f"sq{i}"]))   # x_i == M & carry-in
         exact.append(S(f"s_andn2_b64 %[scy], %[sk1], %[sq{i}]", ["scy"]))      # the reference's carry
-    # layout: test1, branch -> 5 (exact chain); plain chain, fix_test, branch -> 3 (exact fix);
-    # fast fix, s_branch 4; 5: exact chain (falls through); 3: exact fix; 4: end
-    l1, s1 = schedule(test1 + [S("s_cmp_lg_u64 %[srare], 0"), S("s_cbranch_scc1 5f")])
-    l2, s2 = schedule(plain + fix_test(h, "scy") + branch_if_rare("3f"), s1)
+    # one wave-uniform test for both rare edges: the plain chain runs first; max3 of the x words the
+    # lossy-carry test reads and of the words fix_test reads, then one compare.  Layout: plain chain,
+    # tests, branch -> 3; fast fix, s_branch 4; 3: exact chain (recomputed from the inputs) + exact
+    # fix; 4: end
+    both = [V("v_max3_u32 %[vt3], %[x2], %[x4], %[x6]"),
+            V(f"v_max3_u32 %[vt3], %[vt3], %[{h[1]}], %[{h[4]}]"),
+            V(f"v_cmp_gt_i32 %[stp], 0, %[{h[7]}]", ["stp"]),
+            V("v_cmp_eq_u32 %[srare], -1, %[vt3]", ["srare"]),
+            S(f"s_or_b64 %[sm], {cref('scy')}, %[stp]", ["sm"])]
+    l2, s2 = schedule(plain + both + branch_if_rare("3f"))
     l3, _ = schedule(fix_fast(h), s2)
-    l5, s5 = schedule(exact, s1)
-    l6, _ = schedule(fix_seq(h, h, "scy"), merge(s2, s5))
-    lines = l1 + l2 + l3 + ["s_branch 4f", "5:"] + l5 + ["3:"] + l6 + ["4:"]
+    l5, s5 = schedule(exact, s2)
+    l6, _ = schedule(fix_seq(h, h, "scy"), s5)
+    lines = l2 + l3 + ["s_branch 4f", "3:"] + l5 + l6 + ["4:"]
     return emit("fe_fold_asm", ["Fold of the exact 512-bit product (curve25519_ops.cu:114-145): t_lo as halves",
                                 "ta[0..7], x_i = lo64(19 t_{i+4}) as halves xa[0..7]; carry chain with the lossy",
                                 "carry cy_i = c_i & !(x_i == 2^64-1 & cy_{i-1}), then the fix-up.  The plain",

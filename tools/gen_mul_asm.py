@@ -24,10 +24,11 @@ def offdiag(k):
 
 
 def emit_column(k, prods=None, first=None, bounded=False):
-    """One product-scanning column as asm lines.  bounded: the column's first product cannot carry
-    out of the 64-bit accumulator (the caller has checked the operand words that bound it, see
-    BOUNDED below), so only the later products' carries are counted.  Returns (prods, lines,
-    counted) with counted = the number of carries counted into c2 (0: c2 is not written)."""
+    """One product-scanning column as asm lines.  bounded (an int, True = 1): that many leading
+    products of the column cannot carry out of the 64-bit accumulator (the caller has checked the
+    operand words that bound them, see BOUNDED below), so only the later products' carries are
+    counted.  Returns (prods, lines, counted) with counted = the number of carries counted into c2
+    (0: c2 is not written)."""
     prods = column(k) if prods is None else prods
     first = (k == 0) if first is None else first
     need_carry = not first
@@ -36,7 +37,7 @@ def emit_column(k, prods=None, first=None, bounded=False):
     counted = 0
     for t, (i, j) in enumerate(prods):
         s = t % 3
-        skip = need_carry and bounded and t == 0
+        skip = need_carry and t < int(bounded)
         seq.append(("mad", i, j, "sd" if skip else f"s{s}", t))
         if need_carry and not skip:
             pending.append(s)
@@ -83,7 +84,7 @@ def emit_column(k, prods=None, first=None, bounded=False):
 BOUNDED = 0xFFFFFFEF
 
 
-def emit_product(out, fname, sig, wname, cols, last, bounded=False, square=False, pre=()):
+def emit_product(out, fname, sig, wname, cols, last, bounded=False, square=False, pre=(), uncounted=None):
     """One generated product function.  cols = [(k, prods, first)]: column k's words go to
     wname[k]; `last` = the index of the final carry word (wname[last] = the accumulator's high part).
     square: operand b is a (the off-diagonal half of a square)."""
@@ -93,7 +94,7 @@ def emit_product(out, fname, sig, wname, cols, last, bounded=False, square=False
     out.extend(pre)
     prev_counted = 0
     for idx, (k, prods, first) in enumerate(cols):
-        _, lines, counted = emit_column(k, prods, first=first, bounded=bounded)
+        _, lines, counted = emit_column(k, prods, first=first, bounded=uncounted(k) if uncounted else bounded)
         if idx > 0:   # the previous column's carry-out: (acc >> 32) + 2^32 (its counted carries)
             out.append("    acc = (acc >> 32) | ((uint64_t)c2 << 32);" if prev_counted else "    acc >>= 32;")
         ai = sorted({i for i, _ in prods} | ({j for _, j in prods} if square else set()))
@@ -152,8 +153,14 @@ def main(path=OUT):
                      bounded=bounded, square=True, pre=("    o[0] = 0;",))
     out.append("// Two rows of the product for a lane quad that shares one multiplication: (a1 2^32 + a0) * b,")
     out.append("// the exact 320-bit partial as 10 words (columns 0..8 + the final carry word).")
+    # column 8's single product a_1 b_7 never carries out in either form: the partial is < 2^320
     rows2 = [(k, [(i, k - i) for i in range(2) if 0 <= k - i <= 7], k == 0) for k in range(9)]
-    emit_product(out, "mul2x8_asm", "uint32_t w[10], const uint32_t a[2], const uint32_t b[8]", "w", rows2, 9)
+    emit_product(out, "mul2x8_asm", "uint32_t w[10], const uint32_t a[2], const uint32_t b[8]", "w", rows2, 9,
+                 uncounted=lambda k: 1 if k == 8 else 0)
+    out.append("// bounded: each column's first product a_0 b_k uncounted (columns 1..7 keep one count), valid when")
+    out.append("// a[0] <= MUL_BOUNDED_WORD (acc_start <= 2^33 - 1 here: at most one counted carry per column).")
+    emit_product(out, "mul2x8_bounded_asm", "uint32_t w[10], const uint32_t a[2], const uint32_t b[8]", "w", rows2,
+                 9, uncounted=lambda k: 1)
     out.append("}  // namespace bp")
     open(path, "w").write("\n".join(out) + "\n")
     print("wrote", path)
