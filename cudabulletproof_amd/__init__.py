@@ -23,7 +23,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB_PATH = os.path.join(HERE, "libcudabulletproof_hip.so")
 CSRC = os.path.join(HERE, "csrc")
-SOURCES = ["bp_kernels.hip", "bp_prove.hip", "bp_pippenger.hip", "bp_capi.hip"]
+SOURCES = ["bp_terms1.hip", "bp_terms2.hip", "bp_terms4.hip", "bp_terms16.hip", "bp_kernels.hip", "bp_prove.hip",
+           "bp_pippenger.hip", "bp_capi.hip"]
 
 _lib = None
 

@@ -225,6 +225,15 @@ void launch_prefix_tables(ge* tab, const ge* G, const ge* H, const ge* h, const 
 // whose chain regions take 4 lanes per proof too; 16: 16-lane rows, chains on quads), k_terms<ql>
 void launch_terms(const RegionList& rl, const SlotDev* slots, const ge* G, const ge* H, const ge* g, const ge* h,
                   const ge* dtab, const fe* two_i, hipStream_t s, int ql = 1);
+// per tick form (bp_terms1.hip, bp_terms2.hip, bp_terms4.hip, bp_terms16.hip): k_terms<1 | 2 | 4 | 16>
+#define BP_DECL_TERMS(Q)                                                                                    \
+    void launch_terms##Q(const RegionList& rl, const SlotDev* slots, const ge* G, const ge* H, const ge* g,  \
+                         const ge* h, const ge* dtab, const fe* two_i, hipStream_t s, unsigned lds_pad);
+BP_DECL_TERMS(1)
+BP_DECL_TERMS(2)
+BP_DECL_TERMS(4)
+BP_DECL_TERMS(16)
+#undef BP_DECL_TERMS
 inline bool region_is_sm(int kind) {
     return kind == RK_STAGE0 || kind == RK_ROUND || kind == RK_FINAL_TERMS || kind == RK_M3 || kind == RK_MSMT;
 }
