@@ -120,7 +120,7 @@ struct EventTimer {
     }
 };
 
-// Per-device state. Tables are built on first use (k_init_tables) and cached.
+// Per-device state. Tables are built on first use (k_init_dtab, k_init_two) and cached.
 struct Engine {
     EventTimer timer;
     int device = -1;
@@ -179,17 +179,28 @@ struct Engine {
         device = dev;
         if ((e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking)) != hipSuccess) return e;
         if ((e = hipMalloc(&dtab, 258 * sizeof(bp::ge))) != hipSuccess) return e;   // + [257] = N_host([256])
-        return ensure_two(4096);
+        bp::launch_init_dtab(dtab, stream);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        return ensure_two(64);   // grows with the largest n a call brings (the first call's path stays short)
     }
+    // two_i[0..n): a grow-only table; growth copies the existing entries and continues the chain.  The
+    // old buffer is freed after the engine stream has synchronised (hipFree waits for the device).
     hipError_t ensure_two(int n) {
         if (n <= two_cap) return hipSuccess;
         hipError_t e;
-        if (two_i && (e = hipFree(two_i)) != hipSuccess) return e;
-        if ((e = hipMalloc(&two_i, (size_t)n * sizeof(bp::fe))) != hipSuccess) return e;
-        two_cap = n;
-        bp::launch_init_tables(dtab, two_i, n, stream);
+        const int cap = std::max(n, 2 * two_cap);
+        bp::fe* nt = nullptr;
+        if ((e = hipMalloc(&nt, (size_t)cap * sizeof(bp::fe))) != hipSuccess) return e;
+        if (two_i && (e = hipMemcpyAsync(nt, two_i, (size_t)two_cap * sizeof(bp::fe), hipMemcpyDeviceToDevice,
+                                         stream)) != hipSuccess)
+            return e;
+        bp::launch_init_two(nt, two_cap, cap, stream);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-        return hipStreamSynchronize(stream);
+        if ((e = hipStreamSynchronize(stream)) != hipSuccess) return e;
+        if (two_i && (e = hipFree(two_i)) != hipSuccess) return e;
+        two_i = nt;
+        two_cap = cap;
+        return hipSuccess;
     }
 };
 
@@ -358,6 +369,10 @@ struct Pipeline {
     // (configs[4]'s shards) the rounds that would run half empty before the latency-bound last
     // ticks carry the MSM work instead.  Needs the lane trees (n <= 64) and L >= 2.
     bool defer_msm = false;
+    // k_terms<1> blocks of per-lane scalar multiplications regroup their items by phase (bp_verify_dev.h
+    // sm_regroup): HIPBP_REGROUP=1 turns it on (A/B: slower, profiles/ab/r05i_regroup.json); xscr is its per-lane q / scalar scratch
+    bool regroup = false;
+    Buf xscr;
     // drain-tick forms (push): HIPBP_QUAD forces lanes (0) / quads (1) / pairs (2) on every tick
     // (-1: by size), HIPBP_QUAD_MAX_ITEMS / HIPBP_PAIR_MAX_ITEMS move the size bounds
     int quad_force = -1;
@@ -400,6 +415,8 @@ struct Pipeline {
         row_max = rm ? strtoull(rm, nullptr, 10) : ROW_MAX_ITEMS;
         quad_max = qm ? strtoull(qm, nullptr, 10) : QUAD_MAX_ITEMS;
         pair_max = pm ? strtoull(pm, nullptr, 10) : PAIR_MAX_ITEMS;
+        const char* rgp = getenv("HIPBP_REGROUP");
+        regroup = rgp && atoi(rgp) != 0;
         const char* dm = getenv("HIPBP_DEFER_MSM");
         defer_msm = dm && atoi(dm) != 0;
         if (const char* sp = getenv("HIPBP_DEFER_SPAN")) {
@@ -443,6 +460,7 @@ struct Pipeline {
         if (sort_bins.p) (void)hipFree(sort_bins.p);
         if (sort_offs.p) (void)hipFree(sort_offs.p);
         if (ptab.p) (void)hipFree(ptab.p);
+        if (xscr.p) (void)hipFree(xscr.p);
     }
     // The batch's per-lane item sets (stage 0's per-lane part, the rounds whose scalar runs are
     // shorter than a wave, the final terms), their lane-order buffers and the sort plan.
@@ -647,7 +665,12 @@ struct Pipeline {
         // Between the two (up to PAIR_MAX_ITEMS), lane pairs (HIPBP_QUAD=2 forces them,
         // HIPBP_PAIR_MAX_ITEMS sets the bound).
         int ql = sm_items <= row_max ? 16 : sm_items <= quad_max ? 4 : sm_items <= pair_max ? 2 : 1;
-        if (!sm_items) ql = 4;   // a tick of chains alone: the chains on quads
+        if (!sm_items) {   // a tick of chains alone: the chains on quads, in the row-form kernel when the
+            // tick is small (a one-proof call's ticks then load one tick code object, not two)
+            unsigned long long chain_items = 0;
+            for (int k = 0; k < tr.count; k++) chain_items += tr.reg[k].items;
+            ql = chain_items <= row_max ? 16 : 4;
+        }
         if (quad_force >= 0) ql = quad_force;
         if (ql > 1) {   // re-lay the regions: scalar-multiplication items ql lanes each
             unsigned long long tot = 0;
@@ -661,6 +684,16 @@ struct Pipeline {
             tr.total = tot;
         }
         if (tr.total >= (1ull << 32)) { g_err = "pipeline tick exceeds 2^32 lanes (batch too large for n)"; return HIPBP_ERR_ARG; }
+        if (ql == 1 && regroup) {   // k_terms<1>'s regrouped blocks: a q / scalar record per tick lane
+            const size_t qb = (size_t)tr.total * sizeof(bp::geq), need = qb + (size_t)tr.total * sizeof(bp::fe);
+            if (need > xscr.cap) {   // the pipeline's earlier ticks may still read the old scratch
+                BP_RET_ON(hipStreamSynchronize(s));
+                BP_RET_ON(xscr.need(std::max(need, 2 * xscr.cap)));
+            }
+            tr.regroup = 1;
+            tr.xq = xscr.as<bp::geq>();
+            tr.xs = (bp::fe*)(xscr.as<uint8_t>() + qb);
+        }
         if (tm) tm->mark(bp::KT_TERMS, false, s);
         bp::launch_terms(tr, slots_dev, G, H, g ? g : h, h, e->dtab, e->two_i, s, ql);
         if (tm) tm->mark(bp::KT_TERMS, true, s);

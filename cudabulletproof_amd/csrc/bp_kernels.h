@@ -7,6 +7,7 @@
 namespace bp {
 struct fe;
 struct ge;
+struct geq;
 
 // Device view of a batch of range proofs in the flat wire format (include/cudabulletproof_hip.h).
 struct BatchView {
@@ -209,15 +210,18 @@ constexpr int LANE_TREE_MAX = 64;
 constexpr int MAX_REGIONS = 24;   // >= log2(MAX_N) + 3 stages in flight + 3 stages with 2 regions
 struct RegionList {
     int count;
-    int pad;
+    int regroup;   // k_terms<1>: blocks of per-lane scalar-multiplications regroup their items by phase
     unsigned long long total;
+    geq* xq;       // regroup scratch, one record per tick lane: the item's q-side operands ...
+    fe* xs;        // ... and its scalar (read by whichever lane holds the item)
     Region reg[MAX_REGIONS];
 };
 
 // Kernel groups of the verify pipeline, for per-kernel HIP-event timing (bench.py roofline).
 enum KernelKind { KT_PREP = 0, KT_TERMS, KT_TREE, KT_COMBINE, KT_COUNT };
 
-void launch_init_tables(ge* dtab, fe* two_i, int nmax, hipStream_t s);
+void launch_init_dtab(ge* dtab, hipStream_t s);                       // dtab[0..257]
+void launch_init_two(fe* two_i, int from, int to, hipStream_t s);     // two_i[from..to)
 // Prefix tables (SlotDev::ptab) of the bases G[0..n), H[0..n), h, g (g nullable: its rows are
 // left unwritten): tab[(2n + 2) << K].
 void launch_prefix_tables(ge* tab, const ge* G, const ge* H, const ge* h, const ge* g, int n, int K, hipStream_t s);
