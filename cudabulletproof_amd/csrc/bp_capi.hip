@@ -369,10 +369,6 @@ struct Pipeline {
     // (configs[4]'s shards) the rounds that would run half empty before the latency-bound last
     // ticks carry the MSM work instead.  Needs the lane trees (n <= 64) and L >= 2.
     bool defer_msm = false;
-    // k_terms<1> blocks of per-lane scalar multiplications regroup their items by phase (bp_verify_dev.h
-    // sm_regroup): HIPBP_REGROUP=1 turns it on (A/B: slower, profiles/ab/r05i_regroup.json); xscr is its per-lane q / scalar scratch
-    bool regroup = false;
-    Buf xscr;
     // drain-tick forms (push): HIPBP_QUAD forces lanes (0) / quads (1) / pairs (2) on every tick
     // (-1: by size), HIPBP_QUAD_MAX_ITEMS / HIPBP_PAIR_MAX_ITEMS move the size bounds
     int quad_force = -1;
@@ -415,8 +411,6 @@ struct Pipeline {
         row_max = rm ? strtoull(rm, nullptr, 10) : ROW_MAX_ITEMS;
         quad_max = qm ? strtoull(qm, nullptr, 10) : QUAD_MAX_ITEMS;
         pair_max = pm ? strtoull(pm, nullptr, 10) : PAIR_MAX_ITEMS;
-        const char* rgp = getenv("HIPBP_REGROUP");
-        regroup = rgp && atoi(rgp) != 0;
         const char* dm = getenv("HIPBP_DEFER_MSM");
         defer_msm = dm && atoi(dm) != 0;
         if (const char* sp = getenv("HIPBP_DEFER_SPAN")) {
@@ -460,7 +454,6 @@ struct Pipeline {
         if (sort_bins.p) (void)hipFree(sort_bins.p);
         if (sort_offs.p) (void)hipFree(sort_offs.p);
         if (ptab.p) (void)hipFree(ptab.p);
-        if (xscr.p) (void)hipFree(xscr.p);
     }
     // The batch's per-lane item sets (stage 0's per-lane part, the rounds whose scalar runs are
     // shorter than a wave, the final terms), their lane-order buffers and the sort plan.
@@ -684,16 +677,6 @@ struct Pipeline {
             tr.total = tot;
         }
         if (tr.total >= (1ull << 32)) { g_err = "pipeline tick exceeds 2^32 lanes (batch too large for n)"; return HIPBP_ERR_ARG; }
-        if (ql == 1 && regroup) {   // k_terms<1>'s regrouped blocks: a q / scalar record per tick lane
-            const size_t qb = (size_t)tr.total * sizeof(bp::geq), need = qb + (size_t)tr.total * sizeof(bp::fe);
-            if (need > xscr.cap) {   // the pipeline's earlier ticks may still read the old scratch
-                BP_RET_ON(hipStreamSynchronize(s));
-                BP_RET_ON(xscr.need(std::max(need, 2 * xscr.cap)));
-            }
-            tr.regroup = 1;
-            tr.xq = xscr.as<bp::geq>();
-            tr.xs = (bp::fe*)(xscr.as<uint8_t>() + qb);
-        }
         if (tm) tm->mark(bp::KT_TERMS, false, s);
         bp::launch_terms(tr, slots_dev, G, H, g ? g : h, h, e->dtab, e->two_i, s, ql);
         if (tm) tm->mark(bp::KT_TERMS, true, s);

@@ -7,7 +7,6 @@
 namespace bp {
 struct fe;
 struct ge;
-struct geq;
 
 // Device view of a batch of range proofs in the flat wire format (include/cudabulletproof_hip.h).
 struct BatchView {
@@ -210,10 +209,8 @@ constexpr int LANE_TREE_MAX = 64;
 constexpr int MAX_REGIONS = 24;   // >= log2(MAX_N) + 3 stages in flight + 3 stages with 2 regions
 struct RegionList {
     int count;
-    int regroup;   // k_terms<1>: blocks of per-lane scalar-multiplications regroup their items by phase
+    int pad;
     unsigned long long total;
-    geq* xq;       // regroup scratch, one record per tick lane: the item's q-side operands ...
-    fe* xs;        // ... and its scalar (read by whichever lane holds the item)
     Region reg[MAX_REGIONS];
 };
 

@@ -448,134 +448,6 @@ __device__ __forceinline__ void poly_task(const SlotDev& sd, size_t p) {
     }
 }
 
-// ------------------------------------------------------------------ regrouped per-lane scalar mults
-// k_terms<1> blocks whose 256 lanes all run per-lane scalar multiplications (sm_lane_loop: one
-// ge25519_add per step, add(r, r) or add(r, P) per lane, the unified step ge_add_sel paying for both
-// forms) regroup their items by phase every step: each item's state (the point and its bit cursor)
-// moves through LDS so that the doublings come first, then the adds, then the finished items; waves
-// that hold only doublings run ge_dbl (its squares), only adds ge_add_qp, and at most two waves per
-// block (the boundaries) the unified step.  Each item runs the reference's operations in the
-// reference's order (curve25519_ops.cu:397-415), so the bits are sm_lane_loop's.  The q-side operands
-// and the scalar stay in a global scratch record (RegionList::xq / xs, one per tick lane) that
-// whichever lane holds the item reads: q at its point of use in an add, one scalar word per step.
-// Two barriers per step: wave counts -> ranks -> records written; then records read.
-constexpr int XW = 36;   // dwords per exchange record: the point (32) + meta (1), 16-B aligned
-constexpr size_t XBUF_BYTES = (size_t)TPB * XW * 4 + 2 * (TPB / 64) * 4 * 4;   // records + 2 x wave counts
-
-__device__ __forceinline__ void x_put(uint8_t* smem, int slot, const ge& r, uint32_t meta) {
-    uint4* rec = reinterpret_cast<uint4*>(smem) + (size_t)slot * (XW / 4);
-    const fe* c[4] = {&r.X, &r.Y, &r.Z, &r.T};
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const uint64_t a = c[k]->v[2 * h], b = c[k]->v[2 * h + 1];
-            rec[2 * k + h] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
-        }
-    reinterpret_cast<uint32_t*>(rec + 8)[0] = meta;
-}
-
-__device__ __forceinline__ uint32_t x_get(const uint8_t* smem, int slot, ge& r) {
-    const uint4* rec = reinterpret_cast<const uint4*>(smem) + (size_t)slot * (XW / 4);
-    fe* c[4] = {&r.X, &r.Y, &r.Z, &r.T};
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const uint4 u = rec[2 * k + h];
-            c[k]->v[2 * h] = (uint64_t)u.x | ((uint64_t)u.y << 32);
-            c[k]->v[2 * h + 1] = (uint64_t)u.z | ((uint64_t)u.w << 32);
-        }
-    return reinterpret_cast<const uint32_t*>(rec + 8)[0];
-}
-
-// meta: bit cursor i + 1 (0 = finished), add phase, home lane
-__device__ __forceinline__ uint32_t xm_pack(int i, bool add, int home) {
-    return (uint32_t)(i + 1) | (add ? 1u << 9 : 0u) | ((uint32_t)home << 16);
-}
-
-// Every active lane of the block calls this together (a block-uniform decision, k_terms<1>); active
-// lanes are the block's first `A` lanes, in its first `waves` waves (early-returned padding lanes
-// are its last ones).  live: this
-// lane has an item (s, P, its prefix table ptab / K); the result is this lane's own item's point.
-__device__ __forceinline__ ge sm_regroup(bool live, const fe& s, const ge& P, const ge* __restrict__ dtab,
-                                      const ge* ptab, int K, uint8_t* smem, geq* __restrict__ xq,
-                                      fe* __restrict__ xs, size_t gbase, int waves) {
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    uint32_t* cnt = reinterpret_cast<uint32_t*>(smem + (size_t)TPB * XW * 4);   // [2][waves][D, A, done, -]
-    ge r = ge_zero();
-    int i = -1;
-    if (live) {
-        const geq q = ge_prep(P);
-        xq[gbase + tid] = q;
-        xs[gbase + tid] = s;
-        const int lz = fe_clz256(s);
-        const bool pre = K > 0 && lz < K && ptab != nullptr;
-        r = ld_ge(pre ? &ptab[prefix_index(s, K)] : &dtab[lz]);
-        i = pre ? 255 - K : 255 - lz;
-    }
-    bool add = false;
-    int home = tid;
-    __syncthreads();   // every scratch record is written (vmcnt(0) before the barrier)
-    const uint32_t* sw = reinterpret_cast<const uint32_t*>(xs + gbase);   // 8 words per home lane
-    for (int par = 0;; par ^= 1) {
-        const int op = i < 0 ? 2 : (add ? 1 : 0);
-        const uint64_t mD = __ballot(op == 0), mA = __ballot(op == 1), mX = __ballot(op == 2);
-        if (lane == 0) {
-            uint32_t* c = cnt + (par * (TPB / 64) + w) * 4;
-            c[0] = (uint32_t)__popcll(mD);
-            c[1] = (uint32_t)__popcll(mA);
-            c[2] = (uint32_t)__popcll(mX);
-        }
-        __syncthreads();
-        int ND = 0, NA = 0, pD = 0, pA = 0, pX = 0;
-#pragma unroll
-        for (int v = 0; v < TPB / 64; v++) {
-            if (v >= waves) break;   // a wave past the region's end has returned: its words are stale
-            const uint32_t* c = cnt + (par * (TPB / 64) + v) * 4;
-            const int d = (int)c[0], a = (int)c[1], x = (int)c[2];
-            ND += d;
-            NA += a;
-            if (v < w) { pD += d; pA += a; pX += x; }
-        }
-        if (ND + NA == 0) break;   // block-uniform: every item finished
-        const uint64_t mine = op == 0 ? mD : op == 1 ? mA : mX;
-        const int rank = __popcll(mine & ((1ull << lane) - 1));
-        const int dest = op == 0 ? pD + rank : op == 1 ? ND + pA + rank : ND + NA + pX + rank;
-        x_put(smem, dest, r, xm_pack(i, add, home));
-        __syncthreads();
-        const uint32_t meta = x_get(smem, tid, r);
-        i = (int)(meta & 511) - 1;
-        add = (meta >> 9) & 1;
-        home = (int)(meta >> 16);
-        // this wave's lanes: [64 w, 64 w + 64) of D items [0, ND), add items [ND, ND + NA), finished after
-        const int lo = 64 * w, hi = lo + 64;
-        const bool hasD = lo < ND, hasA = lo < ND + NA && hi > ND;
-        if (!hasD && !hasA) continue;
-        const uint32_t word = i >= 0 ? sw[(size_t)home * 8 + (i >> 5)] : 0u;   // bit i: the D step's branch
-#ifdef BP_RG_HOTQ   // timing experiment only (wrong results): every add reads one hot record
-        const geq* q = xq + gbase;
-#else
-        const geq* q = xq + gbase + home;
-#endif
-        if (i >= 0) {
-            if (hasD && !hasA) r = ge_dbl(r);
-            else if (!hasD) r = ge_add_qp<true>(r, q, true);
-            else r = ge_add_sel<true, true>(r, q, add);
-            if (!add && ((word >> (i & 31)) & 1)) {
-                add = true;    // a set bit: its add(r, P) next
-            } else {
-                add = false;   // next bit
-                i--;
-            }
-        }
-    }
-    x_put(smem, home, r, 0);   // each item back to its home lane, whose job stores it
-    __syncthreads();
-    (void)x_get(smem, tid, r);
-    return r;
-}
-
 // One pipeline tick = ONE launch.  Every region is one in-flight batch at its own stage
 // (challenges / stage 0 / MSM trees / fold round r / final terms / final assembly), so a launch
 // carries a whole batch's worth of independent work however deep the batch-level dependency
@@ -603,12 +475,7 @@ __global__ BP_TERMS_BOUNDS void k_terms(RegionList rl, const SlotDev* __restrict
                                                const ge* __restrict__ G, const ge* __restrict__ H,
                                                const ge* __restrict__ g, const ge* __restrict__ h,
                                                const ge* __restrict__ dtab, const fe* __restrict__ two_i) {
-    // the q-operand slots (and RK_TREE's point array); k_terms<1>'s regrouped blocks use the same LDS
-    // for their exchange records
-    constexpr size_t QS_BYTES = (size_t)TPB * sizeof(geq);
-    constexpr size_t SMEM = QL == 1 && XBUF_BYTES > QS_BYTES ? XBUF_BYTES : QS_BYTES;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM];
-    geq* qs = reinterpret_cast<geq*>(smem);
+    __shared__ geq qs[TPB];
     size_t i = gid();
     if (i >= rl.total) return;
     const Region rg = find_region(rl, i);
@@ -652,8 +519,6 @@ __global__ BP_TERMS_BOUNDS void k_terms(RegionList rl, const SlotDev* __restrict
         // the scalar-multiplication kinds: fill the job, then the one call site
         SmJob jb;
         jb.base = -1;
-        jb.s = fe_set(0);   // (a padding lane's values: it votes in the regroup test below)
-        jb.P.Z = fe_set(1);
         bool live = true;
         uint32_t li = (uint32_t)l;   // < 2^32: Pipeline::push keeps a tick below 2^32 lanes
         if (QL == 16) li >>= 4;      // the row's / quad's / pair's item
@@ -674,45 +539,8 @@ __global__ BP_TERMS_BOUNDS void k_terms(RegionList rl, const SlotDev* __restrict
             if (sd.perm_ft) li = sd.perm_ft[li];
             final_terms_job(sd, li, G, H, jb);
         }
-        const ge* pt = (live && sd.ptab && jb.base >= 0) ? sd.ptab + ((size_t)jb.base << sd.pbits) : nullptr;
-        if (QL == 1 && rl.regroup) {
-            // regroup the block's items by phase when every one of its lanes is a scalar-multiplication
-            // lane of this region (block-uniform: the block's first and last lanes' regions), every
-            // item's P has Z = 1 (the add form reads no Z2) and some wave's scalars differ per lane
-            // (a block of wave-uniform scalars keeps sm_uniform's scalar branches)
-            const size_t b0 = (size_t)blockIdx.x * TPB;
-            const size_t b1 = (b0 + TPB < rl.total ? b0 + TPB : rl.total) - 1;
-            if (find_region(rl, b0).begin == rg.begin && find_region(rl, b1).begin == rg.begin) {
-                uint32_t same = 1;
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const uint32_t lo = (uint32_t)jb.s.v[k], hi = (uint32_t)(jb.s.v[k] >> 32);
-                    same &= (lo == __builtin_amdgcn_readfirstlane(lo)) & (hi == __builtin_amdgcn_readfirstlane(hi));
-                }
-                const bool zone_ok = !live || fe_is_one(jb.P.Z);
-                const bool per_lane = !__all(same);   // (padding lanes hold jb.s of no item: they vote per-lane)
-                // the block's vote through LDS: one word per wave (the waves past the region's end have
-                // returned: `waves` counts the others)
-                uint32_t* vote = reinterpret_cast<uint32_t*>(smem + (size_t)TPB * XW * 4);
-                const size_t end = rg.begin + rg.items < rl.total ? rg.begin + rg.items : rl.total;
-                const int waves = (int)((end - b0 + 63) >> 6) < TPB / 64 ? (int)((end - b0 + 63) >> 6) : TPB / 64;
-                const uint32_t mine = (__all(zone_ok) ? 1u : 0u) | (__any(per_lane) ? 2u : 0u);
-                if ((threadIdx.x & 63) == 0) vote[threadIdx.x >> 6] = mine;
-                __syncthreads();
-                uint32_t all_zone = 1, any_lane = 0;
-                for (int v = 0; v < waves; v++) {
-                    all_zone &= vote[v] & 1u;
-                    any_lane |= vote[v] >> 1;
-                }
-                // (sm_regroup's counts reuse these words only after its own first barrier)
-                if (all_zone && any_lane) {
-                    const ge t = sm_regroup(live, jb.s, jb.P, dtab, pt, pt ? sd.pbits : 0, smem, rl.xq, rl.xs, b0, waves);
-                    if (live) *jb.dst = jb.dev_norm ? ge_norm_dev(t) : ge_norm_host(t);
-                    return;
-                }
-            }
-        }
         if (live) {
+            const ge* pt = (sd.ptab && jb.base >= 0) ? sd.ptab + ((size_t)jb.base << sd.pbits) : nullptr;
             if (QL == 16) {
                 const ge t = sm_row(jb.s, jb.P, dtab, pt, pt ? sd.pbits : 0);
                 if ((threadIdx.x & 15) == 0) *jb.dst = jb.dev_norm ? ge_norm_dev(t) : ge_norm_host(t);
