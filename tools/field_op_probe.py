@@ -1,3 +1,5 @@
+"""Smoke each named batch field op (bp.field_op) on 1024 random elements, one line per op, stopping at the
+first failure (tools/, not a test): python tools/field_op_probe.py add sub mul ..."""
 import sys, os
 sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "."))
 import numpy as np, torch

@@ -1,3 +1,8 @@
+// probe_stream.hip — the HIP runtime's first-queue cost, apart from this library: device count,
+// one malloc, then (mode 0) hipStreamCreateWithFlags + a launch on it, or (mode 1) the first launch
+// on the null stream; then a second stream and a launch on it.  One JSON line, wall-clock ms.
+// Build: hipcc --offload-arch=gfx950 -O2 tools/probe_stream.hip -o build/probe_stream
+// (profiles/probe_stream_r05i.jsonl)
 #include <hip/hip_runtime.h>
 #include <chrono>
 #include <cstdio>
