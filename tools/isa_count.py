@@ -69,6 +69,8 @@ def main():
         cyc = sum(cost(i) * n for i, n in c.items() if not i.startswith(("global_", "ds_", "buffer_", "scratch_")))
         print(f"{name:14s} VALU {valu:5d}  ~cyc {cyc:7.0f}  s_nop {c['s_nop']:4d}  "
               f"SALU {sum(n for i, n in c.items() if i.startswith('s_') and i != 's_nop'):4d}  | {top}")
+        if os.environ.get("ISA_FULL") and os.environ["ISA_FULL"] in name:   # every VALU opcode of one kernel
+            print("    " + ", ".join(f"{k}:{v}" for k, v in sorted(c.items(), key=lambda kv: -kv[1]) if k.startswith("v_")))
 
 
 if __name__ == "__main__":
