@@ -1440,12 +1440,12 @@ def test_pipeline_lane_tree_knob_same_bits(bp, oracle, monkeypatch, n, B, lt):
                       G, H, g, h, step=1)
 
 
-@pytest.mark.parametrize("n,B,K", [(16, 70, 22), (16, 70, 23), (64, 40, 20)])
+@pytest.mark.parametrize("n,B,K", [(16, 70, 22), (16, 70, 23), (64, 40, 20), (64, 40, 21)])
 def test_pipeline_headline_table_width_same_bits(bp, oracle, n, B, K):
-    """The headline's table width (bench.py: K = 23 at n = 64, 140 GB): prefix tables of K = 20-23
-    bits through a generator set (as bench.py uses them) give the table-free pipeline's bits,
-    and a sample equals the oracle (n = 16 at K = 22 / 23: 18 / 36 GB of tables; n = 64 at K = 20:
-    17 GB)."""
+    """The headline's table width (bench.py DEFAULT_PREFIX_BITS: K = 21 at n = 64, 34.9 GB; round 4
+    ran K = 23): prefix tables of K = 20-23 bits through a generator set (as bench.py uses them) give
+    the table-free pipeline's bits, and a sample equals the oracle (n = 16 at K = 22 / 23: 18 / 36 GB
+    of tables; n = 64 at K = 20 / 21: 17 / 35 GB)."""
     import torch
     from cudabulletproof_amd import synth
     dev = torch.device("cuda:0")
