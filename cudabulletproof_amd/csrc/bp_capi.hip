@@ -120,7 +120,7 @@ struct EventTimer {
     }
 };
 
-// Per-device state. Tables are built on first use (k_init_dtab, k_init_two) and cached.
+// Per-device state. The identity-doubling and power-of-two tables are built on first use and cached.
 struct Engine {
     EventTimer timer;
     int device = -1;
@@ -178,25 +178,45 @@ struct Engine {
         if (e != hipSuccess) return e;
         device = dev;
         if ((e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking)) != hipSuccess) return e;
-        if ((e = hipMalloc(&dtab, 258 * sizeof(bp::ge))) != hipSuccess) return e;   // + [257] = N_host([256])
-        bp::launch_init_dtab(dtab, stream);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        return ensure_two(64);   // grows with the largest n a call brings (the first call's path stays short)
+        if ((e = hipMalloc(&dtab, 258 * sizeof(bp::ge))) != hipSuccess) return e;
+        // dtab[k] = the identity doubled k times (ge25519_scalarmult's leading zeros), [257] = the
+        // host-normalized [256]: computed here with the C forms of the same arithmetic (the device asm
+        // forms equal them bit for bit, tests/test_generated_asm.py, asm_check), so a one-proof call
+        // launches no set-up kernel and loads no code object besides its own ticks'
+        std::vector<bp::ge> t(258);
+        t[0] = bp::ge_zero();
+        for (int k = 1; k <= 256; k++) t[k] = bp::ge_add(t[k - 1], t[k - 1]);
+        t[257] = bp::ge_norm_host(t[256]);
+        if ((e = upload(dtab, t.data(), t.size() * sizeof(bp::ge))) != hipSuccess) return e;
+        return ensure_two(64);   // grows with the largest n a call brings
     }
-    // two_i[0..n): a grow-only table; growth copies the existing entries and continues the chain.  The
-    // old buffer is freed after the engine stream has synchronised (hipFree waits for the device).
+    // Host -> device (bytes a multiple of 16), synchronously: staged in the pinned buffer and read from
+    // there by a kernel (launch_upload), not by a copy-engine transfer (the process's first
+    // hipMemcpyAsync of these 33 KB cost ~7 ms on the first call's path).  The stream is drained
+    // first: a caller's own staged copy out of `pinned` may still be queued on it.
+    hipError_t upload(void* dst, const void* src, size_t bytes) {
+        hipError_t e;
+        if ((e = hipStreamSynchronize(stream)) != hipSuccess) return e;
+        if ((e = need_pinned(bytes)) != hipSuccess) return e;
+        memcpy(pinned, src, bytes);
+        bp::launch_upload(dst, pinned, bytes, stream);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        return hipStreamSynchronize(stream);
+    }
+    // two_i[i] = i successive fe_mul(., 2) from 1 (bulletproof_range_proof.cu:705-712): a grow-only
+    // table, extended on the host (C forms) and uploaded whole on growth.  The old device buffer is
+    // freed after the engine stream has synchronised (hipFree waits for the device).
+    std::vector<bp::fe> two_host;
     hipError_t ensure_two(int n) {
         if (n <= two_cap) return hipSuccess;
         hipError_t e;
         const int cap = std::max(n, 2 * two_cap);
+        const bp::fe two = bp::fe_add(bp::fe_set(1), bp::fe_set(1));
+        while ((int)two_host.size() < cap)
+            two_host.push_back(two_host.empty() ? bp::fe_set(1) : bp::fe_mul(two_host.back(), two));
         bp::fe* nt = nullptr;
         if ((e = hipMalloc(&nt, (size_t)cap * sizeof(bp::fe))) != hipSuccess) return e;
-        if (two_i && (e = hipMemcpyAsync(nt, two_i, (size_t)two_cap * sizeof(bp::fe), hipMemcpyDeviceToDevice,
-                                         stream)) != hipSuccess)
-            return e;
-        bp::launch_init_two(nt, two_cap, cap, stream);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        if ((e = hipStreamSynchronize(stream)) != hipSuccess) return e;
+        if ((e = upload(nt, two_host.data(), (size_t)cap * sizeof(bp::fe))) != hipSuccess) return e;
         if (two_i && (e = hipFree(two_i)) != hipSuccess) return e;
         two_i = nt;
         two_cap = cap;

@@ -217,8 +217,6 @@ struct RegionList {
 // Kernel groups of the verify pipeline, for per-kernel HIP-event timing (bench.py roofline).
 enum KernelKind { KT_PREP = 0, KT_TERMS, KT_TREE, KT_COMBINE, KT_COUNT };
 
-void launch_init_dtab(ge* dtab, hipStream_t s);                       // dtab[0..257]
-void launch_init_two(fe* two_i, int from, int to, hipStream_t s);     // two_i[from..to)
 // Prefix tables (SlotDev::ptab) of the bases G[0..n), H[0..n), h, g (g nullable: its rows are
 // left unwritten): tab[(2n + 2) << K].
 void launch_prefix_tables(ge* tab, const ge* G, const ge* H, const ge* h, const ge* g, int n, int K, hipStream_t s);
@@ -227,6 +225,9 @@ void launch_prefix_tables(ge* tab, const ge* G, const ge* H, const ge* h, const 
 void launch_terms(const RegionList& rl, const SlotDev* slots, const ge* G, const ge* H, const ge* g, const ge* h,
                   const ge* dtab, const fe* two_i, hipStream_t s, int ql = 1);
 // per tick form (bp_terms1.hip, bp_terms2.hip, bp_terms4.hip, bp_terms16.hip): k_terms<1 | 2 | 4 | 16>
+// dst[0..bytes) = src (device-visible pinned host memory), bytes a multiple of 16, by a kernel of the
+// row-form tick's code object (bp_terms16.hip)
+void launch_upload(void* dst, const void* src, size_t bytes, hipStream_t s);
 #define BP_DECL_TERMS(Q)                                                                                    \
     void launch_terms##Q(const RegionList& rl, const SlotDev* slots, const ge* G, const ge* H, const ge* g,  \
                          const ge* h, const ge* dtab, const fe* two_i, hipStream_t s, unsigned lds_pad);

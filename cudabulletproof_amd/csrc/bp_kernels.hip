@@ -7,7 +7,6 @@
 // the reference's order, because the arithmetic is not associative.
 #include "bp_kernels.h"
 #include "ge25519_dev.h"
-#include "ge25519_quad.h"
 #include "sha256_dev.h"
 
 namespace bp {
@@ -21,39 +20,7 @@ constexpr int TPB = 256;   // threads per block for lane-per-item kernels
 __device__ __forceinline__ size_t gid() { return (size_t)blockIdx.x * blockDim.x + threadIdx.x; }
 
 // ------------------------------------------------------------------ tables
-// dtab[k] = k successive ge25519_add(r, r) of the identity (0,1,1,0): the state of
-// ge25519_scalarmult after k leading zero bits (curve25519_ops.cu:399-414); dtab[257] =
-// ge25519_normalize(dtab[256]), the normalized result of any point times the zero scalar.
-// One wave; each lane quad runs the chain of doublings on ge_op_quad (3 product latencies per
-// doubling instead of 9: the table is on the first call's path), lane 0 stores.
-__global__ void k_init_dtab(ge* dtab) {
-    ge r = ge_zero();
-    if (threadIdx.x == 0) dtab[0] = r;
-    for (int k = 1; k <= 256; k++) {
-        r = ge_op_quad<true>(r, r);
-        if (threadIdx.x == 0) dtab[k] = r;
-    }
-    const ge nz = ge_norm_host(r);   // a zero scalar's host-normalized term, whatever the point
-    if (threadIdx.x == 0) dtab[257] = nz;
-}
-
-// two_i[i] = i successive fe_mul(., 2) from 1 (bulletproof_range_proof.cu:705-712), entries
-// [from, to): continues the chain from two_i[from - 1] (the table grows with the largest n seen).
-__global__ void k_init_two(fe* two_i, int from, int to) {
-    if (gid() != 0) return;
-    const fe two = fe_add(fe_set(1), fe_set(1));
-    fe t = from == 0 ? fe_set(1) : fe_mul(two_i[from - 1], two);
-    for (int i = from; i < to; i++) {
-        two_i[i] = t;
-        t = fe_mul(t, two);
-    }
-}
-
-void launch_init_dtab(ge* dtab, hipStream_t s) { k_init_dtab<<<1, 64, 0, s>>>(dtab); }
-void launch_init_two(fe* two_i, int from, int to, hipStream_t s) {
-    if (to > from) k_init_two<<<1, 64, 0, s>>>(two_i, from, to);
-}
-
+// (dtab, the identity-doubling table, and two_i are built on the host: bp_capi.hip Engine::init)
 // tab[b << K | p] = the first K steps of ge25519_scalarmult (curve25519_ops.cu:397-415) on base b
 // for a scalar whose top K bits are p, from the identity: one add(r, r) per bit and one add(r, P)
 // per set bit — the per-lane step of sm_lane_loop, so the same operations as the verify kernels.
