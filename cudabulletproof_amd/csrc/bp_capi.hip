@@ -195,6 +195,7 @@ struct Engine {
     // hipMemcpyAsync of these 33 KB cost ~7 ms on the first call's path).  The stream is drained
     // first: a caller's own staged copy out of `pinned` may still be queued on it.
     hipError_t upload(void* dst, const void* src, size_t bytes) {
+        if (bytes % 16) return hipErrorInvalidValue;   // (whole uint4s: the tables are 32- / 128-B records)
         hipError_t e;
         if ((e = hipStreamSynchronize(stream)) != hipSuccess) return e;
         if ((e = need_pinned(bytes)) != hipSuccess) return e;
