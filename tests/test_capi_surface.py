@@ -72,3 +72,38 @@ def test_product_does_not_use_oracle():
             if f.endswith((".py", ".hip", ".h", ".cpp")):
                 txt = open(os.path.join(dp, f)).read()
                 assert "oracle" not in txt.replace("no CPU fallback", ""), f
+
+
+def test_no_device_means_no_result():
+    """With no HIP device visible the engine has no CPU fallback: the Python mirror raises before
+    touching the C ABI, and the C ABI itself (cuda_range_proof_verify, reference error behaviour:
+    device error -> stderr + exit, cuda_bulletproof_kernels.cu:13-21) ends the process instead of
+    returning a verdict.  Run in child processes with every device hidden."""
+    import sys
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="-1", ROCR_VISIBLE_DEVICES="-1")
+    py = ("import numpy as np, cudabulletproof_amd as bp\n"
+          "d = np.load('tests/golden/proofs_n16.npz')\n"
+          "try:\n"
+          "    bp.cuda_range_proof_verify({}, d['V'][0], 16, d['G'], d['H'], d['g'], d['h'])\n"
+          "    print('RESULT')\n"
+          "except bp.BulletproofError as e:\n"
+          "    print('RAISED', e)\n")
+    r = subprocess.run([sys.executable, "-c", py], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert "RAISED" in r.stdout and "no CPU fallback" in r.stdout and "RESULT" not in r.stdout, (r.stdout, r.stderr)
+    # the C ABI called directly (bypassing the Python check) on the same well-formed proof: no verdict
+    # comes back
+    py2 = ("import ctypes, sys, numpy as np, cudabulletproof_amd as bp\n"
+           "sys.path.insert(0, 'tests')\n"
+           "from test_gpu_parity import _proof\n"
+           "d = np.load('tests/golden/proofs_n16.npz')\n"
+           "keep = []\n"
+           "rp = bp._range_proof_struct(_proof(d, 0), 16, keep)\n"
+           "u = lambda a: np.ascontiguousarray(a, np.uint64)\n"
+           "V, g, h, G, H = u(d['V'][0]), u(d['g']), u(d['h']), u(d['G']), u(d['H'])\n"
+           "p = lambda a: ctypes.c_void_p(a.ctypes.data)\n"
+           "gv, hv = bp.PointVector(p(G).value, len(G)), bp.PointVector(p(H).value, len(H))\n"
+           "ok = bp.lib().cuda_range_proof_verify(ctypes.byref(rp), p(V), ctypes.c_size_t(16), ctypes.byref(gv), "
+           "ctypes.byref(hv), p(g), p(h))\n"
+           "print('RESULT', ok)\n")
+    r = subprocess.run([sys.executable, "-c", py2], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "RESULT" not in r.stdout and "HIP error" in r.stderr, (r.returncode, r.stdout, r.stderr)
