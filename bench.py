@@ -422,7 +422,8 @@ def rooflines(dom, B, n, steps, launches, avg_ms, dt, kern_ms, pcfg, npipes):
     algorithmic bytes and a breakdown model.  VALU: `frac` = VALUBusy (PMC: the fraction of cycles
     in which the SIMDs issued VALU work); beside it the region's issue rate (SQ_INSTS_VALU per
     launch x launches / wall time), the cycles per instruction per SIMD that rate means at the PMC
-    clock, and the rates of k_terms' point-op loops run alone (profiles/valu_step_roof.json)."""
+    clock and at the shader clock measured under this load (profiles/clock/), and the rates of
+    k_terms' point-op loops run alone (profiles/valu_step_roof.json)."""
     per_batch = alg_bytes(dom, B, n)
     per_launch = per_batch * steps / launches if per_batch else None
     achieved = (per_launch / (avg_ms * 1e-3)) / 1e9 if per_launch else None
@@ -467,6 +468,12 @@ def rooflines(dom, B, n, steps, launches, avg_ms, dt, kern_ms, pcfg, npipes):
         "isolated_loops_source": "profiles/valu_step_roof.json (tools/ubench_step.hip: k_terms' point-op loops "
                                  "from registers + LDS at its occupancy)",
         "valu_utilization_pct": pmc(dom, "valu_utilization_pct", pcfg), "pmc_config": pcfg,
+        "loaded_clock_mhz": loaded_clock_mhz(),
+        "cycles_per_instr_per_simd_loaded_clock": 1024 * loaded_clock_mhz() * 1e6 / vagg
+        if vagg and loaded_clock_mhz() else None,
+        "loaded_clock_source": "profiles/clock/*.json (tools/clock_watch.sh: rocm-smi shader clock, median over the "
+                               "headline's loaded samples; not throttled at ~1.25 kW): the issue interval this run's "
+                               "aggregate VALU rate means at that clock",
         "frac_alg": alg_vi / vi * busy / 100 if alg_vi and vi and busy else None,
         "alg_product_valu_per_launch": alg_vi,
         "frac_alg_rule": "minimum product VALU per launch (2 VALU per 32x32 limb product: 464 products per doubling "
@@ -501,6 +508,16 @@ def alg_valu_per_verify(n, K):
     v_mad_u64_u32 + one carry count), per the point_ops_model, / 64 lanes."""
     dbl, add = point_ops_model(n, K)
     return 2 * (dbl * PRODUCTS_DBL + add * PRODUCTS_ADD) / 64
+
+
+def loaded_clock_mhz():
+    """Median shader clock under the headline's load, from the newest profiles/clock/clock_*.json."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "clock", "clock_*.json")), key=os.path.getmtime)
+    try:
+        return float(json.load(open(files[-1]))["sclk_mhz_median_loaded"]) if files else None
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def step_roof():
