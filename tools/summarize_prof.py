@@ -68,9 +68,10 @@ def prove_summary(tag):
     except (OSError, ValueError, IndexError):
         pv = {}
     lines = [f"# rocprofv3 summary — prover, {tag}", "",
-             "Command: `tools/profile_prove.sh " + tag + "` on one MI355X: bench.py's prove leg (B = 65536 64-bit "
-             "proofs per hipbp_batch_generate_range_proof batch, K = 22 prefix tables, two streams, 2 timed + 1 "
-             "warm-up batch), after a 3-step verify leg whose kernels are not listed.",
+             "Command: `tools/profile_prove.sh " + tag + "` on one MI355X: bench.py's prove leg (B = "
+             f"{pv.get('batch', '?')} 64-bit proofs per hipbp_batch_generate_range_proof batch, K = "
+             f"{pv.get('prefix_bits', '?')} prefix tables, {pv.get('streams', '?')} streams, 2 timed + 1 warm-up "
+             "batch), after a short verify leg whose kernels are not listed.",
              "", f"Prove leg in the traced run: {pv.get('value', float('nan')):.0f} proofs/s "
              f"({pv.get('ms_per_batch', float('nan')):.1f} ms per batch of {pv.get('batch', '?')}), "
              f"deterministic across streams: {pv.get('deterministic_across_streams')}.", "",
@@ -91,10 +92,12 @@ def prove_summary(tag):
         hbm = (2 * mean(fe) + mean(wr)) * 1024 / 1e6 if fe and wr else float("nan")
         lines.append(f"| {k} | {r['Calls']} | {float(r['AverageNs']) / 1e6:.3f} | {float(r['TotalDurationNs']) / 1e6:.2f} | "
                      f"{mean(b):.1f} | {mean(vi):.0f} | {hbm:.1f} |")
-    lines += ["", "Per batch: prep, sort, terms0 (all A/S terms: the heavy scalar-mults, K = 22 prefix tables for "
+    lines += ["", "Per batch: prep, sort, terms0 (all A/S terms: the heavy scalar-mults, prefix tables for "
               "the generator bases), chain0, commit, terms1, tx, then per IPA round rterms / chain / round, final. "
-              "The rterms and chain launches are latency-bound tails (one scalar-mult chain whatever their size); "
-              "the two streams put one batch's tails under the other's terms0.",
+              "The commit, rterms and chain launches are latency-bound tails (commit: the A11 sequential "
+              "accumulations, one lane per proof; rterms: one scalar-mult chain whatever their size); the streams "
+              "put one batch's tails under the other batches' terms0, so their kernel times overlap (the "
+              "per-launch averages exceed the per-batch wall time).",
               "HBM bytes apply the gfx950 FETCH_SIZE x2 correction (MI355X_MICROARCH.md)."]
     out_md = os.path.join(ROOT, "profiles", f"rocprof_{tag}_prove_summary.md")
     open(out_md, "w").write("\n".join(lines) + "\n")
