@@ -456,6 +456,19 @@ def rooflines(dom, B, n, steps, launches, avg_ms, dt, kern_ms, pcfg, npipes):
     clk = pmc(dom, "eff_clock_ghz", pcfg)
     vagg = vi * launches / dt if vi else None   # all launches of the timed region / its wall time
     loops = step_roof()
+    clk_loaded = loaded_clock_mhz()
+    # the products the formulas need, per second of the timed region, against the guide's nominal
+    # wave64 issue of every SIMD (1024 SIMDs x the loaded shader clock / 2 cycles per instruction):
+    # a roof that is not the kernel's own measured issue rate
+    nominal = 1024 * clk_loaded * 1e6 / 2 if clk_loaded else None
+    frac_nominal = alg_vi * launches / dt / nominal if alg_vi and nominal else None
+    frac_alg = alg_vi / vi * busy / 100 if alg_vi and vi and busy else None
+    # scalars the driver's parsed copy of the line keeps (it drops nested objects)
+    roofline["kernel_ms_per_step"] = avg_ms / npipes if npipes else avg_ms
+    roofline["frac_per_launch_overlapped"] = achieved / HBM_PEAK_GBS if achieved else None
+    roofline["valu_frac_busy"] = busy / 100 if busy else None
+    roofline["valu_frac_alg"] = frac_alg
+    roofline["valu_frac_nominal_issue"] = frac_nominal
     valu_roofline = {
         "kernel": dom, "unit": "wave64 VALU instr/s", "frac": busy / 100 if busy else None,
         "frac_source": "VALUBusy (rocprofv3 PMC on this configuration, profiles/pmc_traffic.json): the share of "
@@ -468,13 +481,15 @@ def rooflines(dom, B, n, steps, launches, avg_ms, dt, kern_ms, pcfg, npipes):
         "isolated_loops_source": "profiles/valu_step_roof.json (tools/ubench_step.hip: k_terms' point-op loops "
                                  "from registers + LDS at its occupancy)",
         "valu_utilization_pct": pmc(dom, "valu_utilization_pct", pcfg), "pmc_config": pcfg,
-        "loaded_clock_mhz": loaded_clock_mhz(),
-        "cycles_per_instr_per_simd_loaded_clock": 1024 * loaded_clock_mhz() * 1e6 / vagg
-        if vagg and loaded_clock_mhz() else None,
+        "loaded_clock_mhz": clk_loaded,
+        "cycles_per_instr_per_simd_loaded_clock": 1024 * clk_loaded * 1e6 / vagg if vagg and clk_loaded else None,
+        "frac_nominal_issue": frac_nominal,
+        "frac_nominal_issue_rule": "minimum product VALU per launch x launches / the timed region's wall time, over "
+                                   "1024 SIMDs x loaded shader clock / 2 cycles (the guide's nominal wave64 issue)",
         "loaded_clock_source": "profiles/clock/*.json (tools/clock_watch.sh: rocm-smi shader clock, median over the "
                                "headline's loaded samples; not throttled at ~1.25 kW): the issue interval this run's "
                                "aggregate VALU rate means at that clock",
-        "frac_alg": alg_vi / vi * busy / 100 if alg_vi and vi and busy else None,
+        "frac_alg": frac_alg,
         "alg_product_valu_per_launch": alg_vi,
         "frac_alg_rule": "minimum product VALU per launch (2 VALU per 32x32 limb product: 464 products per doubling "
                          "with its squares, 512 per add with Z2 = 1; point ops per verify from bench.point_ops_model "
@@ -511,9 +526,10 @@ def alg_valu_per_verify(n, K):
 
 
 def loaded_clock_mhz():
-    """Median shader clock under the headline's load, from the newest profiles/clock/clock_*.json."""
+    """Median shader clock under the headline's load, from the latest round's profiles/clock/clock_<tag>.json
+    (ordered by file name, i.e. by round tag: a checkout gives every file the same mtime)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "clock", "clock_*.json")), key=os.path.getmtime)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "clock", "clock_*.json")))
     try:
         return float(json.load(open(files[-1]))["sclk_mhz_median_loaded"]) if files else None
     except (OSError, ValueError, KeyError):
@@ -1068,16 +1084,18 @@ def prove_leg(args, dev, gens=None):
             "prefix_bits": gens.bits if gens is not None else 0}
 
 
-def prefix_leg(args, dev, world, bits, batches, oks, ref_oks, G, H, g, h, streams):
+def prefix_leg(args, dev, world, bits, batches, ref_oks, G, H, g, h, streams):
     """The headline configuration at another prefix-table width (`prefix_legs`): fresh pipelines on
     the same streams over the same resident batches, a generator set with `bits`-bit tables (none at
     0: every scalar-mult is the reference's full 256-bit double-and-add, cuda_bulletproof_kernels.cu:26-41),
     filled, then args.steps ticks timed between barrier + synchronize like `value` (max over ranks).
-    The verdicts of every batch must equal the headline's (`verdicts_match_headline`)."""
+    The leg writes its own zeroed verdict buffers; the verdicts of every batch must equal the
+    headline's (`verdicts_match_headline`; None when the leg pushed fewer than all the batches)."""
     import torch
     import torch.distributed as dist
     import cudabulletproof_amd as bp
     B, n, nb = args.batch, args.n, len(batches)
+    oks = [torch.zeros_like(o) for o in ref_oks]
     gens = None
     torch.cuda.synchronize(dev)
     tb = time.perf_counter()
@@ -1107,7 +1125,8 @@ def prefix_leg(args, dev, world, bits, batches, oks, ref_oks, G, H, g, h, stream
         for pp in pipes:
             pp.flush()
         torch.cuda.synchronize(dev)
-        same = all(torch.equal(o, r) for o, r in zip(oks[:nb], ref_oks))
+        pushed = (pipes[0].depth - 1) * npipe + args.steps
+        same = all(torch.equal(o, r) for o, r in zip(oks, ref_oks)) if pushed >= nb else None
     finally:
         for pp in pipes:
             pp.close()
@@ -1123,11 +1142,57 @@ def prefix_leg(args, dev, world, bits, batches, oks, ref_oks, G, H, g, h, stream
             "tables_build_s": build_s if bits else None, "verdicts_match_headline": same}
 
 
+def kfd_gpu_count(sysfs="/sys/class/kfd/kfd/topology/nodes", dev_dri="/dev/dri", env=None):
+    """GPUs this process could open, counted without the HIP runtime (the launcher parent must not
+    bring it up): KFD topology nodes with SIMDs (CPU nodes have simd_count 0) whose render node
+    /dev/dri/renderD<drm_render_minor> exists here (a container sees only the GPUs passed to it),
+    capped by the visible-device lists HIP honours (HIP_ / ROCR_ / CUDA_VISIBLE_DEVICES).  None when
+    the topology is absent (no amdgpu driver)."""
+    env = os.environ if env is None else env
+    try:
+        nodes = sorted(os.listdir(sysfs))
+    except OSError:
+        return None
+    count = 0
+    for nd in nodes:
+        props = {}
+        try:
+            for line in open(os.path.join(sysfs, nd, "properties")):
+                k, _, v = line.strip().partition(" ")
+                props[k] = v
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0") or 0) <= 0:
+            continue
+        minor = props.get("drm_render_minor")
+        if minor is not None and not os.path.exists(os.path.join(dev_dri, f"renderD{minor}")):
+            continue
+        count += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(var)
+        if v is not None:
+            count = min(count, len([x for x in v.split(",") if x.strip() and x.strip() != "-1"]))
+    return count
+
+
+def hip_mapped():
+    """The HIP / HSA runtime libraries mapped into this process (/proc/self/maps), [] if none."""
+    try:
+        libs = {line.split()[-1] for line in open("/proc/self/maps") if len(line.split()) >= 6}
+    except OSError:
+        return []
+    return sorted(os.path.basename(p) for p in libs if "libamdhip64" in p or "libhsa-runtime64" in p)
+
+
 def rank_launch(args):
     """`--gpus N` means N ranks.  Under a launcher (WORLD_SIZE set) the world must be N.  Without
     one and N > 1, this process starts `torch.distributed.run --nproc-per-node N` on this script as
-    a CHILD (before anything here touches the GPU; counting devices does not) and returns its exit
-    status; N larger than the visible GPUs is an error (--rehearse puts every rank on cuda:0).
+    a CHILD and returns its exit status; N larger than the visible GPUs is an error (--rehearse puts
+    every rank on cuda:0).  This launcher never touches the GPU: no torch import, devices counted
+    from the KFD topology (kfd_gpu_count).  Before the spawn it runs the CPU legs rank 0 would run
+    at N = 1 (cpu_baseline, configs0: children and host code only) and hands their JSON to rank 0
+    through a temp file (BENCH_CPU_LEGS), with whether a HIP runtime was mapped here up to the spawn.
+    BENCH_LAUNCH_DRYRUN=1 prints that hand-over instead of spawning (tests/test_bench_helpers.py).
     Returns None when this process is a rank and should run the bench."""
     ws = os.environ.get("WORLD_SIZE")
     if ws is not None:
@@ -1139,18 +1204,44 @@ def rank_launch(args):
         return None
     import socket
     import subprocess
-    import torch
-    have = torch.cuda.device_count()
-    if have < args.gpus and not args.rehearse:
-        print(f"bench.py: --gpus {args.gpus} needs {args.gpus} GPUs, {have} visible "
+    import tempfile
+    have = kfd_gpu_count()
+    if (have is None or have < args.gpus) and not args.rehearse:
+        print(f"bench.py: --gpus {args.gpus} needs {args.gpus} GPUs, {have or 0} visible "
               f"(--rehearse runs every rank on cuda:0 with gloo)", file=sys.stderr)
         return 3
-    with socket.socket() as s:   # a free rendezvous port on the loopback
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
-    return subprocess.call(cmd)
+    legs = {"cpu_baseline": None, "configs0": None}
+    if not args.no_cpu:
+        legs["cpu_baseline"] = cpu_baseline(args.n, args.cpu_seconds, args.cpu_procs)
+        legs["configs0"] = configs0_leg()
+    legs["launcher"] = {"gpus_visible_kfd": have, "hip_mapped_before_spawn": hip_mapped(),
+                        "note": "the torchrun parent: counted GPUs from /sys/class/kfd, ran the CPU legs, spawned"}
+    fd, path = tempfile.mkstemp(prefix="bench_cpu_legs_", suffix=".json")
+    with os.fdopen(fd, "w") as f:
+        json.dump(legs, f)
+    try:
+        if os.environ.get("BENCH_LAUNCH_DRYRUN") == "1":
+            print(json.dumps(dict(legs, hand_over=path)), flush=True)
+            return 0
+        with socket.socket() as s:   # a free rendezvous port on the loopback
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+        return subprocess.call(cmd, env=dict(os.environ, BENCH_CPU_LEGS=path))
+    finally:
+        os.unlink(path)
+
+
+def cpu_legs_handed_over():
+    """The launcher parent's CPU legs (rank_launch), or None when this rank was not started by it."""
+    path = os.environ.get("BENCH_CPU_LEGS")
+    if not path:
+        return None
+    try:
+        return json.load(open(path))
+    except (OSError, ValueError):
+        return None
 
 
 def device_pci(dev):
@@ -1205,8 +1296,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # CPU baseline first, before this process touches the GPU: its worker processes are started
     # from a process with no HIP state (no fork/exec of a GPU-initialised process)
-    cpu, configs0, sample = None, None, None
-    if not args.no_cpu and rank == 0 and world == 1:
+    # (at N > 1 the torchrun parent ran them before the spawn and hands them to rank 0)
+    cpu, configs0, sample, launcher = None, None, None, None
+    handed = cpu_legs_handed_over() if rank == 0 and world > 1 else None
+    if handed is not None:
+        cpu, configs0, launcher = handed["cpu_baseline"], handed["configs0"], handed["launcher"]
+    elif not args.no_cpu and rank == 0 and world == 1:
         cpu = cpu_baseline(args.n, args.cpu_seconds, args.cpu_procs)
         configs0 = configs0_leg()
     if rank == 0 and args.proofs == "prover" and not args.no_check:
@@ -1330,7 +1425,7 @@ def main():
     prefix_legs = None
     if pipes and args.table_legs.strip():   # the same workload at other table widths, e.g. none (K = 0)
         ref_oks = [o.clone() for o in oks[:nb]]
-        prefix_legs = {f"k{b}": prefix_leg(args, dev, world, b, batches, oks, ref_oks, Gd, Hd, gd, hd, streams)
+        prefix_legs = {f"k{b}": prefix_leg(args, dev, world, b, batches, ref_oks, Gd, Hd, gd, hd, streams)
                        for b in (int(x) for x in args.table_legs.split(",")) if b != args.prefix_bits}
     # every rank's identity + the verdicts of its own batches (gathered: proves N distinct ranks ran)
     ranks = [rank_info(dev, oks[:nb])]
@@ -1414,7 +1509,7 @@ def main():
                         if reps else None),
             "roofline": roofline, "valu_roofline": valu_roofline, "cpu_baseline": cpu, "verify_check": check,
             "with_h2d": h2d, "configs0": configs0, "msm": msm, "ipa": ipa, "prove": prove,
-            "sharded_2p16": sharded, "host_api": host_api,
+            "sharded_2p16": sharded, "host_api": host_api, "launcher": launcher,
         }
         for k, leg in (prefix_legs or {}).items():   # scalars in `config` (the driver keeps config's scalars)
             line["config"][f"{k}_value"] = leg["value"]

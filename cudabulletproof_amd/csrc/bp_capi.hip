@@ -206,8 +206,11 @@ struct Engine {
     }
     // two_i[i] = i successive fe_mul(., 2) from 1 (bulletproof_range_proof.cu:705-712): a grow-only
     // table, extended on the host (C forms) and uploaded whole on growth.  The old device buffer is
-    // freed after the engine stream has synchronised (hipFree waits for the device).
+    // retired, never freed: ticks and prover launches already queued on OTHER streams (user
+    // pipelines, caller prover streams) may still read it, and upload() drains only the engine
+    // stream.  Growth doubles, so the retired buffers total less than the live one (a few KB).
     std::vector<bp::fe> two_host;
+    std::vector<bp::fe*> two_retired;
     hipError_t ensure_two(int n) {
         if (n <= two_cap) return hipSuccess;
         hipError_t e;
@@ -218,7 +221,7 @@ struct Engine {
         bp::fe* nt = nullptr;
         if ((e = hipMalloc(&nt, (size_t)cap * sizeof(bp::fe))) != hipSuccess) return e;
         if ((e = upload(nt, two_host.data(), (size_t)cap * sizeof(bp::fe))) != hipSuccess) return e;
-        if (two_i && (e = hipFree(two_i)) != hipSuccess) return e;
+        if (two_i) two_retired.push_back(two_i);
         two_i = nt;
         two_cap = cap;
         return hipSuccess;
@@ -1295,7 +1298,7 @@ int hipbp_field_op(int op, fe25519* r, const fe25519* a, const fe25519* b, size_
     hipError_t err;
     Engine* e = engine_or_null(&err);
     BP_RET_ON(err);
-    if (op < 0 || op > 9) { g_err = "bad op"; return HIPBP_ERR_ARG; }
+    if (op < 0 || op > 10) { g_err = "bad op"; return HIPBP_ERR_ARG; }
     if (!a || (!b && op != 3 && op != 5 && op != 7)) { g_err = "null operand"; return HIPBP_ERR_ARG; }
     if (count == 0) return HIPBP_OK;
     hipStream_t s = pick(stream, *e);

@@ -7,6 +7,7 @@
 // the reference's order, because the arithmetic is not associative.
 #include "bp_kernels.h"
 #include "ge25519_dev.h"
+#include "ge25519_quad.h"
 #include "sha256_dev.h"
 
 namespace bp {
@@ -330,6 +331,13 @@ void launch_terms(const RegionList& rl, const SlotDev* slots, const ge* G, const
 __global__ __launch_bounds__(TPB) void k_field_op(int op, fe* r, const fe* __restrict__ a, const fe* __restrict__ b,
                                                   size_t count) {
     size_t i = gid();
+    if (op == 10) {   // fe_mul_q4, the drain forms' quad-split product: element i >> 2 on lane quad i >> 2
+        i >>= 2;      // (a whole quad leaves together: the DPP sums stay inside live quads)
+        if (i >= count) return;
+        const fe z = fe_mul_q4(a[i], b[i]);
+        if ((threadIdx.x & 3) == 0) r[i] = z;
+        return;
+    }
     if (i >= count) return;
     fe x = a[i], y;
     if (op != 3 && op != 7) y = b[i];   // unary ops take no b
@@ -362,7 +370,7 @@ __global__ __launch_bounds__(TPB) void k_field_op(int op, fe* r, const fe* __res
 
 void launch_field_op(int op, fe* r, const fe* a, const fe* b, size_t count, hipStream_t s) {
     if (count == 0) return;
-    k_field_op<<<nblk(count), TPB, 0, s>>>(op, r, a, b, count);
+    k_field_op<<<nblk(op == 10 ? 4 * count : count), TPB, 0, s>>>(op, r, a, b, count);
 }
 
 

@@ -8,7 +8,7 @@ namespace bp {
 
 // The engine's table upload (bp_capi.hip Engine::upload): the kernel reads the pinned host staging
 // buffer directly, so the first call's path issues no copy-engine transfer (a first hipMemcpyAsync of
-// the 33-KB identity-doubling table cost ~7 ms; profiles/dropin_first_call_r05o.txt).  It lives in
+// the 33-KB identity-doubling table cost ~7 ms; profiles/dropin_first_call_r05g.txt).  It lives in
 // the row-form tick's code object, which a one-proof call loads anyway.
 __global__ void k_upload(uint4* __restrict__ dst, const uint4* __restrict__ src, size_t n16) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x)

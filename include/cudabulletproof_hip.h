@@ -296,7 +296,8 @@ int hipbp_point_tree(ge25519* result, const ge25519* points, size_t n, void* str
  * 4 SoA add (limbwise, no carry), 5 invert (host chain), 6 the product fold alone on the
  * 512-bit t = a || b (fe25519_mul's reduction, curve25519_ops.cu:114-145), 7 fe25519_sq,
  * 8 / 9 the sum / difference of the fused add-and-sub block the lane-quad forms use (the same
- * values as ops 0 / 1). */
+ * values as ops 0 / 1), 10 fe25519_mul formed as the drain forms' quad-split product (fe_mul_q4:
+ * four lanes per element, the same value as op 2). */
 int hipbp_field_op(int op, fe25519* r, const fe25519* a, const fe25519* b, size_t count, void* stream);
 /* Frees every workspace the library caches for `stream` on the current device (canonical MSM /
  * point-tree, prover, one-shot verify pipelines, the Pippenger workspace pair with its side stream

@@ -85,11 +85,13 @@ def test_rank_launch_command(monkeypatch):
     import subprocess
     seen = {}
     monkeypatch.delenv("WORLD_SIZE", raising=False)
-    monkeypatch.setattr(subprocess, "call", lambda cmd: seen.setdefault("cmd", cmd) and 0)
+    monkeypatch.setattr(subprocess, "call", lambda cmd, env=None: seen.update(cmd=cmd, env=env) or 0)
     monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--rehearse", "--steps", "3"])
-    a = argparse.Namespace(gpus=4, rehearse=True)
+    a = argparse.Namespace(gpus=4, rehearse=True, no_cpu=True)
     assert bench.rank_launch(a) == 0
     cmd = seen["cmd"]
+    # the CPU legs' hand-over file is named to the ranks and removed after them
+    assert seen["env"]["BENCH_CPU_LEGS"] and not os.path.exists(seen["env"]["BENCH_CPU_LEGS"])
     assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"] and "--nproc-per-node=4" in cmd
     assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
     assert cmd[-5:] == ["--gpus", "4", "--rehearse", "--steps", "3"] and cmd[-6].endswith("bench.py")
@@ -128,3 +130,58 @@ def test_measured_multirank_run_needs_distinct_devices_over_rccl():
         for p in procs:
             p.join(timeout=60)
         assert res == {0: "exit 4", 1: "exit 4"}, res
+
+
+def _kfd_node(root, name, simd, minor):
+    d = os.path.join(root, name)
+    os.makedirs(d)
+    with open(os.path.join(d, "properties"), "w") as f:
+        f.write(f"cpu_cores_count {0 if simd else 64}\nsimd_count {simd}\n")
+        if minor is not None:
+            f.write(f"drm_render_minor {minor}\n")
+
+
+def test_kfd_gpu_count(tmp_path):
+    """The launcher counts GPUs from the KFD topology without the HIP runtime: nodes with SIMDs whose
+    render node exists in this container, capped by the visible-device lists."""
+    sysfs, dri = str(tmp_path / "nodes"), str(tmp_path / "dri")
+    os.makedirs(dri)
+    _kfd_node(sysfs, "0", 0, None)           # a CPU node
+    for i, minor in enumerate((128, 136, 144)):
+        _kfd_node(sysfs, str(i + 1), 1024, minor)
+    for minor in (128, 136):                 # the third GPU is not passed to this container
+        open(os.path.join(dri, f"renderD{minor}"), "w").close()
+    assert bench.kfd_gpu_count(sysfs, dri, env={}) == 2
+    assert bench.kfd_gpu_count(sysfs, dri, env={"HIP_VISIBLE_DEVICES": "1"}) == 1
+    assert bench.kfd_gpu_count(sysfs, dri, env={"ROCR_VISIBLE_DEVICES": "0,1,2,3"}) == 2
+    assert bench.kfd_gpu_count(str(tmp_path / "absent"), dri, env={}) is None
+
+
+def test_hip_mapped_probe_sees_torch():
+    """hip_mapped() reads /proc/self/maps: a process that imported torch (a ROCm build) has the HIP runtime
+    mapped, a bare interpreter has not — the probe the launcher's HIP-free check relies on."""
+    import subprocess
+    code = "import sys; sys.path.insert(0, %r); import bench; a = bench.hip_mapped(); import torch; " \
+           "print(bool(a), bool(bench.hip_mapped()))" % ROOT
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    before, after = p.stdout.split()
+    assert before == "False"
+    import torch
+    if torch.version.hip:
+        assert after == "True"
+
+
+def test_launcher_parent_is_hip_free_and_hands_cpu_legs_to_rank0():
+    """`bench.py --gpus N` without a launcher: the parent never maps the HIP runtime up to the spawn,
+    and it runs the CPU baseline + configs[0] legs itself, so the N-rank line carries them
+    (BENCH_LAUNCH_DRYRUN=1: the parent prints the hand-over instead of spawning)."""
+    import json
+    p = _run_bench(["--gpus", "2", "--rehearse", "--cpu-seconds", "0.3", "--cpu-procs", "1"],
+                   {"BENCH_LAUNCH_DRYRUN": "1"}, timeout=600)
+    assert p.returncode == 0, p.stderr[-2000:]
+    legs = json.loads(p.stdout.strip().splitlines()[-1])
+    assert legs["launcher"]["hip_mapped_before_spawn"] == []
+    cpu = legs["cpu_baseline"]
+    assert cpu is not None and cpu["value"] > 0 and cpu["cores"] == 1 and cpu["kind"] in ("reference", "port")
+    assert not os.path.exists(legs["hand_over"])

@@ -746,6 +746,44 @@ def test_bounded_product_gate(bp, oracle, op):
         assert np.array_equal(got[i], oracle.fe_mul(a[i], b[i])), i
 
 
+def test_quad_product_gate(bp, oracle):
+    """fe_mul_q4 (ge25519_quad.h, the k_terms<4> / <16> drain forms' product split over a lane quad)
+    runs the bounded 2x8 row products (mul2x8_bounded_asm) unless some lane's row word a[0] — x word
+    0, 2, 4 or 6 — exceeds 0xFFFFFFEF, when the wave runs the counting mul2x8_asm.  Through
+    field_op "mul_q4" (one element per quad, 16 per wave): (1) every row word at or just under the
+    bound with all other words 2^32 - 1; (2) one element per wave with one row word just over the
+    bound or 2^32 - 1, at a rotating row position; (3) all-ones operands.  Every element equals the
+    oracle's fe25519_mul (curve25519_ops.cu:93-149)."""
+    import torch
+    rng = np.random.default_rng(19)
+    LOW = 0xFFFFFFEF
+
+    def fe_words(words):
+        return np.array([words[2 * k] | (words[2 * k + 1] << 32) for k in range(4)], np.uint64)
+    a_l, b_l = [], []
+    for w in range(64):
+        for el in range(16):
+            aw = [0xFFFFFFFF if rng.random() < 0.7 else int(rng.integers(0, 2**32)) for _ in range(8)]
+            bw = [0xFFFFFFFF if rng.random() < 0.7 else int(rng.integers(0, 2**32)) for _ in range(8)]
+            for k in (0, 2, 4, 6):
+                aw[k] = LOW - int(rng.integers(0, 3))
+            if 8 <= w < 56 and el == (w * 7) % 16:   # one quad lane over the bound: the counting form
+                aw[2 * (w % 4)] = [LOW + 1, 0xFFFFFFFF][(w // 4) % 2]
+            if w >= 56:
+                aw, bw = [0xFFFFFFFF] * 8, [0xFFFFFFFF] * 8
+            a_l.append(fe_words(aw))
+            b_l.append(fe_words(bw))
+    a, b = np.stack(a_l), np.stack(b_l)
+    dev = torch.device("cuda:0")
+    T = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(np.int64)).to(dev)
+    r = torch.empty(len(a), 4, dtype=torch.int64, device=dev)
+    bp.field_op("mul_q4", r, T(a), T(b))
+    torch.cuda.synchronize()
+    got = r.cpu().numpy().view(np.uint64)
+    for i in range(len(a)):
+        assert np.array_equal(got[i], oracle.fe_mul(a[i], b[i])), i
+
+
 def _edge_cases(op, rng):
     """Operand pairs that put one lane on each rare edge the field asm tests for (fe_add_asm /
     fe_sub_asm / fe_fold_asm in field_asm.h): every exact-form branch taken by exactly the case
