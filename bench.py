@@ -96,6 +96,9 @@ def parse():
     ap.add_argument("--shard-defer", type=int, default=1,
                     help="configs[4]: split stage 0 in the shard's pipelines (hipbp_pipeline_defer_msm: the MSM "
                          "terms beside the fold rounds, so the drain overlaps them); same bits")
+    ap.add_argument("--shard-stagger", type=int, default=0,
+                    help="configs[4]: each push's stream waits for the previous push's pipeline to finish this many "
+                         "more ticks (0: all pushes start together)")
     ap.add_argument("--host-count", type=int, default=32768, help="proofs per host-struct API call")
     ap.add_argument("--no-host", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip the headline self-check (verify_check)")
@@ -970,7 +973,15 @@ def _shard_run(args, dev, world, B, n, total, lo, hi, tiles, pipes, Bs, defer):
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for k, b in enumerate(batches):
-            pipes[k % len(pipes)].push(b, ok[offs[k]:offs[k + 1]])
+            pp = pipes[k % len(pipes)]
+            if args.shard_stagger and k > 0 and len(pipes) > 1:   # start after the previous push's first ticks
+                prev = pipes[(k - 1) % len(pipes)]
+                for _ in range(args.shard_stagger):
+                    prev.push(None)
+                ev = torch.cuda.Event()
+                ev.record(prev.stream)
+                pp.stream.wait_event(ev)
+            pp.push(b, ok[offs[k]:offs[k + 1]])
         for pp in pipes:
             pp.flush()
         torch.cuda.synchronize(dev)   # the pipelines' streams have written every verdict
