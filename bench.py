@@ -1312,7 +1312,8 @@ def main():
     handed = cpu_legs_handed_over() if rank == 0 and world > 1 else None
     if handed is not None:
         cpu, configs0, launcher = handed["cpu_baseline"], handed["configs0"], handed["launcher"]
-    elif not args.no_cpu and rank == 0 and world == 1:
+    elif not args.no_cpu and rank == 0:   # N = 1, or ranks started by an outer launcher (the driver's
+        # torchrun): rank 0 runs them before init_process_group, the other ranks wait at the rendezvous
         cpu = cpu_baseline(args.n, args.cpu_seconds, args.cpu_procs)
         configs0 = configs0_leg()
     if rank == 0 and args.proofs == "prover" and not args.no_check:

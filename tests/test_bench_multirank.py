@@ -40,11 +40,20 @@ def test_bench_ranks_rehearsal_matches_one_rank(one_rank_line, N):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     l1 = one_rank_line
     # no outer launcher: `--gpus N` makes bench.py start the N ranks itself (torch.distributed.run child)
-    # at N = 8 the launcher parent also runs the CPU legs (GPU-free, before the spawn) for rank 0's line
+    # N = 8: bench.py's own launcher parent runs the CPU legs (GPU-free, before the spawn) for rank 0's
+    # line; N = 4: an outer torchrun (the driver's way) starts the ranks and rank 0 runs them itself
     small = [a for a in SMALL[:-2] if a != "--no-cpu"] + ["--cpu-seconds", "0.5", "--cpu-procs", "2"] \
-        if N == 8 else SMALL[:-2]
-    two = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(N), "--rehearse"] + small
-                         + LEGS, capture_output=True, text=True, timeout=900, cwd=ROOT, env=env)
+        if N in (4, 8) else SMALL[:-2]
+    outer = []
+    if N == 4:
+        import socket
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        outer = ["-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={N}", "--master-addr", "127.0.0.1",
+                 "--master-port", str(port)]
+    two = subprocess.run([sys.executable] + outer + [os.path.join(ROOT, "bench.py"), "--gpus", str(N), "--rehearse"]
+                         + small + LEGS, capture_output=True, text=True, timeout=900, cwd=ROOT, env=env)
     assert two.returncode == 0, two.stderr[-2000:]
     l2 = _line(two.stdout)
     assert l1["n_gpus"] == 1 and l2["n_gpus"] == N
@@ -68,8 +77,12 @@ def test_bench_ranks_rehearsal_matches_one_rank(one_rank_line, N):
     assert l1["repeats"]["n"] == l2["repeats"]["n"] == 5
     assert l2["config"]["passes_in_warmup_batch"] >= l1["config"]["passes_in_warmup_batch"]
     assert l2["ipa"]["n_gpus"] == 1 and l2["prove"]["n_gpus"] == 1 and l2["prove"]["valid"] == 256
-    assert l2["launcher"]["hip_mapped_before_spawn"] == [] and l1["launcher"] is None
-    if N == 8:   # the N-rank line carries the CPU baseline the parent timed
+    assert l1["launcher"] is None
+    if N == 4:
+        assert l2["launcher"] is None   # started by the outer launcher
+    else:
+        assert l2["launcher"]["hip_mapped_before_spawn"] == []
+    if N in (4, 8):   # the N-rank line carries the CPU baseline (parent or rank 0 timed it)
         assert l2["cpu_baseline"] is not None and l2["cpu_baseline"]["value"] > 0
         assert l2["configs0"] is not None
 
