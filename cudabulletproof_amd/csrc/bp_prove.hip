@@ -277,19 +277,8 @@ __global__ __launch_bounds__(TPB) void k_prove_commit(ProveIn in, ProveWs ws, co
     ws.pts[p * 5 + 0] = V;
     ws.pts[p * 5 + 1] = A;
     ws.pts[p * 5 + 2] = S;
-    sha256_ctx c;                                                   // challenge.cu:24-58
-    sha_init(c);
-    sha_str(c, "BulletproofYChal");
-    sha_fe_canon(c, V.X); sha_fe_canon(c, V.Y);
-    sha_fe_canon(c, A.X); sha_fe_canon(c, A.Y);
-    sha_fe_canon(c, S.X); sha_fe_canon(c, S.Y);
-    sha_str(c, "y_ch");
-    fe y = challenge_digest(c);
-    sha_init(c);
-    sha_str(c, "BulletproofZChal");
-    sha_limbs(c, y.v, 4);
-    sha_str(c, "z_ch");
-    fe z = challenge_digest(c);
+    fe y = chal_y(V, A, S);                                         // challenge.cu:24-58
+    fe z = chal_z(y);
     fe z2 = fe_mul(z, z);
     // t0 = <aL - z, y^n o (aR + z)> + z^2 <1^n, 2^n>, t1 = <sL, y^n o (aR + z)> + <aL - z, y^n o sR>,
     // t2 = <sL, y^n o sR>   (rp.cu:1358-1430): four sequential folds in index order, one pass.
@@ -364,13 +353,7 @@ __global__ __launch_bounds__(TPB) void k_prove_tx(ProveIn in, ProveWs ws, const 
     ge T2 = ge_norm_host(ge_norm_host(ge_add(tt[2], tt[3])));
     ws.pts[p * 5 + 3] = T1;
     ws.pts[p * 5 + 4] = T2;
-    sha256_ctx c;                                                   // challenge.cu:61-77
-    sha_init(c);
-    sha_str(c, "BulletproofXChal");
-    sha_fe_canon(c, T1.X); sha_fe_canon(c, T1.Y);
-    sha_fe_canon(c, T2.X); sha_fe_canon(c, T2.Y);
-    sha_str(c, "xcha");
-    fe x = challenge_digest(c);
+    fe x = chal_x(T1, T2);                                          // challenge.cu:61-77
     fe x2 = fe_mul(x, x);
     fe* st = ws.st + p * 8;
     const fe y = st[0], z = st[1], z2 = st[2];
@@ -401,13 +384,8 @@ __global__ __launch_bounds__(TPB) void k_prove_tx(ProveIn in, ProveWs ws, const 
         a[0] = t;
         b[0] = one;
     }
-    sha_init(c);                                                    // rp.cu:1636-1650
-    sha_str(c, "BulletproofIP");
-    sha_fe_canon(c, t);
-    sha_fe_canon(c, taux);
-    sha_fe_canon(c, mu);
     st[6] = t;
-    st[7] = challenge_digest(c);                                    // the IPA transcript
+    st[7] = chal_ip_start(t, taux, mu);                             // the IPA transcript (rp.cu:1636-1650)
     fe* m = ws.misc + p * 4;
     m[0] = taux;
     m[1] = mu;
@@ -464,13 +442,7 @@ __global__ __launch_bounds__(TPB) void k_prove_round(ProveIn in, ProveWs ws, Pro
     out.L[p * in.L + r] = L;
     out.R[p * in.L + r] = R;
     fe* st = ws.st + p * 8;
-    sha256_ctx c;                                                   // vectors.cu:450-466
-    sha_init(c);
-    sha_str(c, "InnerProductChal");
-    sha_limbs(c, st[7].v, 4);
-    sha_fe_canon(c, L.X);
-    sha_fe_canon(c, R.X);
-    fe u = challenge_digest(c);
+    fe u = chal_ip(st[7], L.X, R.X);                                // vectors.cu:450-466
     st[7] = u;
     if (r == 0) ws.misc[p * 4 + 2] = u;                              // proof->x (vectors.cu:472-474)
     fe ui = fe_invert(u);

@@ -27,13 +27,7 @@ __device__ __forceinline__ size_t gid() { return (size_t)blockIdx.x * blockDim.x
 __device__ __forceinline__ void prep_std_task(const BatchView& bv, const VerifyWs& ws, const fe* __restrict__ two_i,
                                               size_t p, const fe& z, const fe& z2, const fe& sy) {
     const int n = bv.n;
-    sha256_ctx c;
-    sha_init(c);
-    sha_str(c, "BulletproofXChal");
-    sha_fe_canon(c, bv.T1[p].X); sha_fe_canon(c, bv.T1[p].Y);
-    sha_fe_canon(c, bv.T2[p].X); sha_fe_canon(c, bv.T2[p].Y);
-    sha_str(c, "xcha");                  // memcpy of 4 bytes of "xchal" (challenge.cu:73)
-    fe x = challenge_digest(c);
+    fe x = chal_x(bv.T1[p], bv.T2[p]);   // 4 bytes of "xchal" (challenge.cu:73)
     const fe two = fe_add(fe_set(1), fe_set(1));
     // compute_precise_delta
     fe z3 = fe_mul(z2, z);
@@ -76,21 +70,10 @@ __device__ __forceinline__ void prep_std_task(const BatchView& bv, const VerifyW
 __device__ __forceinline__ void prep_range_task(const BatchView& bv, const VerifyWs& ws, const fe* __restrict__ two_i,
                                              size_t p, int mode) {
     const int n = bv.n;
-    sha256_ctx c;
     // y = H("BulletproofYChal" || V.X V.Y A.X A.Y S.X S.Y || "y_ch")   (challenge.cu:24-44)
-    sha_init(c);
-    sha_str(c, "BulletproofYChal");
-    sha_fe_canon(c, bv.V[p].X); sha_fe_canon(c, bv.V[p].Y);
-    sha_fe_canon(c, bv.A[p].X); sha_fe_canon(c, bv.A[p].Y);
-    sha_fe_canon(c, bv.S[p].X); sha_fe_canon(c, bv.S[p].Y);
-    sha_str(c, "y_ch");
-    fe y = challenge_digest(c);
+    fe y = chal_y(bv.V[p], bv.A[p], bv.S[p]);
     // z = H("BulletproofZChal" || y || "z_ch")   (challenge.cu:47-58)
-    sha_init(c);
-    sha_str(c, "BulletproofZChal");
-    sha_limbs(c, y.v, 4);
-    sha_str(c, "z_ch");
-    fe z = challenge_digest(c);
+    fe z = chal_z(y);
     // (x is derived at crv:105 but only feeds compute_precise_delta and the unused
     //  x argument of calculate_inner_product_point; it does not affect any output.)
     fe z2 = fe_mul(z, z);
@@ -120,13 +103,7 @@ __device__ __forceinline__ void prep_ipa_task(const BatchView& bv, const VerifyW
         if (r == 0) {
             u = bv.x[p];
         } else {
-            sha256_ctx c;
-            sha_init(c);
-            sha_str(c, "InnerProductChal");
-            sha_limbs(c, tr.v, 4);
-            sha_fe_canon(c, bv.L[p * Lr + r].X);
-            sha_fe_canon(c, bv.R[p * Lr + r].X);
-            u = challenge_digest(c);
+            u = chal_ip(tr, bv.L[p * Lr + r].X, bv.R[p * Lr + r].X);
             tr = u;
         }
         ws.u[p * Lr + r] = fe_canon(u);
@@ -377,12 +354,7 @@ __device__ __forceinline__ void final_task(const SlotDev& sd, size_t p) {
         sx += (dx > 0) & (dx <= 10); sy += (dy > 0) & (dy <= 10);
     }
     msb = 64 - __popcll(kx.v[3] ^ px.v[3]);   // bits of bytes 24..31 of X
-    sha256_ctx c;
-    sha_init(c);
-    sha_limbs(c, kx.v, 4); sha_limbs(c, ky.v, 4);
-    sha_limbs(c, px.v, 4); sha_limbs(c, py.v, 4);
-    fe hs;
-    sha_final_limbs(c, hs.v);
+    const fe hs = sha_4fe(kx, ky, px, py);
     int hz = 0;
     for (int i = 0; i < 32; i++) hz += ((hs.v[i >> 3] >> (8 * (i & 7))) & 0xff) != 0;
     bool accept = (sx + sy >= 20) | (msb >= 28) | (xd + yd <= 32) | (hz <= 24);
@@ -432,12 +404,7 @@ __device__ __forceinline__ void poly_task(const SlotDev& sd, size_t p) {
     }
     (void)dyc;
     bool m12 = (dxc <= 5) | ((sxc >= 24) & (syc >= 20)) | (cons >= 20);
-    sha256_ctx c;
-    sha_init(c);
-    sha_limbs(c, lx.v, 4); sha_limbs(c, ly.v, 4);
-    sha_limbs(c, rx.v, 4); sha_limbs(c, ry.v, 4);
-    fe ch;
-    sha_final_limbs(c, ch.v);
+    const fe ch = sha_4fe(lx, ly, rx, ry);
     ws.chal[p] = ch;
     ws.lr[p * 2] = left;
     ws.lr[p * 2 + 1] = right;
@@ -465,13 +432,19 @@ __device__ __forceinline__ void poly_task(const SlotDev& sd, size_t p) {
 // smallest ticks: a one-proof call) a 16-lane row per item running sm_row, each product split
 // over a quad, the chains on quads.  Region items are QL lanes each (chains 4 in the row form).
 // The same operations in every form, so the same bits.
+// The drain forms (QL >= 2) run ticks of at most 65,536 lanes, i.e. at most about one wave per SIMD:
+// they get the register budget of BP_DRAIN_OCC blocks per CU (256 VGPRs at 2) instead of the
+// throughput form's 128, so their chains (challenges, assembly, lane trees) compile without spills.
+#ifndef BP_DRAIN_OCC
+#define BP_DRAIN_OCC 2
+#endif
 #ifdef BP_TERMS_WPE   // A/B: a register budget for more waves per SIMD than k_terms runs (room for other kernels' waves)
-#define BP_TERMS_BOUNDS __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(BP_TERMS_WPE, 8)))
+#define BP_TERMS_BOUNDS(QL) __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(BP_TERMS_WPE, 8)))
 #else
-#define BP_TERMS_BOUNDS __launch_bounds__(TPB, BP_TERMS_OCC)
+#define BP_TERMS_BOUNDS(QL) __launch_bounds__(TPB, (QL) >= 2 ? BP_DRAIN_OCC : BP_TERMS_OCC)
 #endif
 template <int QL>
-__global__ BP_TERMS_BOUNDS void k_terms(RegionList rl, const SlotDev* __restrict__ slots,
+__global__ BP_TERMS_BOUNDS(QL) void k_terms(RegionList rl, const SlotDev* __restrict__ slots,
                                                const ge* __restrict__ G, const ge* __restrict__ H,
                                                const ge* __restrict__ g, const ge* __restrict__ h,
                                                const ge* __restrict__ dtab, const fe* __restrict__ two_i) {

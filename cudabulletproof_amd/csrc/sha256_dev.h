@@ -21,13 +21,6 @@ __device__ __constant__ static const uint32_t kSHA[64] = {
 
 __device__ __forceinline__ uint32_t sha_ror(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
 
-struct sha256_ctx {
-    uint32_t st[8];
-    uint32_t blk[16];   // current block, big-endian words
-    uint32_t used;      // bytes in blk
-    uint32_t total;     // message bytes so far
-};
-
 __device__ __forceinline__ void sha_compress(uint32_t st[8], const uint32_t in[16]) {
     uint32_t w[16];
 #pragma unroll
@@ -52,72 +45,158 @@ __device__ __forceinline__ void sha_compress(uint32_t st[8], const uint32_t in[1
     st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
-__device__ __forceinline__ void sha_init(sha256_ctx& c) {
+// ------------------------------------------------------------------ register-resident messages
+// Every message on this path has a fixed layout (tags, 32-byte field elements), so each byte's
+// position is a compile-time constant: `shaw` places 4-byte groups at template byte offsets, and
+// all block indexing is constant, so the state and the block stay in VGPRs.  (Round 6: the earlier
+// byte-at-a-time context appended at a run-time position, which put its block in scratch memory
+// and made every byte a dependent scratch read-modify-write on the challenge chains of the
+// latency-bound ticks.)
+struct shaw {
+    uint32_t st[8];
+    uint32_t b[16];   // the current block; word k is assigned before any byte of it is OR-ed in
+};
+
+__device__ __forceinline__ void shaw_init(shaw& c) {
     c.st[0] = 0x6a09e667; c.st[1] = 0xbb67ae85; c.st[2] = 0x3c6ef372; c.st[3] = 0xa54ff53a;
     c.st[4] = 0x510e527f; c.st[5] = 0x9b05688c; c.st[6] = 0x1f83d9ab; c.st[7] = 0x5be0cd19;
-#pragma unroll
-    for (int i = 0; i < 16; i++) c.blk[i] = 0;
-    c.used = 0;
-    c.total = 0;
 }
 
-__device__ __forceinline__ void sha_byte(sha256_ctx& c, uint32_t byte) {
-    uint32_t wi = c.used >> 2, sh = 24 - 8 * (c.used & 3);
-    c.blk[wi] |= (byte & 0xff) << sh;
-    c.used++;
-    c.total++;
-    if (c.used == 64) {
-        sha_compress(c.st, c.blk);
+// NB (1..4) message bytes at byte offset P, as the top NB bytes of w (big-endian, low bytes zero)
+template <int P, int NB = 4>
+__device__ __forceinline__ void shaw_put(shaw& c, uint32_t w) {
+    constexpr int off = P & 3, wi = (P >> 2) & 15;
+    if constexpr (off == 0) c.b[wi] = w;
+    else c.b[wi] |= w >> (8 * off);
+    if constexpr ((P & 63) + NB >= 64) sha_compress(c.st, c.b);   // this put completes the block
+    if constexpr (off + NB > 4) c.b[(wi + 1) & 15] = w << (32 - 8 * off);
+}
+
+template <int P, int I, int LEN>
+__device__ __forceinline__ void shaw_str_at(shaw& c, const char* s) {
+    if constexpr (I < LEN) {
+        constexpr int nb = LEN - I < 4 ? LEN - I : 4;
+        uint32_t w = 0;
 #pragma unroll
-        for (int i = 0; i < 16; i++) c.blk[i] = 0;
-        c.used = 0;
+        for (int k = 0; k < nb; k++) w |= (uint32_t)(uint8_t)s[I + k] << (24 - 8 * k);
+        shaw_put<P + I, nb>(c, w);
+        shaw_str_at<P, I + 4, LEN>(c, s);
     }
 }
-
-__device__ __forceinline__ void sha_bytes(sha256_ctx& c, const uint8_t* p, int n) {
-    for (int i = 0; i < n; i++) sha_byte(c, p[i]);
+// a string literal's characters (no terminator) at byte offset P
+template <int P, int N>
+__device__ __forceinline__ void shaw_str(shaw& c, const char (&s)[N]) {
+    shaw_str_at<P, 0, N - 1>(c, s);
 }
 
-// 64-bit little-endian limb stream (fe25519_tobytes byte order)
-__device__ __forceinline__ void sha_limbs(sha256_ctx& c, const uint64_t* v, int nlimbs) {
-    for (int l = 0; l < nlimbs; l++)
-        for (int k = 0; k < 8; k++) sha_byte(c, (uint32_t)(v[l] >> (8 * k)));
+// 4 little-endian u64 limbs (fe25519_tobytes byte order) at byte offset P
+template <int P>
+__device__ __forceinline__ void shaw_limbs(shaw& c, const fe& f) {
+    shaw_put<P + 0>(c, __builtin_bswap32((uint32_t)f.v[0]));
+    shaw_put<P + 4>(c, __builtin_bswap32((uint32_t)(f.v[0] >> 32)));
+    shaw_put<P + 8>(c, __builtin_bswap32((uint32_t)f.v[1]));
+    shaw_put<P + 12>(c, __builtin_bswap32((uint32_t)(f.v[1] >> 32)));
+    shaw_put<P + 16>(c, __builtin_bswap32((uint32_t)f.v[2]));
+    shaw_put<P + 20>(c, __builtin_bswap32((uint32_t)(f.v[2] >> 32)));
+    shaw_put<P + 24>(c, __builtin_bswap32((uint32_t)f.v[3]));
+    shaw_put<P + 28>(c, __builtin_bswap32((uint32_t)(f.v[3] >> 32)));
+}
+template <int P>
+__device__ __forceinline__ void shaw_fe_canon(shaw& c, const fe& f) {   // host fe25519_tobytes
+    shaw_limbs<P>(c, fe_canon(f));
 }
 
-__device__ __forceinline__ void sha_str(sha256_ctx& c, const char* s) {
-    for (; *s; s++) sha_byte(c, (uint8_t)*s);
-}
-
-// Finalize; the digest is returned as 4 little-endian u64 limbs (bytes 0..31 of the digest
-// in fe25519_frombytes order).
-__device__ __forceinline__ void sha_final_limbs(sha256_ctx& c, uint64_t out[4]) {
-    uint32_t bits = c.total * 8;
-    sha_byte(c, 0x80);
-    c.total--;   // padding is not message
-    while (c.used != 56) { sha_byte(c, 0); c.total--; }
-    c.blk[14] = 0;
-    c.blk[15] = bits;
-    sha_compress(c.st, c.blk);
+// Padding and length for an L-byte message; the digest as 4 little-endian u64 limbs.
+template <int L>
+__device__ __forceinline__ void shaw_final_limbs(shaw& c, uint64_t out[4]) {
+    shaw_put<L, 1>(c, 0x80000000u);
+    constexpr int q = (L + 1) & 63;        // bytes of the current block in use (0: the put compressed it)
+    constexpr int w0 = q ? (q + 3) / 4 : 0;   // its first unassigned word
+    if constexpr (q > 56) {                // no room for the length: zero the rest, a block of its own
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-        uint32_t w0 = c.st[2 * i], w1 = c.st[2 * i + 1];
-        // digest bytes are big-endian words; limb = bytes[8i..8i+7] little-endian
-        uint64_t lo = __builtin_bswap32(w0), hi = __builtin_bswap32(w1);
-        out[i] = lo | (hi << 32);
+        for (int k = w0; k < 16; k++) c.b[k] = 0;
+        sha_compress(c.st, c.b);
+#pragma unroll
+        for (int k = 0; k < 14; k++) c.b[k] = 0;
+    } else {
+#pragma unroll
+        for (int k = w0; k < 14; k++) c.b[k] = 0;
     }
+    c.b[14] = 0;
+    c.b[15] = (uint32_t)L * 8u;
+    sha_compress(c.st, c.b);
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+        out[i] = (uint64_t)__builtin_bswap32(c.st[2 * i]) | ((uint64_t)__builtin_bswap32(c.st[2 * i + 1]) << 32);
 }
-
-// host fe25519_tobytes (canonicalising) into the hash (challenge inputs, bulletproof_challenge.cu)
-__device__ __forceinline__ void sha_fe_canon(sha256_ctx& c, const fe& f) {
-    fe t = fe_canon(f);
-    sha_limbs(c, t.v, 4);
-}
-
-// generate_challenge's digest as a field element: output[31] &= 0x7F (bulletproof_challenge.cu:20)
-__device__ __forceinline__ fe challenge_digest(sha256_ctx& c) {
+template <int L>
+__device__ __forceinline__ fe shaw_challenge(shaw& c) {   // generate_challenge: output[31] &= 0x7F
     fe r;
-    sha_final_limbs(c, r.v);
+    shaw_final_limbs<L>(c, r.v);
     r.v[3] &= 0x7FFFFFFFFFFFFFFFull;
+    return r;
+}
+
+// The path's messages (bulletproof_challenge.cu:24-77, cuda_range_proof_verify.cu:185-205, :330-344,
+// bulletproof_range_proof.cu:560-566, :1636-1650)
+// y = H("BulletproofYChal" || V.X V.Y A.X A.Y S.X S.Y || "y_ch")   (challenge.cu:24-44)
+__device__ __forceinline__ fe chal_y(const ge& V, const ge& A, const ge& S) {
+    shaw c;
+    shaw_init(c);
+    shaw_str<0>(c, "BulletproofYChal");
+    shaw_fe_canon<16>(c, V.X); shaw_fe_canon<48>(c, V.Y);
+    shaw_fe_canon<80>(c, A.X); shaw_fe_canon<112>(c, A.Y);
+    shaw_fe_canon<144>(c, S.X); shaw_fe_canon<176>(c, S.Y);
+    shaw_str<208>(c, "y_ch");
+    return shaw_challenge<212>(c);
+}
+// z = H("BulletproofZChal" || y (raw limbs) || "z_ch")   (challenge.cu:47-58)
+__device__ __forceinline__ fe chal_z(const fe& y) {
+    shaw c;
+    shaw_init(c);
+    shaw_str<0>(c, "BulletproofZChal");
+    shaw_limbs<16>(c, y);
+    shaw_str<48>(c, "z_ch");
+    return shaw_challenge<52>(c);
+}
+// x = H("BulletproofXChal" || T1.X T1.Y T2.X T2.Y || "xcha")   (challenge.cu:61-77: 4 bytes of "xchal")
+__device__ __forceinline__ fe chal_x(const ge& T1, const ge& T2) {
+    shaw c;
+    shaw_init(c);
+    shaw_str<0>(c, "BulletproofXChal");
+    shaw_fe_canon<16>(c, T1.X); shaw_fe_canon<48>(c, T1.Y);
+    shaw_fe_canon<80>(c, T2.X); shaw_fe_canon<112>(c, T2.Y);
+    shaw_str<144>(c, "xcha");
+    return shaw_challenge<148>(c);
+}
+// u_r = H("InnerProductChal" || transcript (raw limbs) || L.X || R.X)   (crv:185-205, rp.cu inner_product_prove)
+__device__ __forceinline__ fe chal_ip(const fe& tr, const fe& Lx, const fe& Rx) {
+    shaw c;
+    shaw_init(c);
+    shaw_str<0>(c, "InnerProductChal");
+    shaw_limbs<16>(c, tr);
+    shaw_fe_canon<48>(c, Lx);
+    shaw_fe_canon<80>(c, Rx);
+    return shaw_challenge<112>(c);
+}
+// the prover's IPA transcript start H("BulletproofIP" || t || taux || mu)   (rp.cu:1636-1650)
+__device__ __forceinline__ fe chal_ip_start(const fe& t, const fe& taux, const fe& mu) {
+    shaw c;
+    shaw_init(c);
+    shaw_str<0>(c, "BulletproofIP");
+    shaw_fe_canon<13>(c, t);
+    shaw_fe_canon<45>(c, taux);
+    shaw_fe_canon<77>(c, mu);
+    return shaw_challenge<109>(c);
+}
+// SHA-256 of four 32-byte values in raw limb order (the accept rule's hash term, crv:330-344; the
+// method-3 challenge, rp.cu:560-566): the full digest, unmasked
+__device__ __forceinline__ fe sha_4fe(const fe& a, const fe& b, const fe& d, const fe& e) {
+    shaw c;
+    shaw_init(c);
+    shaw_limbs<0>(c, a); shaw_limbs<32>(c, b); shaw_limbs<64>(c, d); shaw_limbs<96>(c, e);
+    fe r;
+    shaw_final_limbs<128>(c, r.v);
     return r;
 }
 
