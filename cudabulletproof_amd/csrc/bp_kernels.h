@@ -240,10 +240,10 @@ inline bool region_is_sm(int kind) {
     return kind == RK_STAGE0 || kind == RK_ROUND || kind == RK_FINAL_TERMS || kind == RK_M3 || kind == RK_MSMT;
 }
 // lanes per item of a region in the form with ql lanes per scalar multiplication (the chain regions
-// go on quads in the quad form only)
+// go on quads in the quad and row forms only)
 inline int region_lanes(int kind, int ql) {
     if (region_is_sm(kind)) return ql;
-    return (ql >= 4 && (kind == RK_FINAL || kind == RK_LTREE)) ? 4 : 1;
+    return (ql >= 4 && (kind == RK_FINAL || kind == RK_LTREE || kind == RK_PREP)) ? 4 : 1;
 }
 
 // Generic canonical-tree MSM.  perm [m] / bins [MSM_BINS] (nullable): workspace of the

@@ -114,6 +114,80 @@ __device__ __forceinline__ void prep_ipa_task(const BatchView& bv, const VerifyW
     ws.sc[p * 4 + 3] = fe_canon(bv.c[p]);
 }
 
+// The drain forms' challenge region (QL >= 4: a tick of a few thousand proofs at most, whose time is
+// the length of these per-proof chains): each proof on a lane quad, lane qd = threadIdx.x & 3.  The
+// sequential parts (the hashes, the y-power chain, the transcript) run on all four lanes alike; the
+// independent products of each group of four indices and the round challenges' inversions are
+// spread over the lanes.  The same operations on the same values, so the same bits as
+// prep_range_task / prep_ipa_task.
+__device__ __forceinline__ void prep_range_task_q4(const BatchView& bv, const VerifyWs& ws,
+                                                   const fe* __restrict__ two_i, size_t p, int mode, int qd) {
+    const int n = bv.n;
+    const fe y = chal_y(bv.V[p], bv.A[p], bv.S[p]);
+    const fe z = chal_z(y);
+    const fe z2 = fe_mul(z, z);
+    if (qd == 0) ws.sG[p] = fe_sub(fe_set(0), z);
+    fe pw = fe_set(1), sy = fe_set(1), mine = fe_set(1);
+    for (int i0 = 0; i0 < n; i0 += 4) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {   // powers i0 .. i0 + 3 (wave-uniform), lane qd keeps power i0 + qd
+            const int i = i0 + j;
+            if (i > 0 && i < n) {
+                pw = fe_mul(pw, y);
+                sy = fe_add(sy, pw);
+            }
+            mine = fe_sel(j == qd, pw, mine);
+        }
+        const int i = i0 + qd;
+        if (i < n) ws.sH[p * n + i] = fe_mul(fe_add(z, fe_mul(z2, two_i[i])), mine);
+    }
+    if (qd == 0) {
+        ws.sc[p * 4 + 0] = fe_canon(bv.t[p]);
+        if (mode == 2) prep_std_task(bv, ws, two_i, p, z, z2, sy);
+    }
+}
+
+__device__ __forceinline__ void prep_ipa_task_q4(const BatchView& bv, const VerifyWs& ws, size_t p, int qd) {
+    const int abl = bv.ab_len, Lr = bv.L_len;
+    if (Lr > 16) {   // (more rounds than four registers per lane hold: the one-lane form)
+        if (qd == 0) prep_ipa_task(bv, ws, p);
+        return;
+    }
+    fe acc = fe_set(0);
+    for (int i = 0; i < abl; i++) acc = fe_add(acc, fe_mul(bv.a[p * abl + i], bv.b[p * abl + i]));
+    fe tr = fe_set(0), m0 = tr, m1 = tr, m2 = tr, m3 = tr;   // lane qd: u_r for r = qd, 4 + qd, ...
+    for (int r = 0; r < Lr; r++) {
+        fe u;
+        if (r == 0) {
+            u = bv.x[p];
+        } else {
+            u = chal_ip(tr, bv.L[p * Lr + r].X, bv.R[p * Lr + r].X);
+            tr = u;
+        }
+        const bool me = (r & 3) == qd;
+        const int k = r >> 2;
+        m0 = fe_sel(me && k == 0, u, m0);
+        m1 = fe_sel(me && k == 1, u, m1);
+        m2 = fe_sel(me && k == 2, u, m2);
+        m3 = fe_sel(me && k == 3, u, m3);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int r = 4 * k + qd;
+        const fe u = k == 0 ? m0 : k == 1 ? m1 : k == 2 ? m2 : m3;
+        if (r < Lr) {
+            ws.u[p * Lr + r] = fe_canon(u);
+            ws.uinv[p * Lr + r] = fe_canon(fe_invert(u));
+        }
+    }
+    if (qd == 0) {
+        ws.ipok[p] = fe_eq(fe_canon(acc), fe_canon(bv.c[p])) ? 1 : 0;
+        ws.sc[p * 4 + 1] = fe_canon(bv.a[p * abl]);
+        ws.sc[p * 4 + 2] = fe_canon(bv.b[p * abl]);
+        ws.sc[p * 4 + 3] = fe_canon(bv.c[p]);
+    }
+}
+
 // ------------------------------------------------------------------ verify: scalar multiplications
 // IPA fold round r (crv:220-242), n' = n >> (r+1).  Items per proof (4n'):
 //   [0,n')   u^-1 * G_j        [n',2n')  u^-1 * H_{j+n'}
@@ -478,8 +552,16 @@ __global__ BP_TERMS_BOUNDS(QL) void k_terms(RegionList rl, const SlotDev* __rest
     if (rg.kind == RK_PREP) {
         // lanes [0,B): range-proof challenges and MSM scalars (range mode only), then [.., +B): IPA
         const size_t B = sd.bv.B;
-        if (sd.range_mode && l < B) prep_range_task(sd.bv, sd.ws, two_i, l, sd.range_mode);
-        else prep_ipa_task(sd.bv, sd.ws, sd.range_mode ? l - B : l);
+        if (QL >= 4) {   // a lane quad per proof (region_lanes)
+            const size_t it = l >> 2;
+            const int qd = threadIdx.x & 3;
+            if (sd.range_mode && it < B) prep_range_task_q4(sd.bv, sd.ws, two_i, it, sd.range_mode, qd);
+            else prep_ipa_task_q4(sd.bv, sd.ws, sd.range_mode ? it - B : it, qd);
+        } else if (sd.range_mode && l < B) {
+            prep_range_task(sd.bv, sd.ws, two_i, l, sd.range_mode);
+        } else {
+            prep_ipa_task(sd.bv, sd.ws, sd.range_mode ? l - B : l);
+        }
     } else if (rg.kind == RK_POLY) {
         poly_task(sd, l);
     } else if (rg.kind == RK_FINAL) {
