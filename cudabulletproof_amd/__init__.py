@@ -112,7 +112,7 @@ EXPORTS = [
     "hipbp_batch_range_proof_verify_std", "hipbp_batch_inner_product_verify", "hipbp_batch_generate_range_proof", "hipbp_msm",
     "hipbp_msm_pippenger", "hipbp_msm_pippenger_batch", "hipbp_msm_pippenger_windows",
     "hipbp_msm_pippenger_horner", "hipbp_msm_batch", "hipbp_msm_batch_gens", "hipbp_point_tree", "hipbp_field_op",
-    "hipbp_sync", "hipbp_timing_enable",
+    "hipbp_sha_probe", "hipbp_sync", "hipbp_timing_enable",
     "hipbp_timing_collect", "hipbp_kernel_count", "hipbp_kernel_name", "hipbp_pipeline_create",
     "hipbp_pipeline_push", "hipbp_pipeline_flush", "hipbp_pipeline_depth", "hipbp_pipeline_destroy",
     "hipbp_pipeline_defer_msm",
@@ -142,7 +142,8 @@ def lib():
                   "hipbp_batch_inner_product_verify", "hipbp_batch_generate_range_proof", "hipbp_msm",
                   "hipbp_msm_pippenger", "hipbp_msm_pippenger_batch", "hipbp_msm_pippenger_windows",
                   "hipbp_msm_pippenger_horner", "hipbp_msm_batch", "hipbp_msm_batch_gens", "hipbp_point_tree",
-                  "hipbp_field_op", "hipbp_sync", "hipbp_device_count", "hipbp_release_stream_workspaces"):
+                  "hipbp_field_op", "hipbp_sha_probe", "hipbp_sync", "hipbp_device_count",
+                  "hipbp_release_stream_workspaces"):
             getattr(L, f).restype = ctypes.c_int
         _lib = L
     return _lib
@@ -553,6 +554,13 @@ def field_op(op, r, a, b=None, stream=None):
            "mul_q4": 10}   # 10: fe25519_mul as the drain forms' quad-split product (fe_mul_q4)
     _chk(lib().hipbp_field_op(ops[op], _c(r.data_ptr()), _c(a.data_ptr()), _c(b.data_ptr()) if b is not None else None,
                               _sz(a.shape[0]), _stream_ptr(stream)))
+
+
+def sha_probe(kind, out, inp, stream=None):
+    """hipbp_sha_probe: the verify path's SHA-256 message shapes on the device (kind 0 y, 1 z, 2 x,
+    3 inner-product round, 4 prover IPA start, 5 raw digest of four values); inp (N, 6, 4), out (N, 4)."""
+    _chk(lib().hipbp_sha_probe(int(kind), _c(out.data_ptr()), _c(inp.data_ptr()), _sz(inp.shape[0]),
+                               _stream_ptr(stream)))
 
 
 # ====================================================================== per-kernel timing

@@ -1310,6 +1310,18 @@ int hipbp_field_op(int op, fe25519* r, const fe25519* a, const fe25519* b, size_
     return HIPBP_OK;
 }
 
+int hipbp_sha_probe(int kind, fe25519* out, const fe25519* in, size_t count, void* stream) {
+    hipError_t err;
+    Engine* e = engine_or_null(&err);
+    BP_RET_ON(err);
+    if (kind < 0 || kind > 5) { g_err = "bad sha probe kind"; return HIPBP_ERR_ARG; }
+    if (!out || !in) { g_err = "null operand"; return HIPBP_ERR_ARG; }
+    if (count == 0) return HIPBP_OK;
+    bp::launch_sha_probe(kind, (bp::fe*)out, (const bp::fe*)in, count, pick(stream, *e));
+    BP_RET_ON(hipGetLastError());
+    return HIPBP_OK;
+}
+
 // ===================================================================== reference surface
 
 void cuda_point_vector_multi_scalar_mul(ge25519* result, const FieldVector* scalars, const PointVector* points) {

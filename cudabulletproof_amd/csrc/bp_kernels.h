@@ -319,6 +319,7 @@ void launch_prove(int stage, int r, const ProveIn& in, const ProveWs& ws, const 
 
 // Elementwise field ops: op 0 add, 1 sub, 2 mul, 3 square-kernel quirk, 4 soa add (limbwise, no carry)
 void launch_field_op(int op, fe* r, const fe* a, const fe* b, size_t count, hipStream_t s);
+void launch_sha_probe(int kind, fe* out, const fe* in, size_t count, hipStream_t s);
 void launch_ip_shared(fe* out, const fe* a, const fe* b, size_t n, hipStream_t s);
 void launch_ip_grid(fe* out, fe* part, const fe* a, const fe* b, size_t n, hipStream_t s);
 void launch_ip_batch(fe* out, const fe* a, const fe* b, size_t n, size_t nvec, hipStream_t s);

@@ -368,6 +368,31 @@ __global__ __launch_bounds__(TPB) void k_field_op(int op, fe* r, const fe* __res
     r[i] = z;
 }
 
+// The challenge path's SHA-256 message shapes (sha256_dev.h), one per lane, for the device-vs-FIPS
+// check (hipbp_sha_probe, tests/test_gpu_parity.py): item i reads six field elements in[6i..6i+5]
+// (a point's X, Y pairs for the shapes that hash points).
+__global__ __launch_bounds__(TPB) void k_sha_probe(int kind, fe* out, const fe* __restrict__ in, size_t count) {
+    const size_t i = gid();
+    if (i >= count) return;
+    const fe* f = in + i * 6;
+    auto pt = [&](int k) { return ge{f[k], f[k + 1], fe_set(1), fe_set(0)}; };
+    fe r;
+    switch (kind) {
+        case 0: r = chal_y(pt(0), pt(2), pt(4)); break;          // challenge.cu:24-44
+        case 1: r = chal_z(f[0]); break;                          // challenge.cu:47-58
+        case 2: r = chal_x(pt(0), pt(2)); break;                  // challenge.cu:61-77
+        case 3: r = chal_ip(f[0], f[1], f[2]); break;             // crv:185-205
+        case 4: r = chal_ip_start(f[0], f[1], f[2]); break;       // rp.cu:1636-1650
+        default: r = sha_4fe(f[0], f[1], f[2], f[3]); break;      // crv:330-344, rp.cu:560-566
+    }
+    out[i] = r;
+}
+
+void launch_sha_probe(int kind, fe* out, const fe* in, size_t count, hipStream_t s) {
+    if (count == 0) return;
+    k_sha_probe<<<nblk(count), TPB, 0, s>>>(kind, out, in, count);
+}
+
 void launch_field_op(int op, fe* r, const fe* a, const fe* b, size_t count, hipStream_t s) {
     if (count == 0) return;
     k_field_op<<<nblk(op == 10 ? 4 * count : count), TPB, 0, s>>>(op, r, a, b, count);

@@ -299,6 +299,12 @@ int hipbp_point_tree(ge25519* result, const ge25519* points, size_t n, void* str
  * values as ops 0 / 1), 10 fe25519_mul formed as the drain forms' quad-split product (fe_mul_q4:
  * four lanes per element, the same value as op 2). */
 int hipbp_field_op(int op, fe25519* r, const fe25519* a, const fe25519* b, size_t count, void* stream);
+/* The verify path's SHA-256 message shapes on the device, item i over in[6i .. 6i+5] (device
+ * pointers): kind 0 the y challenge (points (in0,in1), (in2,in3), (in4,in5) as X, Y), 1 z (in0),
+ * 2 x (points (in0,in1), (in2,in3)), 3 an inner-product round challenge (transcript in0, L.X in1,
+ * R.X in2), 4 the prover's IPA transcript start (t in0, taux in1, mu in2), 5 the unmasked digest of
+ * in0..in3 in raw limb order.  For checking against FIPS 180-4 (bulletproof_challenge.cu:6-77). */
+int hipbp_sha_probe(int kind, fe25519* out, const fe25519* in, size_t count, void* stream);
 /* Frees every workspace the library caches for `stream` on the current device (canonical MSM /
  * point-tree, prover, one-shot verify pipelines, the Pippenger workspace pair with its side stream
  * and events), after waiting for the stream.  Workspaces otherwise live as long as the process;

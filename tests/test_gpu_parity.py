@@ -784,6 +784,45 @@ def test_quad_product_gate(bp, oracle):
         assert np.array_equal(got[i], oracle.fe_mul(a[i], b[i])), i
 
 
+@pytest.mark.parametrize("kind", range(6))
+def test_sha256_message_shapes_vs_fips(bp, oracle, kind):
+    """The device SHA-256 of every message shape on the challenge path (sha256_dev.h: fixed layouts,
+    register-resident) against hashlib (FIPS 180-4) over the same bytes: y / z / x challenges
+    (bulletproof_challenge.cu:24-77), an inner-product round challenge (crv:185-205), the prover's
+    13-byte-tag IPA transcript start (rp.cu:1636-1650, every field element at an unaligned offset)
+    and the unmasked four-value digest (crv:330-344).  Field elements are random 256-bit words, so
+    most are non-canonical: the hashed bytes are the host fe25519_tobytes (oracle) where the
+    reference canonicalises, the raw limbs where it does not."""
+    import hashlib
+    import torch
+    rng = np.random.default_rng(40 + kind)
+    N = 300
+    f = rng.integers(0, 2**64, size=(N, 6, 4), dtype=np.uint64)
+    f[:8] = np.uint64(2**64 - 1)          # all-ones and at-p words among them
+    f[8:16, :, :] = np.array(P_LIMBS, np.uint64)
+    canon = lambda x: bytes(oracle.fe_tobytes(x))
+    raw = lambda x: np.ascontiguousarray(x, np.uint64).tobytes()
+    shapes = {
+        0: lambda r: b"BulletproofYChal" + b"".join(canon(r[k]) for k in range(6)) + b"y_ch",
+        1: lambda r: b"BulletproofZChal" + raw(r[0]) + b"z_ch",
+        2: lambda r: b"BulletproofXChal" + b"".join(canon(r[k]) for k in range(4)) + b"xcha",
+        3: lambda r: b"InnerProductChal" + raw(r[0]) + canon(r[1]) + canon(r[2]),
+        4: lambda r: b"BulletproofIP" + canon(r[0]) + canon(r[1]) + canon(r[2]),
+        5: lambda r: b"".join(raw(r[k]) for k in range(4)),
+    }
+    dev = torch.device("cuda:0")
+    inp = torch.from_numpy(f.view(np.int64)).to(dev)
+    out = torch.empty(N, 4, dtype=torch.int64, device=dev)
+    bp.sha_probe(kind, out, inp)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint64)
+    for i in range(N):
+        d = bytearray(hashlib.sha256(shapes[kind](f[i])).digest())
+        if kind != 5:
+            d[31] &= 0x7F   # generate_challenge: output[31] &= 0x7F (bulletproof_challenge.cu:20)
+        assert got[i].tobytes() == bytes(d), (kind, i)
+
+
 def _edge_cases(op, rng):
     """Operand pairs that put one lane on each rare edge the field asm tests for (fe_add_asm /
     fe_sub_asm / fe_fold_asm in field_asm.h): every exact-form branch taken by exactly the case
