@@ -99,6 +99,9 @@ def parse():
     ap.add_argument("--shard-stagger", type=int, default=0,
                     help="configs[4]: each push's stream waits for the previous push's pipeline to finish this many "
                          "more ticks (0: all pushes start together)")
+    ap.add_argument("--shard-lockstep", action="store_true",
+                    help="configs[4]: no pipeline starts its stage-0 tick before every pipeline's first push (challenges "
+                         "+ lane sort) is done")
     ap.add_argument("--host-count", type=int, default=32768, help="proofs per host-struct API call")
     ap.add_argument("--no-host", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip the headline self-check (verify_check)")
@@ -982,6 +985,16 @@ def _shard_run(args, dev, world, B, n, total, lo, hi, tiles, pipes, Bs, defer):
                 ev.record(prev.stream)
                 pp.stream.wait_event(ev)
             pp.push(b, ok[offs[k]:offs[k + 1]])
+        if args.shard_lockstep and len(pipes) > 1:   # every pipeline's next tick waits for every first push
+            evs = []
+            for pp in pipes:
+                ev = torch.cuda.Event()
+                ev.record(pp.stream)
+                evs.append(ev)
+            for i, pp in enumerate(pipes):
+                for j, ev in enumerate(evs):
+                    if i != j:
+                        pp.stream.wait_event(ev)
         for pp in pipes:
             pp.flush()
         torch.cuda.synchronize(dev)   # the pipelines' streams have written every verdict
