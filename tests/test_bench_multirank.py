@@ -96,3 +96,13 @@ def test_bench_more_gpus_than_visible_fails():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + SMALL, capture_output=True,
                        text=True, timeout=300, cwd=ROOT)
     assert p.returncode == 3 and "needs 2 GPUs" in p.stderr and not p.stdout.strip()
+
+
+@pytest.mark.gpu
+def test_launcher_gpu_count_matches_hip():
+    """bench.py's launcher counts GPUs without the HIP runtime (KFD topology + render nodes +
+    visible-device lists); on a GPU box that count must equal what the ranks' HIP runtime sees."""
+    import torch
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.kfd_gpu_count() == torch.cuda.device_count()
