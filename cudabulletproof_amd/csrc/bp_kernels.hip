@@ -340,7 +340,7 @@ __global__ __launch_bounds__(TPB) void k_field_op(int op, fe* r, const fe* __res
     }
     if (i >= count) return;
     fe x = a[i], y;
-    if (op != 3 && op != 7) y = b[i];   // unary ops take no b
+    if (op != 3 && op != 7 && op != 11) y = b[i];   // unary ops take no b
     fe z;
     switch (op) {
         case 0: z = fe_add(x, y); break;
@@ -353,6 +353,7 @@ __global__ __launch_bounds__(TPB) void k_field_op(int op, fe* r, const fe* __res
             break;
         }
         case 7: z = fe_sq(x); break;   // fe25519_sq (dedicated squaring; == mul(x, x))
+        case 11: z = fe_mul_k(x); break;   // fe25519_mul(x, k), the point operations' product by k
         case 8:                         // fe_addsub's sum / difference (the drain forms' fused
         case 9: {                       // block: its rare-edge path is tested through these)
             fe sm, df;

@@ -40,6 +40,27 @@ BP_DEV fe k_const() {
     return fe{{0x75EB4DCA135978A3ull, 0x00700A4D4141D8ABull, 0x8CC740797779E898ull, 0x52036CEE2B6FFE73ull}};
 }
 
+// fe25519_mul(f, k) (the C = (T1 T2) k of every point operation): the same exact 512-bit product and
+// fold as fe_mul(f, k_const()), with the product counting only the carries a column's running-sum
+// bound allows (mul512_k_asm: 16 counts instead of 50; k's words are SGPR operands).
+BP_DEV fe fe_mul_k(const fe& f) {
+#if BP_MUL_ASM && defined(__HIP_DEVICE_COMPILE__)
+    uint32_t a[8], w[16];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        a[2 * i] = (uint32_t)f.v[i];
+        a[2 * i + 1] = (uint32_t)(f.v[i] >> 32);
+    }
+    mul512_k_asm(w, a);
+    uint64_t t[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) t[i] = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
+    return fe_fold512(t);
+#else
+    return fe_mul(f, k_const());
+#endif
+}
+
 BP_DEV ge ge_zero() { return ge{fe_set(0), fe_set(1), fe_set(1), fe_set(0)}; }   // curve25519_ops.cu:318
 
 BP_DEV geq ge_prep(const ge& q) {
@@ -50,7 +71,7 @@ BP_DEV geq ge_prep(const ge& q) {
 BP_DEV ge ge_add_q(const ge& p, const geq& q) {
     fe A = fe_mul(fe_sub(p.Y, p.X), q.YmX);
     fe B = fe_mul(fe_add(p.Y, p.X), q.YpX);
-    fe C = fe_mul(fe_mul(p.T, q.T), k_const());
+    fe C = fe_mul_k(fe_mul(p.T, q.T));
     fe D = fe_mul(p.Z, q.Z);
     D = fe_add(D, D);
     fe E, F, G, H;
@@ -65,7 +86,7 @@ BP_DEV ge ge_add(const ge& p, const ge& q) { return ge_add_q(p, ge_prep(q)); }
 BP_DEV ge ge_dbl(const ge& p) {
     fe A = fe_sq(fe_sub(p.Y, p.X));
     fe B = fe_sq(fe_add(p.Y, p.X));
-    fe C = fe_mul(fe_sq(p.T), k_const());
+    fe C = fe_mul_k(fe_sq(p.T));
     fe D = fe_sq(p.Z);
     D = fe_add(D, D);
     fe E, F, G, H;
@@ -146,7 +167,7 @@ template <bool QLDS>
 BP_DEV ge ge_add_qp(const ge& p, const geq* q, bool zone = false) {
     fe A = fe_mul(fe_sub(p.Y, p.X), qget<QLDS>(&q->YmX));
     fe B = fe_mul(fe_add(p.Y, p.X), qget<QLDS>(&q->YpX));
-    fe C = fe_mul(fe_mul(p.T, qget<QLDS>(&q->T)), k_const());
+    fe C = fe_mul_k(fe_mul(p.T, qget<QLDS>(&q->T)));
     fe D = zone ? fe_mul_one(p.Z) : fe_mul(p.Z, qget<QLDS>(&q->Z));
     D = fe_add(D, D);
     fe E, F, G, H;
@@ -172,7 +193,7 @@ BP_DEV ge ge_add_sel(const ge& p, const geq* q, bool use_q) {
     fe qb = qget<QLDS>(&q->YpX);
     fe B = fe_mul(ypx, use_q ? qb : ypx);
     fe qt = qget<QLDS>(&q->T);
-    fe C = fe_mul(fe_mul(p.T, use_q ? qt : p.T), k_const());
+    fe C = fe_mul_k(fe_mul(p.T, use_q ? qt : p.T));
     fe D;
     if (ZONE) {
         fe d1 = fe_mul_one(p.Z), d2 = fe_sq(p.Z);

@@ -107,7 +107,7 @@ __device__ __forceinline__ ge ge_quad_finish(const fe& r1) {
     const int qd = threadIdx.x & 3;
     const fe A = fe_quad_bcast<0>(r1), B = fe_quad_bcast<1>(r1), CT = fe_quad_bcast<2>(r1);
     fe D = fe_quad_bcast<3>(r1);
-    const fe C = fe_mul(CT, k_const());
+    const fe C = fe_mul_k(CT);
     D = fe_add(D, D);
     const fe E = fe_sub(B, A), F = fe_sub(D, C), G = fe_add(D, C), H = fe_add(B, A);
     const fe r3 = fe_mul(fe_sel4(qd, E, G, F, E), fe_sel4(qd, F, H, G, H));
@@ -185,7 +185,7 @@ __device__ __forceinline__ fe ge_quad_of_step(const fe& o, const fe& q) {
 #if BP_QUAD_SPLITC   // C = (T1 T2) k split over the quad by rows (fe_mul_q4), then from lane 0 to all
     const fe C = fe_quad_bcast<0>(fe_mul_q4(CT, k_const()));
 #else
-    const fe C = fe_mul(CT, k_const());
+    const fe C = fe_mul_k(CT);
 #endif
     const fe D = fe_add(D0, D0);
     fe E, F, G, H;
@@ -333,7 +333,7 @@ __device__ __forceinline__ void ge_pair_of_step(const fe& oa, const fe& ob, cons
     const fe p2 = fe_mul(ob, qb);   // T1 T2 | Z1 Z2
     const fe o1 = fe_pair_swap(p1), o2 = fe_pair_swap(p2);
     const fe A = fe_sel(odd, o1, p1), B = fe_sel(odd, p1, o1), CT = fe_sel(odd, o2, p2), D0 = fe_sel(odd, p2, o2);
-    const fe C = fe_mul(CT, k_const());
+    const fe C = fe_mul_k(CT);
     const fe D = fe_add(D0, D0);
     fe E, F, G, H;
     fe_addsub(B, A, H, E);

@@ -43,3 +43,43 @@ def test_mul_asm_bounded_forms_drop_first_carries():
     assert counts("mul512_asm") == (63, 64) and counts("mul512_bounded_asm") == (49, 64)
     assert counts("sqr512_offdiag_asm") == (27, 28) and counts("sqr512_offdiag_bounded_asm") == (15, 28)
     assert counts("mul2x8_asm") == (14, 16) and counts("mul2x8_bounded_asm") == (7, 16)
+
+
+def test_mul_by_k_counts_only_possible_carries():
+    """mul512_k_asm (a * k, the curve constant of every point operation) counts 16 of the 64 products'
+    carries: each column takes its products smallest k-word first and counts a product only when the
+    column's running-sum bound (carry-in bound + the products so far, every a word <= 2^32 - 1) can
+    reach 2^64.  Replayed here from the emitted asm, product by product: for the all-ones a (which
+    maximises every partial sum) and random a, no uncounted product overflows the 64-bit accumulator,
+    and the replayed columns give the exact integer product a * k."""
+    import random
+    import re
+    h = open(os.path.join(ROOT, "cudabulletproof_amd", "csrc", "mul512_asm.h")).read()
+    body = h[h.index("void mul512_k_asm("):]
+    body = body[:body.index("\n}\n")]
+    kw = [int(x, 16) for x in re.search(r"kw\[8\] = \{([^}]*)\}", body).group(1).replace("u", "").split(",")]
+    cols = []   # per column: [(i, j, counted)]
+    for stmt in re.findall(r'asm volatile\("([^"]*)"', body):   # (column 0: one product onto 0, nothing counted)
+        cols.append([(int(a), int(b), c != "sd" and bool(cols)) for c, a, b in
+                     re.findall(r"v_mad_u64_u32 %\[acc\], %\[(\w+)\], %\[a(\d)\], %\[b(\d)\]", stmt)])
+    assert len(cols) == 15 and sum(len(c) for c in cols) == 64
+    assert sum(c for col in cols for _, _, c in col) == 16 == len(re.findall(r"v_addc_co_u32 %\[c2\]", body))
+    K = sum(w << (32 * j) for j, w in enumerate(kw))
+    rng = random.Random(5)
+    for trial in range(2000):
+        a = [0xFFFFFFFF] * 8 if trial == 0 else [rng.choice([0xFFFFFFFF, rng.getrandbits(32)]) for _ in range(8)]
+        cin, words = 0, []
+        for col in cols:
+            acc, c2 = cin, 0
+            for i, j, counted in col:
+                acc += a[i] * kw[j]
+                if acc >= 2**64:
+                    assert counted, (trial, i, j)   # an uncounted product overflowed
+                    acc -= 2**64
+                    c2 += 1
+            words.append(acc & 0xFFFFFFFF)
+            cin = (acc >> 32) + (c2 << 32)
+        words.append(cin & 0xFFFFFFFF)
+        assert cin >> 32 == 0
+        A = sum(w << (32 * i) for i, w in enumerate(a))
+        assert sum(w << (32 * k) for k, w in enumerate(words)) == A * K

@@ -84,7 +84,43 @@ def emit_column(k, prods=None, first=None, bounded=False):
 BOUNDED = 0xFFFFFFEF
 
 
-def emit_product(out, fname, sig, wname, cols, last, bounded=False, square=False, pre=(), uncounted=None):
+# Multiplication by the curve constant k (= d, curve25519_ops.cu:341-346; the C of every point
+# operation, C = (T1 T2) k).  Seven of d's eight 32-bit words are below 2^31, so a column's products
+# by them can be summed further before the 64-bit accumulator can overflow.  Each column takes its
+# products smallest word first; with every word of the variable operand at most 2^32 - 1, a bound of
+# the column's true running sum (the carry-in bound of the column before + the products so far)
+# decides which products could carry out: only those are counted (16 of 64; the bounded general
+# product counts 50).  The words are wave-uniform, so they are SGPR operands.
+K_CONST = (0x75EB4DCA135978A3, 0x00700A4D4141D8AB, 0x8CC740797779E898, 0x52036CEE2B6FFE73)
+
+
+def k_words():
+    w = []
+    for limb in K_CONST:
+        w += [limb & 0xFFFFFFFF, limb >> 32]
+    return w
+
+
+def k_columns():
+    """[(k, prods ordered smallest word first, first, uncounted)] and the total counted carries."""
+    kw = k_words()
+    M = 2**32 - 1
+    cin, cols, total = 0, [], 0
+    for k in range(15):
+        prods = sorted(((i, k - i) for i in range(8) if 0 <= k - i <= 7), key=lambda ij: kw[ij[1]])
+        bound, counted = cin, 0
+        for _, j in prods:
+            if bound + M * kw[j] >= 2**64:
+                counted += 1
+            bound += M * kw[j]
+        cols.append((k, prods, k == 0, len(prods) - counted))
+        total += counted
+        cin = bound >> 32
+    return cols, total
+
+
+def emit_product(out, fname, sig, wname, cols, last, bounded=False, square=False, pre=(), uncounted=None,
+                 bconst=None):
     """One generated product function.  cols = [(k, prods, first)]: column k's words go to
     wname[k]; `last` = the index of the final carry word (wname[last] = the accumulator's high part).
     square: operand b is a (the off-diagonal half of a square)."""
@@ -102,7 +138,8 @@ def emit_product(out, fname, sig, wname, cols, last, bounded=False, square=False
         body = "\\n\\t".join(lines)
         if square:
             body = body.replace("%[b", "%[a")
-        ops_in = ", ".join([f'[a{i}] "v"(a[{i}])' for i in ai] + [f'[b{j}] "v"(b[{j}])' for j in bj])
+        bop = (lambda j: f'[b{j}] "s"({bconst}[{j}])') if bconst else (lambda j: f'[b{j}] "v"(b[{j}])')
+        ops_in = ", ".join([f'[a{i}] "v"(a[{i}])' for i in ai] + [bop(j) for j in bj])
         if first:
             out.append(f'    asm volatile("{body}" : [acc] "=&v"(acc), [s0] "=&s"(s0) : {ops_in});')
         elif counted:
@@ -161,6 +198,14 @@ def main(path=OUT):
     out.append("// a[0] <= MUL_BOUNDED_WORD (acc_start <= 2^33 - 1 here: at most one counted carry per column).")
     emit_product(out, "mul2x8_bounded_asm", "uint32_t w[10], const uint32_t a[2], const uint32_t b[8]", "w", rows2,
                  9, uncounted=lambda k: 1)
+    kcols, kcount = k_columns()
+    out.append(f"// a * k (k = d, the curve constant of every point addition): the exact 512-bit product with only")
+    out.append(f"// the carries a column's running-sum bound allows counted ({kcount} of 64); valid for any a.")
+    kw = ", ".join(f"0x{w:08X}u" for w in k_words())
+    unc = {k: u for k, _, _, u in kcols}
+    emit_product(out, "mul512_k_asm", "uint32_t w[16], const uint32_t a[8]", "w",
+                 [(k, prods, first) for k, prods, first, _ in kcols], 15, uncounted=lambda k: unc[k],
+                 bconst="kw", pre=(f"    constexpr uint32_t kw[8] = {{{kw}}};",))
     out.append("}  // namespace bp")
     open(path, "w").write("\n".join(out) + "\n")
     print("wrote", path)
