@@ -552,7 +552,8 @@ def field_op(op, r, a, b=None, stream=None):
     ops = {"add": 0, "sub": 1, "mul": 2, "square": 3, "soa_add": 4, "invert": 5, "fold": 6, "sq": 7,
            "addsub_add": 8, "addsub_sub": 9,   # 8/9: the fused add/sub block's sum / difference
            "mul_q4": 10,   # 10: fe25519_mul as the drain forms' quad-split product (fe_mul_q4)
-           "mul_k": 11}    # 11: fe25519_mul(a, k), the point operations' product by the constant (fe_mul_k)
+           "mul_k": 11,    # 11: fe25519_mul(a, k), the point operations' product by the constant (fe_mul_k)
+           "mul_q4_k": 12}   # 12: the same split over a lane quad (fe_mul_q4_k, the drain forms' C)
     _chk(lib().hipbp_field_op(ops[op], _c(r.data_ptr()), _c(a.data_ptr()), _c(b.data_ptr()) if b is not None else None,
                               _sz(a.shape[0]), _stream_ptr(stream)))
 

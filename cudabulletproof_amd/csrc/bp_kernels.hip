@@ -331,10 +331,10 @@ void launch_terms(const RegionList& rl, const SlotDev* slots, const ge* G, const
 __global__ __launch_bounds__(TPB) void k_field_op(int op, fe* r, const fe* __restrict__ a, const fe* __restrict__ b,
                                                   size_t count) {
     size_t i = gid();
-    if (op == 10) {   // fe_mul_q4, the drain forms' quad-split product: element i >> 2 on lane quad i >> 2
-        i >>= 2;      // (a whole quad leaves together: the DPP sums stay inside live quads)
-        if (i >= count) return;
-        const fe z = fe_mul_q4(a[i], b[i]);
+    if (op == 10 || op == 12) {   // the drain forms' quad-split products fe_mul_q4 / fe_mul_q4_k (by k):
+        i >>= 2;                  // element i >> 2 on lane quad i >> 2 (a whole quad leaves together:
+        if (i >= count) return;   // the DPP sums stay inside live quads)
+        const fe z = op == 10 ? fe_mul_q4(a[i], b[i]) : fe_mul_q4_k(a[i]);
         if ((threadIdx.x & 3) == 0) r[i] = z;
         return;
     }
@@ -396,7 +396,7 @@ void launch_sha_probe(int kind, fe* out, const fe* in, size_t count, hipStream_t
 
 void launch_field_op(int op, fe* r, const fe* a, const fe* b, size_t count, hipStream_t s) {
     if (count == 0) return;
-    k_field_op<<<nblk(op == 10 ? 4 * count : count), TPB, 0, s>>>(op, r, a, b, count);
+    k_field_op<<<nblk(op == 10 || op == 12 ? 4 * count : count), TPB, 0, s>>>(op, r, a, b, count);
 }
 
 

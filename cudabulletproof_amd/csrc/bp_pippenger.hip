@@ -528,7 +528,7 @@ __device__ __forceinline__ ge ge_op16(const ge& p, const ge& q) {
     }
     const fe A = fe_row_bcast<0>(r1), B = fe_row_bcast<4>(r1), CT = fe_row_bcast<8>(r1);
     fe D = fe_row_bcast<12>(r1);
-    const fe C = fe_quad_bcast<0>(fe_mul_q4(CT, k_const()));
+    const fe C = fe_quad_bcast<0>(fe_mul_q4_k(CT));
     D = fe_add(D, D);
     const fe E = fe_sub(B, A), F = fe_sub(D, C), G = fe_add(D, C), H = fe_add(B, A);
     const fe r3 = fe_mul_q4(fe_sel4(qi, E, G, F, E), fe_sel4(qi, F, H, G, H));

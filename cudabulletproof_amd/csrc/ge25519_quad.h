@@ -59,20 +59,18 @@ __device__ __forceinline__ uint32_t dpp_qperm_1133(uint32_t v) {
 __device__ __forceinline__ uint32_t dpp_qperm_2222(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xAA, 0xF, 0xF, true);   // lane l <- quad lane 2
 }
-__device__ __forceinline__ fe fe_mul_q4(const fe& x, const fe& y) {
+// this lane's two rows of x: words 2 rb, 2 rb + 1 (rb = the lane's place in its quad)
+__device__ __forceinline__ void q4_rows(const fe& x, uint32_t a[2]) {
     const int rb = threadIdx.x & 3;
     const uint64_t m0 = 0ull - (uint64_t)(rb & 1), m1 = 0ull - (uint64_t)((rb >> 1) & 1);
     const uint64_t x01 = x.v[0] ^ ((x.v[0] ^ x.v[1]) & m0), x23 = x.v[2] ^ ((x.v[2] ^ x.v[3]) & m0);
     const uint64_t xr = x01 ^ ((x01 ^ x23) & m1);
-    const uint32_t a[2] = {(uint32_t)xr, (uint32_t)(xr >> 32)};
-    uint32_t b[8], w[10], q[12], r[16];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        b[2 * i] = (uint32_t)y.v[i];
-        b[2 * i + 1] = (uint32_t)(y.v[i] >> 32);
-    }
-    mul2x8_bounded_asm(w, a, b);   // the counting form when a lane's a[0] exceeds the bound (mul512_asm.h)
-    if (__builtin_expect(__any(a[0] > MUL_BOUNDED_WORD), 0)) mul2x8_asm(w, a, b);
+    a[0] = (uint32_t)xr;
+    a[1] = (uint32_t)(xr >> 32);
+}
+// the quad's four row partials summed (two DPP levels) and folded on the quad's lane 0
+__device__ __forceinline__ fe fe_q4_sum_fold(const uint32_t w[10]) {
+    uint32_t q[12], r[16];
     // lanes 0, 2: q = own partial + the next lane's partial at +2 words (12 words)
     uint32_t n1[10];
 #pragma unroll
@@ -100,6 +98,25 @@ __device__ __forceinline__ fe fe_mul_q4(const fe& x, const fe& y) {
 #pragma unroll
     for (int i = 0; i < 8; i++) t[i] = (uint64_t)r[2 * i] | ((uint64_t)r[2 * i + 1] << 32);
     return fe_fold512(t);
+}
+__device__ __forceinline__ fe fe_mul_q4(const fe& x, const fe& y) {
+    uint32_t a[2], b[8], w[10];
+    q4_rows(x, a);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        b[2 * i] = (uint32_t)y.v[i];
+        b[2 * i + 1] = (uint32_t)(y.v[i] >> 32);
+    }
+    mul2x8_bounded_asm(w, a, b);   // the counting form when a lane's a[0] exceeds the bound (mul512_asm.h)
+    if (__builtin_expect(__any(a[0] > MUL_BOUNDED_WORD), 0)) mul2x8_asm(w, a, b);
+    return fe_q4_sum_fold(w);
+}
+// fe_mul_q4(x, k) for the curve constant k: the rows by k's SGPR words, one carry counted (mul2x8_k_asm)
+__device__ __forceinline__ fe fe_mul_q4_k(const fe& x) {
+    uint32_t a[2], w[10];
+    q4_rows(x, a);
+    mul2x8_k_asm(w, a);
+    return fe_q4_sum_fold(w);
 }
 // Stages 2 and 3 of ge25519_add from the quad's stage-1 products (lane qd holds product qd of
 // {A, B, T1 T2, Z1 Z2}); the result replicated over the quad.
@@ -183,7 +200,7 @@ __device__ __forceinline__ fe ge_quad_of_step(const fe& o, const fe& q) {
     const fe p1 = SQ ? fe_sq(o) : fe_mul(o, q);
     const fe A = fe_quad_bcast<0>(p1), CT = fe_quad_bcast<1>(p1), D0 = fe_quad_bcast<2>(p1), B = fe_quad_bcast<3>(p1);
 #if BP_QUAD_SPLITC   // C = (T1 T2) k split over the quad by rows (fe_mul_q4), then from lane 0 to all
-    const fe C = fe_quad_bcast<0>(fe_mul_q4(CT, k_const()));
+    const fe C = fe_quad_bcast<0>(fe_mul_q4_k(CT));
 #else
     const fe C = fe_mul_k(CT);
 #endif
@@ -257,7 +274,7 @@ __device__ __forceinline__ fe ge_row_of_step(const fe& o, const fe& q) {
     const int qi = (threadIdx.x >> 2) & 3;
     const fe p1 = fe_mul_q4(o, q);   // role qi's stage-1 product, on the quad's lane 0
     const fe A = fe_row_bcast<0>(p1), CT = fe_row_bcast<4>(p1), D0 = fe_row_bcast<8>(p1), B = fe_row_bcast<12>(p1);
-    const fe C = fe_quad_bcast<0>(fe_mul_q4(CT, k_const()));
+    const fe C = fe_quad_bcast<0>(fe_mul_q4_k(CT));
     const fe D = fe_add(D0, D0);
     fe E, F, G, H;
     fe_addsub(B, A, H, E);   // H = B + A, E = B - A

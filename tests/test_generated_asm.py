@@ -45,36 +45,41 @@ def test_mul_asm_bounded_forms_drop_first_carries():
     assert counts("mul2x8_asm") == (14, 16) and counts("mul2x8_bounded_asm") == (7, 16)
 
 
-def test_mul_by_k_counts_only_possible_carries():
-    """mul512_k_asm (a * k, the curve constant of every point operation) counts 16 of the 64 products'
-    carries: each column takes its products smallest k-word first and counts a product only when the
-    column's running-sum bound (carry-in bound + the products so far, every a word <= 2^32 - 1) can
-    reach 2^64.  Replayed here from the emitted asm, product by product: for the all-ones a (which
-    maximises every partial sum) and random a, no uncounted product overflows the 64-bit accumulator,
-    and the replayed columns give the exact integer product a * k."""
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("fn,rows,counted", [("mul512_k_asm", 8, 16), ("mul2x8_k_asm", 2, 1)])
+def test_mul_by_k_counts_only_possible_carries(fn, rows, counted):
+    """The products by k, the curve constant of every point operation (mul512_k_asm: a * k;
+    mul2x8_k_asm: a lane's two rows of fe_mul_q4(x, k)), count 16 of 64 and 1 of 16 carries: each
+    column takes its products smallest k-word first and counts a product only when the column's
+    running-sum bound (carry-in bound + the products so far, every a word <= 2^32 - 1) can reach 2^64.
+    Replayed here from the emitted asm, product by product: for the all-ones a (which maximises every
+    partial sum, so it covers every input) and random a, no uncounted product overflows the 64-bit
+    accumulator, and the replayed columns give the exact integer product a * k."""
     import random
     import re
     h = open(os.path.join(ROOT, "cudabulletproof_amd", "csrc", "mul512_asm.h")).read()
-    body = h[h.index("void mul512_k_asm("):]
+    body = h[h.index(f"void {fn}("):]
     body = body[:body.index("\n}\n")]
     kw = [int(x, 16) for x in re.search(r"kw\[8\] = \{([^}]*)\}", body).group(1).replace("u", "").split(",")]
     cols = []   # per column: [(i, j, counted)]
     for stmt in re.findall(r'asm volatile\("([^"]*)"', body):   # (column 0: one product onto 0, nothing counted)
         cols.append([(int(a), int(b), c != "sd" and bool(cols)) for c, a, b in
                      re.findall(r"v_mad_u64_u32 %\[acc\], %\[(\w+)\], %\[a(\d)\], %\[b(\d)\]", stmt)])
-    assert len(cols) == 15 and sum(len(c) for c in cols) == 64
-    assert sum(c for col in cols for _, _, c in col) == 16 == len(re.findall(r"v_addc_co_u32 %\[c2\]", body))
+    assert len(cols) == rows + 7 and sum(len(c) for c in cols) == 8 * rows
+    assert sum(c for col in cols for _, _, c in col) == counted == len(re.findall(r"v_addc_co_u32 %\[c2\]", body))
     K = sum(w << (32 * j) for j, w in enumerate(kw))
     rng = random.Random(5)
     for trial in range(2000):
-        a = [0xFFFFFFFF] * 8 if trial == 0 else [rng.choice([0xFFFFFFFF, rng.getrandbits(32)]) for _ in range(8)]
+        a = [0xFFFFFFFF] * rows if trial == 0 else [rng.choice([0xFFFFFFFF, rng.getrandbits(32)]) for _ in range(rows)]
         cin, words = 0, []
         for col in cols:
             acc, c2 = cin, 0
-            for i, j, counted in col:
+            for i, j, cnt in col:
                 acc += a[i] * kw[j]
                 if acc >= 2**64:
-                    assert counted, (trial, i, j)   # an uncounted product overflowed
+                    assert cnt, (trial, i, j)   # an uncounted product overflowed
                     acc -= 2**64
                     c2 += 1
             words.append(acc & 0xFFFFFFFF)

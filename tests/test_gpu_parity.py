@@ -784,11 +784,13 @@ def test_quad_product_gate(bp, oracle):
         assert np.array_equal(got[i], oracle.fe_mul(a[i], b[i])), i
 
 
-def test_mul_by_k_vs_oracle(bp, oracle):
+@pytest.mark.parametrize("op", ["mul_k", "mul_q4_k"])
+def test_mul_by_k_vs_oracle(bp, oracle, op):
     """fe_mul_k (ge25519_dev.h: every point operation's C = (T1 T2) k, the product counting only the
-    carries its column bounds allow, tools/gen_mul_asm.py k_columns) equals the oracle's
-    fe25519_mul(x, k) (curve25519_ops.cu:93-149, k = curve25519_ops.cu:341-346) for all-ones words
-    (the partial sums' maximum), words at p and random values, through field_op "mul_k"."""
+    carries its column bounds allow, tools/gen_mul_asm.py k_columns) and its lane-quad split
+    fe_mul_q4_k (the drain forms' C) equal the oracle's fe25519_mul(x, k) (curve25519_ops.cu:93-149,
+    k = curve25519_ops.cu:341-346) for all-ones words (the partial sums' maximum), words at p and
+    random values, through field_op "mul_k" / "mul_q4_k"."""
     import torch
     rng = np.random.default_rng(23)
     N = 4096
@@ -800,7 +802,7 @@ def test_mul_by_k_vs_oracle(bp, oracle):
     k = np.array([0x75EB4DCA135978A3, 0x00700A4D4141D8AB, 0x8CC740797779E898, 0x52036CEE2B6FFE73], np.uint64)
     dev = torch.device("cuda:0")
     r = torch.empty(N, 4, dtype=torch.int64, device=dev)
-    bp.field_op("mul_k", r, torch.from_numpy(x.view(np.int64)).to(dev))
+    bp.field_op(op, r, torch.from_numpy(x.view(np.int64)).to(dev))
     torch.cuda.synchronize()
     got = r.cpu().numpy().view(np.uint64)
     for i in range(N):

@@ -101,13 +101,14 @@ def k_words():
     return w
 
 
-def k_columns():
-    """[(k, prods ordered smallest word first, first, uncounted)] and the total counted carries."""
+def k_columns(rows=8):
+    """[(k, prods ordered smallest word first, first, uncounted)] and the total counted carries, for
+    the product of `rows` words of a (8: the whole product; 2: a lane's two rows of fe_mul_q4) by k."""
     kw = k_words()
     M = 2**32 - 1
     cin, cols, total = 0, [], 0
-    for k in range(15):
-        prods = sorted(((i, k - i) for i in range(8) if 0 <= k - i <= 7), key=lambda ij: kw[ij[1]])
+    for k in range(rows + 7):
+        prods = sorted(((i, k - i) for i in range(rows) if 0 <= k - i <= 7), key=lambda ij: kw[ij[1]])
         bound, counted = cin, 0
         for _, j in prods:
             if bound + M * kw[j] >= 2**64:
@@ -205,6 +206,13 @@ def main(path=OUT):
     unc = {k: u for k, _, _, u in kcols}
     emit_product(out, "mul512_k_asm", "uint32_t w[16], const uint32_t a[8]", "w",
                  [(k, prods, first) for k, prods, first, _ in kcols], 15, uncounted=lambda k: unc[k],
+                 bconst="kw", pre=(f"    constexpr uint32_t kw[8] = {{{kw}}};",))
+    kcols2, kcount2 = k_columns(2)
+    out.append(f"// A lane's two rows of fe_mul_q4(x, k): (a1 2^32 + a0) * k as 10 words, {kcount2} carries counted (the")
+    out.append(f"// bounded general rows count 7).")
+    unc2 = {k: u for k, _, _, u in kcols2}
+    emit_product(out, "mul2x8_k_asm", "uint32_t w[10], const uint32_t a[2]", "w",
+                 [(k, prods, first) for k, prods, first, _ in kcols2], 9, uncounted=lambda k: unc2[k],
                  bconst="kw", pre=(f"    constexpr uint32_t kw[8] = {{{kw}}};",))
     out.append("}  // namespace bp")
     open(path, "w").write("\n".join(out) + "\n")
