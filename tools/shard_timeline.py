@@ -1,4 +1,4 @@
-"""Timeline of the last shard run in a tools/shard_trace.sh kernel trace: every kernel of the last
+"""Timeline of the last shard run in a tools/shard_trace_bench.sh kernel trace: every kernel of the last
 run (the launches after the last gap of > 3 ms with nothing running), per queue, relative to the run's
 first launch; then the time the GPU ran nothing but latency-bound (small-grid) ticks.
 
