@@ -136,6 +136,14 @@ struct Engine {
     Buf host_dev;
     uint8_t* host_pinned = nullptr;
     size_t host_pinned_cap = 0;
+    // ... and the fixed-base prefix tables of the last generator set it saw (G | H | h, h standing
+    // in for g, which cuda_range_proof_verify does not read), kept across calls: a caller verifying
+    // batch after batch against one generator set builds them once.  Keyed by the generators' bytes
+    // (an exact compare of the host copy).  HIPBP_HOST_PREFIX_BITS: 16 by default (1.1 GB at n = 64,
+    // built in ~10 ms; fewer bits for larger n, at most 1.25 GB), 0 turns the tables off.
+    std::vector<uint8_t> host_gens_key;
+    Buf host_gens, host_tab;
+    int host_tab_bits = 0;
     // MSM / point-tree workspaces, one set per stream: the Part-2 calls run asynchronously on
     // the caller's stream, so two MSMs on two streams (or an async MSM and a Part-1 call on the
     // engine stream) must never share buffers.  [0] per-point terms, [1..2] block roots,
@@ -1582,6 +1590,32 @@ int host_shard(int dev, const RangeProof* proofs, const ge25519* V, const size_t
     BP_RET_ON(hipMemcpyAsync(dbuf + gen_off, host + gen_off, (2 * n + 1) * GE, hipMemcpyHostToDevice, st[0]));
     BP_RET_ON(e->ensure_two((int)n));   // engine stream: ordered before the pipeline's first tick
     const ge25519* dgen = (const ge25519*)(dbuf + gen_off);
+    // the generators' prefix tables: reused when this call's generator bytes equal the cached set's
+    // (then the pipelines read this call's copy and the tables built from identical bytes)
+    int hb = 16;
+    if (const char* pb = getenv("HIPBP_HOST_PREFIX_BITS")) hb = std::max(0, std::min(atoi(pb), bp::PREFIX_MAX_BITS));
+    while (hb > 0 && ((2 * n + 2) << hb) * GE > (size_t(5) << 28)) hb--;   // at most 1.25 GB of tables (K = 12 at n = 1024)
+    if (hb > 0) {
+        const uint8_t* key = host + gen_off;
+        const size_t kb = (2 * n + 1) * GE;
+        if (e->host_tab_bits != hb || e->host_gens_key.size() != kb || memcmp(e->host_gens_key.data(), key, kb) != 0) {
+            e->host_tab_bits = 0;
+            e->host_gens_key.clear();
+            BP_RET_ON(hipStreamSynchronize(st[0]));   // a previous call's tables are no longer read
+            BP_RET_ON(hipStreamSynchronize(st[1]));
+            BP_RET_ON(e->host_gens.need((2 * n + 2) * GE));
+            BP_RET_ON(e->host_tab.need(((2 * n + 2) << hb) * GE));
+            uint8_t* dg = e->host_gens.as<uint8_t>();
+            BP_RET_ON(hipMemcpyAsync(dg, dbuf + gen_off, kb, hipMemcpyDeviceToDevice, st[0]));
+            BP_RET_ON(hipMemcpyAsync(dg + kb, dbuf + gen_off + 2 * n * GE, GE, hipMemcpyDeviceToDevice, st[0]));
+            const bp::ge* gg = e->host_gens.as<bp::ge>();
+            bp::launch_prefix_tables(e->host_tab.as<bp::ge>(), gg, gg + n, gg + 2 * n, gg + 2 * n + 1, (int)n, hb,
+                                     st[0]);
+            BP_RET_ON(hipGetLastError());
+            e->host_gens_key.assign(key, key + kb);
+            e->host_tab_bits = hb;
+        }
+    }
     Pipeline* pl[2] = {nullptr, nullptr};
     int rc = HIPBP_OK;
     for (int k = 0; k < 2 && rc == HIPBP_OK; k++) {
@@ -1591,6 +1625,10 @@ int host_shard(int dev, const RangeProof* proofs, const ge25519* V, const size_t
             pl[k]->H = (const bp::ge*)(dgen + n);
             pl[k]->h = (const bp::ge*)(dgen + 2 * n);
             pl[k]->g = nullptr;
+            // (the engine's one-shot pipelines are shared with the other entry points: the tables
+            // are lent for this call only and taken back after the flush below)
+            pl[k]->ext_tab = hb > 0 ? e->host_tab.as<bp::ge>() : nullptr;
+            pl[k]->pbits = hb > 0 ? hb : 0;
         }
     }
     hipEvent_t gens_ready = nullptr;
@@ -1651,6 +1689,11 @@ int host_shard(int dev, const RangeProof* proofs, const ge25519* V, const size_t
         off += cb;
     }
     for (int k = 0; k < 2 && rc == HIPBP_OK; k++) rc = pl[k]->flush();
+    for (int k = 0; k < 2; k++)
+        if (pl[k]) {
+            pl[k]->ext_tab = nullptr;
+            pl[k]->pbits = 0;
+        }
     hipError_t s1 = hipStreamSynchronize(st[1]);
     if (rc == HIPBP_OK && s1 == hipSuccess) {
         if ((err = hipMemcpyAsync(host + ok_off, dok, B, hipMemcpyDeviceToHost, st[0])) == hipSuccess)

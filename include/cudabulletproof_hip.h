@@ -137,7 +137,10 @@ int hipbp_device_count(void);
  * current device (shard d on device (current + d) mod the device count, so num_gpus = 1 stays on
  * the current device), one host thread per device: 1024-proof chunks are packed into pinned staging, copied
  * and pushed as they are packed, alternating over two verify pipelines on two streams; one D2H of
- * the verdicts; no data-path exchange between devices.  Proofs whose a/b length or round
+ * the verdicts; no data-path exchange between devices.  Each device's engine keeps the fixed-base
+ * prefix tables of the last generator set it was called with (G | H | h, exact byte compare;
+ * HIPBP_HOST_PREFIX_BITS, default 16, at most 1.25 GB; 0: none), so calls after the first against
+ * the same generators run the table-started scalar multiplications.  Proofs whose a/b length or round
  * count differs from the first valid proof's go through the single-proof path.  Host pointers,
  * synchronous.  Returns HIPBP_OK or an error code (hipbp_last_error); on an error ok is
  * undefined.  No reference counterpart (the additive batch entry point). */

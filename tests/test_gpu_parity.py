@@ -263,6 +263,22 @@ def test_batch_verify_host_structs(bp, golden, n):
     for ng in (1, 0):
         got = bp.batch_range_proof_verify_host(proofs, V, n, d["G"], d["H"], d["g"], d["h"], num_gpus=ng)
         assert np.array_equal(got, want), (ng, np.nonzero(got != want)[0][:10])
+    # the generators' prefix tables the host path caches across calls: the same verdicts without
+    # tables (HIPBP_HOST_PREFIX_BITS=0) and at other widths, and after a call with another generator
+    # set (G and H swapped: the cache is rebuilt for it, then for the original set again)
+    def host(G, H, m, bits=None):
+        if bits is not None:
+            os.environ["HIPBP_HOST_PREFIX_BITS"] = bits
+        try:
+            return bp.batch_range_proof_verify_host(proofs[:m], V[:m], n, G, H, d["g"], d["h"])
+        finally:
+            os.environ.pop("HIPBP_HOST_PREFIX_BITS", None)
+    swapped = host(d["H"], d["G"], 40, "0")   # no tables: the plain arithmetic's verdicts for (H, G)
+    assert np.array_equal(host(d["H"], d["G"], 40), swapped)
+    for bits in ("0", "8", None):
+        got = host(d["G"], d["H"], len(proofs), bits)
+        assert np.array_equal(got, want), (bits, np.nonzero(got != want)[0][:10])
+    assert np.array_equal(host(d["H"], d["G"], 40), swapped)
     # the multi-device path (shards cut from the index list, one host thread each, verdicts merged),
     # here with every shard on this box's one GPU: 2 and 3 shards give the same verdicts
     for k in ("2", "3"):
