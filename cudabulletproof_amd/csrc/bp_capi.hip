@@ -1603,8 +1603,12 @@ int host_shard(int dev, const RangeProof* proofs, const ge25519* V, const size_t
             e->host_gens_key.clear();
             BP_RET_ON(hipStreamSynchronize(st[0]));   // a previous call's tables are no longer read
             BP_RET_ON(hipStreamSynchronize(st[1]));
-            BP_RET_ON(e->host_gens.need((2 * n + 2) * GE));
-            BP_RET_ON(e->host_tab.need(((2 * n + 2) << hb) * GE));
+            if (e->host_gens.need((2 * n + 2) * GE) != hipSuccess || e->host_tab.need(((2 * n + 2) << hb) * GE) != hipSuccess) {
+                (void)hipGetLastError();   // no room for the tables: verify without them
+                hb = 0;
+            }
+        }
+        if (hb > 0 && e->host_tab_bits == 0) {
             uint8_t* dg = e->host_gens.as<uint8_t>();
             BP_RET_ON(hipMemcpyAsync(dg, dbuf + gen_off, kb, hipMemcpyDeviceToDevice, st[0]));
             BP_RET_ON(hipMemcpyAsync(dg + kb, dbuf + gen_off + 2 * n * GE, GE, hipMemcpyDeviceToDevice, st[0]));
