@@ -8,8 +8,10 @@ TAG=${1:-r01}
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-# the headline configuration (B = 1024, n = 64, the default K, two pipelines), the driver's step count
-BENCH="python3 bench.py --steps 20 --warmup 5 --no-cpu --no-ipa --no-prove --no-shard --no-host --no-check --no-h2d --table-legs= --msm-log2 ${MSM_LOG2:-18}"
+# the headline configuration (B = 1024, n = 64, the default K, two pipelines) and the default bench's
+# own step and warm-up counts, so the trace's k_terms launches are the ones a default bench line times
+# (the other legs off; the MSM leg at ${MSM_LOG2:-20} for its kernels' counters)
+BENCH="python3 bench.py --no-cpu --no-ipa --no-prove --no-shard --no-host --no-check --no-h2d --no-repeats --table-legs= --msm-log2 ${MSM_LOG2:-20}"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- $BENCH > "$OUT/bench_trace.json" 2> "$OUT/trace.err"
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o run -- $BENCH > "$OUT/bench_fetch.json" 2> "$OUT/fetch.err"
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run -- $BENCH > "$OUT/bench_write.json" 2> "$OUT/write.err"

@@ -118,9 +118,9 @@ def main():
         kbits = "?"
     lines = [f"# rocprofv3 summary — {tag}", "",
              "Command: `tools/profile.sh " + tag + "` on one MI355X "
-             "(bench.py --steps 20 --warmup 5 --no-cpu --no-ipa --no-prove --no-shard --no-host --no-check --no-h2d "
+             "(bench.py --no-cpu --no-ipa --no-prove --no-shard --no-host --no-check --no-h2d --no-repeats --table-legs= "
              f"--msm-log2 $MSM_LOG2 under rocprofv3: the headline configuration — B = 1024, n = 64, K = {kbits} prefix "
-             "tables, two pipelines — otherwise defaults).", "",
+             "tables, two pipelines, the default 200 timed steps after 2 warm-up steps — the other legs off).", "",
              "## Kernel trace (`rocprofv3 --kernel-trace --stats`)", "",
              "| kernel | calls | avg ms | min ms | max ms | % time |", "|---|---|---|---|---|---|"]
     for r in stats:
