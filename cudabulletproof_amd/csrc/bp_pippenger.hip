@@ -446,6 +446,13 @@ __global__ __launch_bounds__(PTPB, 4) void k_pip_step(int t, const unsigned* __r
 // bits as the global steps.
 constexpr int TAIL_LAYER = 4;
 constexpr int TAIL_CHUNK = 512;
+// HIPBP_PIP_TAIL_LAYER=t (1 .. 8; A/B runs): the LDS tail from layer t instead (t = 1: nearly every
+// bucket summed in LDS by one block, the whole-bucket staging; same bits, the chunks stay aligned)
+static int pip_tail_layer() {
+    const char* e = getenv("HIPBP_PIP_TAIL_LAYER");
+    const int t = e ? atoi(e) : TAIL_LAYER;
+    return t < 1 ? 1 : t > 8 ? 8 : t;
+}
 __global__ __launch_bounds__(PTPB) void k_pip_tail(const uint32_t* __restrict__ tailq, const unsigned* __restrict__ tailn,
                                                   ge* Q, const uint32_t* __restrict__ off,
                                                   const uint32_t* __restrict__ len, ge* S) {
@@ -729,7 +736,8 @@ static hipError_t pip_buckets(PipWs& ws, const fe* scal, const ge* P, size_t n, 
     PIP_RET(ws.V.need((size_t)W * NC * sizeof(ge)));
     PIP_RET(ws.S.need(nb * sizeof(ge)));
     PIP_RET(ws.maxlen.need(3 * sizeof(unsigned)));
-    const int TT = steps > TAIL_LAYER ? TAIL_LAYER : 0;   // the LDS tail takes over at layer TT (0: none)
+    const int TL = pip_tail_layer();
+    const int TT = steps > TL ? TL : 0;   // the LDS tail takes over at layer TT (0: none)
     if (TT) PIP_RET(ws.tailq.need(nb * sizeof(uint32_t)));
     const size_t nbq = N / BID_PIECE + 1;   // bidfill queue capacity (further pieces of long lists)
     PIP_RET(ws.bq.need(nbq * sizeof(uint2)));

@@ -1056,6 +1056,27 @@ def test_msm_pippenger_key_paths_agree(bp, oracle, monkeypatch):
         assert np.array_equal(outs[0][0], oracle.msm_pippenger(s[:n], P, c)), (n, count, c)
 
 
+def test_msm_pippenger_tail_layers_agree(bp, oracle, monkeypatch):
+    """The LDS tail from another layer (HIPBP_PIP_TAIL_LAYER: 1 = nearly every bucket summed in LDS,
+    the whole-bucket staging measured in profiles/ab/r06ac; 6 = fewer buckets there) gives the
+    oracle's bits: its 512-node chunks stay aligned to the canonical bucket tree."""
+    import torch
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    for n, c in [(70000, 8), (20000, 12), (3001, 11)]:
+        rng = np.random.default_rng(n + 3 * c)
+        P = oracle.base_points(n, 41)
+        s = rand_fe(rng, n)
+        s[5::13] = s[5]   # a crowded bucket per window (a list longer than one chunk at n = 70000)
+        want = oracle.msm_pippenger(s, P, c)
+        for tl in ("1", "2", "6"):
+            monkeypatch.setenv("HIPBP_PIP_TAIL_LAYER", tl)
+            out = torch.zeros(16, dtype=torch.int64, device=dev)
+            bp.msm_pippenger(out, T(s), T(P), c)
+            torch.cuda.synchronize()
+            assert np.array_equal(out.cpu().numpy().view(np.uint64), want), (n, c, tl)
+
+
 def test_msm_pippenger_rejects_bad_window(bp):
     import torch
     dev = torch.device("cuda:0")
