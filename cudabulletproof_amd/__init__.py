@@ -109,7 +109,7 @@ EXPORTS = [
     "cuda_batch_field_invert", "cuda_soa_field_add", "cuda_range_proof_verify", "cuda_inner_product_verify",
     "cuda_benchmark_multi_scalar_mul", "cuda_benchmark_inner_product", "cuda_benchmark_field_operations",
     "cuda_benchmark_range_proof", "hipbp_last_error", "hipbp_device_count", "hipbp_batch_range_proof_verify",
-    "hipbp_batch_range_proof_verify_std", "hipbp_batch_inner_product_verify", "hipbp_batch_generate_range_proof", "hipbp_msm",
+    "hipbp_batch_range_proof_verify_std", "hipbp_batch_range_proof_verify_gens", "hipbp_batch_inner_product_verify", "hipbp_batch_generate_range_proof", "hipbp_msm",
     "hipbp_msm_pippenger", "hipbp_msm_pippenger_batch", "hipbp_msm_pippenger_windows",
     "hipbp_msm_pippenger_horner", "hipbp_msm_batch", "hipbp_msm_batch_gens", "hipbp_point_tree", "hipbp_field_op",
     "hipbp_sha_probe", "hipbp_sync", "hipbp_timing_enable",
@@ -138,7 +138,7 @@ def lib():
         for f in ("cuda_range_proof_verify", "cuda_inner_product_verify"):
             getattr(L, f).restype = ctypes.c_bool
         for f in ("hipbp_batch_range_proof_verify", "hipbp_batch_range_proof_verify_host",
-                  "hipbp_batch_range_proof_verify_std",
+                  "hipbp_batch_range_proof_verify_std", "hipbp_batch_range_proof_verify_gens",
                   "hipbp_batch_inner_product_verify", "hipbp_batch_generate_range_proof", "hipbp_msm",
                   "hipbp_msm_pippenger", "hipbp_msm_pippenger_batch", "hipbp_msm_pippenger_windows",
                   "hipbp_msm_pippenger_horner", "hipbp_msm_batch", "hipbp_msm_batch_gens", "hipbp_point_tree",
@@ -378,6 +378,15 @@ def batch_range_proof_verify(batch, G, H, g, h, ok, P_out=None, check_out=None, 
     _chk(lib().hipbp_batch_range_proof_verify(
         ctypes.byref(s), _c(G.data_ptr()), _c(H.data_ptr()), _c(g.data_ptr()), _c(h.data_ptr()), _c(ok.data_ptr()),
         _c(P_out.data_ptr()) if P_out is not None else None,
+        _c(check_out.data_ptr()) if check_out is not None else None, _stream_ptr(stream)))
+
+
+def batch_range_proof_verify_gens(batch, gens, ok, P_out=None, check_out=None, stream=None):
+    """batch_range_proof_verify with a Generators set's generators and prefix tables
+    (hipbp_batch_range_proof_verify_gens): same bits, the table-started scalar multiplications."""
+    s = batch.c_struct()
+    _chk(lib().hipbp_batch_range_proof_verify_gens(
+        ctypes.byref(s), _c(gens.h), _c(ok.data_ptr()), _c(P_out.data_ptr()) if P_out is not None else None,
         _c(check_out.data_ptr()) if check_out is not None else None, _stream_ptr(stream)))
 
 

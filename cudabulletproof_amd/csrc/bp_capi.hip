@@ -783,7 +783,8 @@ int pipeline_for(Engine& e, hipStream_t s, size_t max_batch, int n, int range_mo
 // One-shot verify of a whole batch on `s` (push + drain of a cached pipeline).
 int run_verify(Engine& e, const hipbp_proof_batch* batch, const ge25519* P_in, const ge25519* G, const ge25519* H,
                const ge25519* h, uint8_t* ok, ge25519* P_out, ge25519* chk_out, int range_mode, hipStream_t s,
-               const ge25519* g = nullptr, uint8_t* flags_out = nullptr, ge25519* poly_out = nullptr) {
+               const ge25519* g = nullptr, uint8_t* flags_out = nullptr, ge25519* poly_out = nullptr,
+               const bp::ge* tab = nullptr, int tab_bits = 0) {
     int rc = check_batch(batch, range_mode);
     if (rc != HIPBP_OK || batch->count == 0) return rc;
     if (range_mode) BP_RET_ON(e.ensure_two((int)batch->n));
@@ -793,8 +794,15 @@ int run_verify(Engine& e, const hipbp_proof_batch* batch, const ge25519* P_in, c
     pl->H = (const bp::ge*)H;
     pl->h = (const bp::ge*)h;
     pl->g = (const bp::ge*)g;
-    if ((rc = pl->push(batch, P_in, ok, P_out, chk_out, flags_out, poly_out)) != HIPBP_OK) return rc;
-    return pl->flush();
+    // a generator set's prefix tables, lent for this call only (the cached pipeline is shared with
+    // the calls that have none): the ticks' slot records take the pointer at push
+    pl->ext_tab = tab_bits ? tab : nullptr;
+    pl->pbits = tab_bits ? tab_bits : 0;
+    rc = pl->push(batch, P_in, ok, P_out, chk_out, flags_out, poly_out);
+    if (rc == HIPBP_OK) rc = pl->flush();
+    pl->ext_tab = nullptr;
+    pl->pbits = 0;
+    return rc;
 }
 
 // ---- host staging for the single-proof reference entry points
@@ -877,6 +885,23 @@ int hipbp_batch_range_proof_verify_std(const hipbp_proof_batch* batch, const ge2
     std::lock_guard<std::mutex> lk(e->mu);
     return run_verify(*e, batch, nullptr, G, H, h, ok, P_out, check_out, 2, pick(stream, *e), g, flags_out,
                       poly_out);
+}
+
+int hipbp_batch_range_proof_verify_gens(const hipbp_proof_batch* batch, void* gens, uint8_t* ok, ge25519* P_out,
+                                        ge25519* check_out, void* stream) {
+    Gens* gs = (Gens*)gens;
+    if (!gs) { g_err = "null gens"; return HIPBP_ERR_ARG; }
+    hipError_t err;
+    Engine* e = engine_or_null(&err);
+    BP_RET_ON(err);
+    if (batch && batch->count == 0) return HIPBP_OK;   // nothing read or written: empty outputs may be null
+    if (!ok) { g_err = "null output"; return HIPBP_ERR_ARG; }
+    if (batch && batch->n != gs->n) { g_err = "batch n differs from the generator set's"; return HIPBP_ERR_ARG; }
+    if (gs->device != e->device) { g_err = "gens: created on another device"; return HIPBP_ERR_ARG; }
+    std::lock_guard<std::mutex> lk(e->mu);
+    return run_verify(*e, batch, nullptr, (const ge25519*)gs->G(), (const ge25519*)gs->H(), (const ge25519*)gs->h(),
+                      ok, P_out, check_out, 1, pick(stream, *e), nullptr, nullptr, nullptr,
+                      gs->bits ? gs->tab.as<bp::ge>() : nullptr, gs->bits);
 }
 
 int hipbp_batch_inner_product_verify(const hipbp_proof_batch* batch, const ge25519* P, const ge25519* G,

@@ -204,6 +204,11 @@ void hipbp_gens_destroy(void* gens);
 /* The pipeline reads its generators and prefix tables from `gens` (same n; the pipeline must be
  * idle; the set must outlive the pipeline's use of it).  Results keep their bits. */
 int hipbp_pipeline_use_gens(void* pipeline, void* gens);
+/* hipbp_batch_range_proof_verify with the generators and prefix tables of a generator set (same n,
+ * same device): a one-shot batch that starts its generator-based scalar multiplications from the
+ * tables (the pipeline path's speed without a pipeline handle).  Same bits as the plain call. */
+int hipbp_batch_range_proof_verify_gens(const hipbp_proof_batch* batch, void* gens, uint8_t* ok, ge25519* P_out,
+                                        ge25519* check_out, void* stream);
 /* Split stage 0 for the batches pushed from now on (on = 1; range_mode 1 or 2, 4 <= n <= 64): a
  * batch's stage-0 tick runs only fold round 0 (and the range_proof_verify polynomial terms); its
  * two MSMs' terms, t*h and c*Q, which only the final assembly reads, run in chunks inside its

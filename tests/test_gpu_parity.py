@@ -1610,6 +1610,52 @@ def test_pipeline_headline_table_width_same_bits(bp, oracle, n, B, K):
                       step=7)
 
 
+@pytest.mark.parametrize("n,K", [(16, 0), (16, 12), (64, 16)])
+def test_batch_verify_gens_matches_plain(bp, golden, n, K):
+    """hipbp_batch_range_proof_verify_gens (a generator set's generators and K-bit prefix tables,
+    one-shot) gives the plain one-shot call's verdicts, P and check points: the reference proofs
+    (their verdicts, P, check points) and 300 synthetic ones; the plain call after it still runs
+    without tables (the lent tables go back); a batch of another n is refused."""
+    import torch
+    from cudabulletproof_amd import synth
+    from oracle import pyoracle
+    d = golden(f"proofs_n{n}")
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(dev)
+    gens = bp.Generators(n, T(d["G"]), T(d["H"]), T(d["g"]), T(d["h"]), prefix_bits=K)
+    try:
+        hs = [pyoracle.head_fields(h) for h in d["head"]]
+        ref = dict(V=d["V"], A=np.stack([h["A"] for h in hs]), S=np.stack([h["S"] for h in hs]),
+                   T1=np.stack([h["T1"] for h in hs]), T2=np.stack([h["T2"] for h in hs]),
+                   t=np.stack([h["t"] for h in hs]), a=d["a"], b=d["b"], c=np.stack([h["c"] for h in hs]),
+                   x=np.stack([h["x"] for h in hs]), L=d["L"], R=d["R"])
+        for arrays in (ref, synth.proofs(300, n, seed=70 + K)):
+            batch = bp.RangeProofBatch.from_numpy(n, arrays, dev)
+            outs = []
+            for use in (False, True, False):
+                ok = torch.zeros(batch.count, dtype=torch.uint8, device=dev)
+                P = torch.zeros(batch.count, 16, dtype=torch.int64, device=dev)
+                chk = torch.zeros(batch.count, 16, dtype=torch.int64, device=dev)
+                if use:
+                    bp.batch_range_proof_verify_gens(batch, gens, ok, P, chk)
+                else:
+                    bp.batch_range_proof_verify(batch, T(d["G"]), T(d["H"]), T(d["g"]), T(d["h"]), ok, P, chk)
+                torch.cuda.synchronize()
+                outs.append([x.cpu() for x in (ok, P, chk)])
+            for o in outs[1:]:
+                for a, b in zip(outs[0], o):
+                    assert torch.equal(a, b)
+            if arrays is ref:
+                assert np.array_equal(outs[1][0].numpy().astype(bool), d["ok_cuda"].astype(bool))
+                assert np.array_equal(outs[1][1].numpy().view(np.uint64), d["P"])
+                assert np.array_equal(outs[1][2].numpy().view(np.uint64), d["check"])
+        other = bp.RangeProofBatch.from_numpy(2 * n, synth.proofs(2, 2 * n, seed=1), dev)
+        with pytest.raises(bp.BulletproofError, match="differs from the generator set"):
+            bp.batch_range_proof_verify_gens(other, gens, torch.zeros(2, dtype=torch.uint8, device=dev))
+    finally:
+        gens.close()
+
+
 def test_prefix_tables_reject_busy_and_bad_bits(bp, oracle):
     import torch
     from cudabulletproof_amd import synth
