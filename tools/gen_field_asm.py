@@ -9,15 +9,20 @@ stay in SGPRs, are combined by SALU (its own issue port) and enter the arithmeti
 of v_addc.  Every operand is a 32-bit VGPR: the C side passes limb halves (free sub-registers),
 so no register pair has to be formed.
 
-Hazard rule these sequences meet (gfx940/gfx950): an SGPR written by a VALU instruction
-(carry-out, v_cmp) and read by a VALU instruction (carry-in, mask) needs 2 wait states in
-between; SALU-written masks can be read at once.  `schedule` inserts the s_nop.  Outputs are
-VGPRs only, inputs are VGPRs or constants, so nothing crosses the asm boundary in an SGPR.
+Hazard rule these sequences meet (gfx950): an SGPR written by a VALU instruction (carry-out,
+v_cmp) and read by a VALU instruction as a mask or source operand (v_cndmask) needs 2 wait states
+in between, read as a carry-in (v_addc / v_subb) 1 wait state, the spacing the compiler itself
+gives the same e64 carry chains (tools/hazard_probe.hip read no stale carry even at 0 on MI355X);
+SALU-written masks can be read at once.  `schedule` inserts the s_nop.  Outputs are VGPRs only,
+inputs are VGPRs or constants, so nothing crosses the asm boundary in an SGPR.
 """
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 OUT = os.path.join(HERE, "..", "cudabulletproof_amd", "csrc", "field_asm.h")
+WAIT_MASK = 2    # VALU-written SGPR read as a mask / source operand
+WAIT_CARRY = 1   # ... read as the carry-in of v_addc / v_subb
+CARRY_READERS = ("v_addc_co_u32", "v_subb_co_u32", "v_subbrev_co_u32")
 
 
 def schedule(ins, state=None):
@@ -30,9 +35,10 @@ def schedule(ins, state=None):
     for text, writes, reads, is_valu in ins:
         if is_valu:
             need = 0
+            wait = WAIT_CARRY if text.split()[0] in CARRY_READERS else WAIT_MASK
             for r in reads:
                 if r in wpos:
-                    need = max(need, 2 - (pos - wpos[r] - 1))
+                    need = max(need, wait - (pos - wpos[r] - 1))
             if need > 0:
                 lines.append(f"s_nop {need - 1}")
                 pos += need

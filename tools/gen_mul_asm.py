@@ -3,14 +3,15 @@ product-scanning columns of gfx950 `v_mad_u64_u32` (64-bit accumulate, carry-out
 lane mask) + `v_addc_co_u32` (carry count), one asm statement per column.
 
 Hazard rule applied inside each statement: a VALU write of an SGPR lane mask is read by a
-VALU carry-in no sooner than 2 wait states later (intervening VALU instructions count 1 each,
-`s_nop N` counts N+1).
+VALU carry-in no sooner than 1 wait state later (intervening VALU instructions count 1 each,
+`s_nop N` counts N+1): the spacing the compiler gives its own e64 carry chains on gfx950
+(tools/hazard_probe.hip read no stale carry even at 0 on MI355X; rounds 1-6 used 2).
 """
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 OUT = os.path.join(HERE, "..", "cudabulletproof_amd", "csrc", "mul512_asm.h")
-WAIT = 2
+WAIT = 1
 
 
 def column(k, square=False):
