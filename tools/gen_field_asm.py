@@ -20,6 +20,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 OUT = os.path.join(HERE, "..", "cudabulletproof_amd", "csrc", "field_asm.h")
+GUARD = []       # no trailing wait states: see emit()
 WAIT_MASK = 2    # VALU-written SGPR read as a mask / source operand
 WAIT_CARRY = 1   # ... read as the carry-in of v_addc / v_subb
 CARRY_READERS = ("v_addc_co_u32", "v_subb_co_u32", "v_subbrev_co_u32")
@@ -146,10 +147,12 @@ def branch_if_rare(label):
 def emit(name, doc, args, ins, outs, vtemps, sgprs, lines, inout=False):
     """args: [(param, prefix)] array params bound to scalars prefix0..7.  lines: scheduled asm.
     inout: the outputs are read-write, initialised from the first array argument."""
-    # the block's last VALU instructions write SGPRs (carry-outs) that the compiler may reuse at once
-    # for a VMEM address: a VALU SGPR write followed by a VMEM read of it needs 5 wait states
-    # (gfx940/gfx950), and the compiler does not see inside the block
-    text = "\\n\\t".join(lines + ["s_nop 4"])
+    # No trailing wait states (rounds 2-6 ended every block with s_nop 4 against "a VALU SGPR write
+    # followed by a VMEM read of it needs 5").  The block's SGPR outputs are early-clobber temporaries
+    # that nothing reads after it, so any later read of those registers follows a new write of them
+    # (the compiler's own, which it pads itself); tools/asm_exit_check.py scans every compiled kernel
+    # for a memory instruction reading an SGPR the block wrote within 5 states (none).
+    text = "\\n\\t".join(lines + GUARD)
     out = [f"// {d}" for d in doc]
     out.append(f"__device__ __forceinline__ void {name}(uint32_t out[8], " +
                ", ".join(f"const uint32_t {p}[8]" for p, _ in args) + ") {")
@@ -400,7 +403,7 @@ def gen_addsub():
     t = [f"t{i}" for i in range(8)]
     sgprs = FIX_SGPRS + ["scy", "sby", "sr1", "sr2", "srare", "sq1", "sq2", "sq3"]
     ins = [f"a{i}" for i in range(8)] + [f"b{i}" for i in range(8)]
-    text = "\\n\\t".join(lines + ["s_nop 4"])
+    text = "\\n\\t".join(lines + GUARD)
     out = ["// fe_add(a, b) and fe_sub(a, b) in one block (curve25519_ops.cu:41-90): the two carry chains",
            "// interleaved, one rare-edge branch for both (tools/gen_field_asm.py gen_addsub).",
            "__device__ __forceinline__ void fe_addsub_asm(uint32_t os[8], uint32_t od[8], const uint32_t fa[8], "
