@@ -69,8 +69,17 @@ __device__ __forceinline__ void q4_rows(const fe& x, uint32_t a[2]) {
     a[1] = (uint32_t)(xr >> 32);
 }
 // the quad's four row partials summed (two DPP levels) and folded on the quad's lane 0
+// (BP_Q4_SUM_ASM: the two levels as one list-scheduled asm block, field_asm.h q4_sum_asm: both carry
+// chains and the DPP moves interleaved, where the compiled form below waits one state per link)
+#ifndef BP_Q4_SUM_ASM
+#define BP_Q4_SUM_ASM 1
+#endif
 __device__ __forceinline__ fe fe_q4_sum_fold(const uint32_t w[10]) {
-    uint32_t q[12], r[16];
+    uint32_t r[16];
+#if BP_Q4_SUM_ASM && defined(__HIP_DEVICE_COMPILE__)
+    q4_sum_asm(r, w);
+#else
+    uint32_t q[12];
     // lanes 0, 2: q = own partial + the next lane's partial at +2 words (12 words)
     uint32_t n1[10];
 #pragma unroll
@@ -94,6 +103,7 @@ __device__ __forceinline__ fe fe_q4_sum_fold(const uint32_t w[10]) {
 #pragma unroll
     for (int i = 12; i < 15; i++) r[i] = __builtin_addc(n2[i - 4], 0u, c, &c);
     r[15] = n2[11] + c;
+#endif
     uint64_t t[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) t[i] = (uint64_t)r[2 * i] | ((uint64_t)r[2 * i + 1] << 32);

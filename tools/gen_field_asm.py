@@ -436,11 +436,80 @@ def gen_canon():
                 [("ha", "h")], [], h, ["vt1", "vt2", "vt3"], FIX_SGPRS + ["srare"], lines, inout=True)
 
 
+def gen_q4_sum():
+    """The lane quad's two DPP levels of fe_q4_sum_fold (ge25519_quad.h) as one scheduled block:
+    level 1 (quad_perm [1,1,3,3]) q = w + (lane|1's w) << 64 bits on lanes 0 and 2, level 2 (quad_perm
+    [2,2,2,2]) r = q + (lane 2's q) << 128 bits on lane 0 -- the exact 512-bit sum of the four 320-bit
+    partials.  The two carry chains (SGPR pairs sa, sb) and the 22 DPP moves are list-scheduled
+    together so each link finds its carry 1 wait state after the write and each DPP its source 2
+    after (the compiler left one wait per link of both chains: 57 of a row step's wait states)."""
+    ins = []   # (name, text, deps [(name, min distance in slots)], writes)
+    for k in range(10):
+        ins.append((f"d1_{k}", f"v_mov_b32_dpp %[n{k}], %[w{k}] quad_perm:[1,1,3,3] row_mask:0xf bank_mask:0xf "
+                    "bound_ctrl:1", []))
+    qsrc = lambda j: None if j < 2 else f"l1_{j}"
+    for i in range(2, 12):
+        a = f"%[w{i}]" if i < 10 else "0"
+        b = f"%[n{i - 2}]"
+        deps = [(f"d1_{i - 2}", 1)] + ([(f"l1_{i - 1}", 2)] if i > 2 else [])
+        if i == 2:
+            ins.append((f"l1_{i}", f"v_add_co_u32 %[q{i}], %[sa], {a}, {b}", deps))
+        else:
+            ins.append((f"l1_{i}", f"v_addc_co_u32 %[q{i}], %[sa], {a}, {b}, %[sa]", deps))
+    for j in range(12):
+        src = f"%[w{j}]" if j < 2 else f"%[q{j}]"
+        deps = [] if j < 2 else [(f"l1_{j}", 3)]   # a VALU-written VGPR read by DPP: 2 wait states
+        ins.append((f"d2_{j}", f"v_mov_b32_dpp %[m{j}], {src} quad_perm:[2,2,2,2] row_mask:0xf bank_mask:0xf "
+                    "bound_ctrl:1", deps))
+    for i in range(4, 16):
+        a = f"%[q{i}]" if i < 12 else "0"
+        deps = [(f"d2_{i - 4}", 1)] + ([(f"l1_{i}", 1)] if i < 12 else []) + ([(f"l2_{i - 1}", 2)] if i > 4 else [])
+        if i == 4:
+            ins.append((f"l2_{i}", f"v_add_co_u32 %[r{i}], %[sb], {a}, %[m{i - 4}]", deps))
+        else:
+            ins.append((f"l2_{i}", f"v_addc_co_u32 %[r{i}], %[sb], {a}, %[m{i - 4}], %[sb]", deps))
+    # list scheduling: each slot takes the first ready instruction, chains first (longest remaining
+    # path), else a wait state
+    prio = {n: (0 if n.startswith("l2") else 1 if n.startswith("l1") else 2 if n.startswith("d2") else 3)
+            for n, _, _ in ins}
+    pos, lines, t = {}, ["s_nop 1"], 0   # the w words may have been written just before the block
+    left = list(ins)
+    while left:
+        ready = [x for x in left if all(d in pos and t >= pos[d] + dist for d, dist in x[2])]
+        if not ready:
+            lines.append("s_nop 0")
+            t += 1
+            continue
+        x = min(ready, key=lambda x: (prio[x[0]], left.index(x)))
+        lines.append(x[1])
+        pos[x[0]] = t
+        left.remove(x)
+        t += 1
+    outs = [f"q{i}" for i in range(2, 12)] + [f"r{i}" for i in range(4, 16)] + [f"n{k}" for k in range(10)] + \
+           [f"m{j}" for j in range(12)]
+    text = "\\n\\t".join(lines)
+    out = ["// fe_q4_sum_fold's two DPP levels (ge25519_quad.h) in one list-scheduled block: r[0..15] (valid on",
+           f"// the quad's lane 0) = the sum of the quad's four partials w[0..9] at word offsets 0, 2, 4, 6 ({t} slots).",
+           "__device__ __forceinline__ void q4_sum_asm(uint32_t r[16], const uint32_t w[10]) {",
+           "    const uint32_t " + ", ".join(f"w{k} = w[{k}]" for k in range(10)) + ";",
+           "    uint32_t " + ", ".join(outs) + ";",
+           "    uint64_t sa, sb;",
+           f'    asm volatile("{text}"',
+           "                 : " + ", ".join([f'[{x}] "=&v"({x})' for x in outs] + ['[sa] "=&s"(sa)', '[sb] "=&s"(sb)']),
+           "                 : " + ", ".join(f'[w{k}] "v"(w{k})' for k in range(10)) + ");",
+           "    r[0] = w0; r[1] = w1; r[2] = q2; r[3] = q3;",
+           "    " + " ".join(f"r[{i}] = r{i};" for i in range(4, 16)),
+           "    (void)sa; (void)sb; " + " ".join(f"(void){x};" for x in [f"q{i}" for i in range(12, 12)]),
+           "}"]
+    return out
+
+
 def main(path=OUT):
     out = ["// GENERATED by tools/gen_field_asm.py -- do not edit by hand.",
            "// gfx950 inline-asm fe25519 add and product fold: the same bits as the C forms in fe25519_dev.h.",
            "#pragma once", "#include <stdint.h>", "namespace bp {"]
-    out += gen_add() + [""] + gen_sub() + [""] + gen_fold() + [""] + gen_canon() + [""] + gen_addsub()
+    out += gen_add() + [""] + gen_sub() + [""] + gen_fold() + [""] + gen_canon() + [""] + gen_addsub() + [""] + \
+        gen_q4_sum()
     out.append("}  // namespace bp")
     open(path, "w").write("\n".join(out) + "\n")
     print("wrote", path)
