@@ -161,6 +161,11 @@ struct Engine {
         Buf b[19];
     };
     std::map<hipStream_t, ProverBufs*> provers;
+    // the generators (G | H | h) a single-proof call last uploaded to h2d[4], as host bytes: the next
+    // call with the same bytes (the reference's caller passes one generator set call after call)
+    // skips their three pageable copies
+    std::vector<uint8_t> single_gens;
+    const void* single_gens_dev = nullptr;
     // pinned host staging for the single-proof entry points (a pageable source of an
     // async copy must outlive the copy; this one does, and the stream is synced after use)
     uint8_t* pinned = nullptr;
@@ -1523,11 +1528,25 @@ static bool verify_single(const InnerProductProof* ip, const RangeProof* rp, con
     if (!stage_single(e, ip, rp, V, &b)) return false;
     b.n = n;
     // generators + h + P
+    const size_t cap0 = e.h2d[4].cap;
     BP_EXIT_ON(e.h2d[4].need(2 * n * sizeof(ge25519) + 3 * sizeof(ge25519)));
+    if (e.h2d[4].cap != cap0) e.single_gens.clear();   // a new buffer (maybe at the old address) holds nothing
     ge25519* dg = e.h2d[4].as<ge25519>();
-    BP_EXIT_ON(hipMemcpyAsync(dg, G->elements, n * sizeof(ge25519), hipMemcpyHostToDevice, e.stream));
-    BP_EXIT_ON(hipMemcpyAsync(dg + n, H->elements, n * sizeof(ge25519), hipMemcpyHostToDevice, e.stream));
-    BP_EXIT_ON(hipMemcpyAsync(dg + 2 * n, h, sizeof(ge25519), hipMemcpyHostToDevice, e.stream));
+    const size_t GB = n * sizeof(ge25519);
+    std::vector<uint8_t>& sg = e.single_gens;
+    const bool same = e.single_gens_dev == (const void*)dg && sg.size() == 2 * GB + sizeof(ge25519) &&
+                      memcmp(sg.data(), G->elements, GB) == 0 && memcmp(sg.data() + GB, H->elements, GB) == 0 &&
+                      memcmp(sg.data() + 2 * GB, h, sizeof(ge25519)) == 0;
+    if (!same) {   // (every earlier user of dg has finished: each call ends with a stream sync)
+        BP_EXIT_ON(hipMemcpyAsync(dg, G->elements, GB, hipMemcpyHostToDevice, e.stream));
+        BP_EXIT_ON(hipMemcpyAsync(dg + n, H->elements, GB, hipMemcpyHostToDevice, e.stream));
+        BP_EXIT_ON(hipMemcpyAsync(dg + 2 * n, h, sizeof(ge25519), hipMemcpyHostToDevice, e.stream));
+        sg.resize(2 * GB + sizeof(ge25519));
+        memcpy(sg.data(), G->elements, GB);
+        memcpy(sg.data() + GB, H->elements, GB);
+        memcpy(sg.data() + 2 * GB, h, sizeof(ge25519));
+        e.single_gens_dev = dg;
+    }
     if (P) BP_EXIT_ON(hipMemcpyAsync(dg + 2 * n + 1, P, sizeof(ge25519), hipMemcpyHostToDevice, e.stream));
     BP_EXIT_ON(e.h2d[5].need(64));
     int rc = run_verify(e, &b, P ? dg + 2 * n + 1 : nullptr, dg, dg + n, dg + 2 * n, e.h2d[5].as<uint8_t>(), nullptr,

@@ -190,6 +190,28 @@ def test_single_verify_matches_reference(bp, golden, n):
         assert ok2 == bool(d["ok_cuda"][i]), i
 
 
+def test_single_verify_generator_reuse(bp, golden):
+    """The single-proof calls keep the last generator set they uploaded and skip the copies when the
+    next call brings the same bytes: alternating generator sets (G and H swapped), sizes (n = 16 / 64:
+    the staging buffer grows) and the two entry points, every verdict equals the batch API's for the
+    same proof and generators (which never reuses them)."""
+    sets = {n: golden(f"proofs_n{n}") for n in (16, 64)}
+    want = {}
+    for n, d in sets.items():
+        arrays = _batch_from_golden(bp, d, None)
+        want[n, False] = _run_batch(bp, n, arrays, d["G"], d["H"], d["g"], d["h"])[0]
+        want[n, True] = _run_batch(bp, n, arrays, d["H"], d["G"], d["g"], d["h"])[0]
+    for rep in range(2):
+        for n in (16, 64, 16):
+            d = sets[n]
+            for swap in (False, True, True, False):
+                G, H = (d["H"], d["G"]) if swap else (d["G"], d["H"])
+                for i in range(min(3, len(d["head"]))):
+                    ok = bp.cuda_range_proof_verify(_proof(d, i), d["V"][i], n, G, H, d["g"], d["h"])
+                    assert ok == bool(want[n, swap][i]), (rep, n, swap, i)
+                    bp.cuda_inner_product_verify(_proof(d, i), d["P"][i], G, H, d["h"])
+
+
 def _batch_from_golden(bp, d, device):
     from oracle.pyoracle import head_fields
     hs = [head_fields(h) for h in d["head"]]
