@@ -25,10 +25,15 @@ def ops(line):
 VALU_SDST2 = ('v_add_co_u32', 'v_addc_co_u32', 'v_sub_co_u32', 'v_subb_co_u32', 'v_subrev_co_u32', 'v_subbrev_co_u32',
               'v_mad_u64_u32', 'v_mad_i64_i32', 'v_div_scale')
 flags = 0; blocks = 0
-for src in SRC:
+def compile_one(src):
     out = os.path.join(tmp, os.path.basename(src) + '.s')
     subprocess.run(['hipcc', '--offload-arch=gfx950', '-O3', '-std=c++17', '-S', '--cuda-device-only', src, '-o', out],
                    check=True, stderr=subprocess.DEVNULL)
+    return out
+from concurrent.futures import ThreadPoolExecutor
+with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as pool:
+    outs = list(pool.map(compile_one, SRC))
+for src, out in zip(SRC, outs):
     lines = [l.strip() for l in open(out)]
     i = 0
     while i < len(lines):
