@@ -3,6 +3,7 @@ csrc/mul512_asm.h, tools/gen_field_asm.py -> csrc/field_asm.h), so a reviewer ca
 generator (with its hazard scheduling and the rare-edge tests) instead of the asm."""
 import importlib.util
 import os
+import re
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -88,3 +89,64 @@ def test_mul_by_k_counts_only_possible_carries(fn, rows, counted):
         assert cin >> 32 == 0
         A = sum(w << (32 * i) for i, w in enumerate(a))
         assert sum(w << (32 * k) for k, w in enumerate(words)) == A * K
+
+
+def _asm_statements(path):
+    """Every inline-asm text of a generated header, split into instruction lines."""
+    s = open(path).read()
+    out = []
+    for m in re.finditer(r'asm volatile\("((?:[^"\\]|\\.)*)"', s):
+        out.append([t.strip() for t in m.group(1).replace("\\n", "\n").replace("\\t", "").split("\n") if t.strip()])
+    return out
+
+
+def _operands(line):
+    op, _, rest = line.partition(" ")
+    return op, [x.strip() for x in rest.split(",")] if rest else []
+
+
+def test_generated_asm_hazard_spacing():
+    """Inside every generated asm statement (mul512_asm.h, field_asm.h), on each straight-line
+    segment: an SGPR a VALU instruction writes is read as a carry-in no sooner than 1 wait state
+    later and as a mask (v_cndmask) no sooner than 2; a VGPR a VALU instruction writes is read by a
+    DPP move no sooner than 2 (intervening instructions count 1 each, s_nop N counts N + 1).  A label
+    starts a new segment (its state comes from several predecessors: the generator's scheduler merges
+    them; here only reads of registers written in the same segment are checked)."""
+    import os
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "cudabulletproof_amd", "csrc")
+    carry_ops = ("v_addc_co_u32", "v_subb_co_u32", "v_subbrev_co_u32")
+    checked = 0
+    for hdr in ("mul512_asm.h", "field_asm.h"):
+        for lines in _asm_statements(os.path.join(root, hdr)):
+            sgpr_w, vgpr_w, pos = {}, {}, 0
+            for line in lines:
+                if line.endswith(":"):   # a label: a new segment
+                    sgpr_w, vgpr_w = {}, {}
+                    continue
+                op, ops = _operands(line)
+                if op == "s_nop":
+                    pos += int(ops[0]) + 1
+                    continue
+                if op.startswith("v_"):
+                    reads = ops[1:]
+                    if op.startswith("v_mov_b32_dpp"):
+                        src = reads[0].split()[0]
+                        if src in vgpr_w:
+                            assert pos - vgpr_w[src] - 1 >= 2, (hdr, line)
+                            checked += 1
+                    if op in carry_ops and reads and reads[-1] in sgpr_w:
+                        assert pos - sgpr_w[reads[-1]] - 1 >= 1, (hdr, line)
+                        checked += 1
+                    if op.startswith("v_cndmask") and reads and reads[-1] in sgpr_w:
+                        assert pos - sgpr_w[reads[-1]] - 1 >= 2, (hdr, line)
+                        checked += 1
+                    if op in ("v_add_co_u32", "v_sub_co_u32", "v_mad_u64_u32") + carry_ops or op.startswith("v_cmp"):
+                        sdst = ops[1] if not op.startswith("v_cmp") else ops[0]
+                        sgpr_w[sdst] = pos
+                    vgpr_w[ops[0]] = pos
+                elif op.startswith("s_") and ops:
+                    sgpr_w.pop(ops[0], None)   # a SALU write: readable at once
+                if op.startswith(("s_branch", "s_cbranch")):
+                    sgpr_w, vgpr_w = {}, {}
+                pos += 1
+    assert checked > 250, checked   # (315 reads checked at round 6)
