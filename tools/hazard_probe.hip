@@ -1,11 +1,11 @@
 // hazard_probe.hip — is a VALU carry-out SGPR read back correctly by the next VALU carry-in at
-// 0, 1 or 2 wait states?  (tools/gen_mul_asm.py / gen_field_asm.py space every such read 2 wait
-// states after its write; the compiler itself pads some e64 carry chains with 1.)  Each sequence
+// 0, 1 or 2 wait states?  (tools/gen_mul_asm.py / gen_field_asm.py space a carry-in read 1 wait
+// state after its write, as the compiler pads its own e64 carry chains, and a mask / source read 2.)  Each sequence
 // first zeroes the SGPR pair with SALU, then a VALU instruction writes carry = 1 into it in every
 // lane, then after K wait states a v_addc_co_u32 reads it as its carry-in: 1 if it saw the VALU
 // write, 0 if it read the stale SALU zero.  One wave alone (the tightest timing) and 4096 waves;
 // prints the lanes x repetitions that read a stale carry, per form and K.  A probe, not a proof:
-// the generators keep 2 wait states.
+// the generators never go below the compiler's own spacing.
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdio>
