@@ -9,7 +9,7 @@ cp $LIB gpurun_out/ab_first/lib_orig.so
 for i in 1 2 3 4; do
   for v in old new; do
     cp ab/lib_$v.so $LIB
-    r=$(timeout -k 10 60 ./build/dropin_latency gpurun_out/ab_first/proof${N:-16}.bin 5)
+    r=$(timeout -k 10 60 ./build/dropin_latency gpurun_out/ab_first/proof${N:-16}.bin ${WARM:-5})
     echo "{\"v\": \"$v\", \"n\": ${N:-16}, \"r\": $r}" >> gpurun_out/ab_first/runs.jsonl
   done
 done

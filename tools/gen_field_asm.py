@@ -190,26 +190,75 @@ def two_way(pre, fast, slow):
     return lp + lf + ["s_branch 4f", "3:"] + ls + ["4:"]
 
 
+def emit_split(name, doc, args, outs, vtemps, fast_sgprs, fast, slow_sgprs, slow):
+    """The fast form and the exact form as two asm statements: the fast one computes the common result
+    and the wave-uniform rare-edge mask srare; the exact one (from the inputs again) runs under a C
+    branch the compiler places out of line.  Measured on one wave (tools/ubench_dep.hip,
+    profiles/ubench/ubench_dep_r06.json): a compare read by the SALU test right after it stalls the
+    wave ~20 cycles and the taken s_branch over an inline exact form costs ~22; srare is written
+    early in the fast statement, so the test after it finds it ready, and the common path falls
+    through (a not-taken branch, ~8 cycles)."""
+    ins = [f"{pre}{i}" for _, pre in args for i in range(8)]
+    outs_c = [f'[{x}] "=&v"({x})' for x in outs + vtemps]
+    ins_c = ", ".join([f'[{x}] "v"({x})' for x in ins] + ['[c80] "v"(0x80000000u)', '[p0l] "s"(0xFFFFFFEDu)'])
+    out = [f"// {d}" for d in doc]
+    out.append(f"__device__ __forceinline__ void {name}(" + ", ".join(f"uint32_t o{k}[8]" for k in range(len(outs) // 8)) +
+               ", " + ", ".join(f"const uint32_t {p}[8]" for p, _ in args) + ") {")
+    for p, pre in args:
+        out.append("    const uint32_t " + ", ".join(f"{pre}{i} = {p}[{i}]" for i in range(8)) + ";")
+    out.append("    uint32_t " + ", ".join(outs + vtemps) + ";")
+    out.append("    uint64_t " + ", ".join(fast_sgprs) + ";")
+    out.append('    asm volatile("{0}"'.format("\\n\\t".join(fast)))
+    out.append("                 : " + ", ".join(outs_c + [f'[{x}] "=&s"({x})' for x in fast_sgprs]))
+    out.append("                 : " + ins_c)
+    out.append('                 : "scc");')
+    out.append("    if (__builtin_expect(srare != 0, 0)) {   // some lane is on a rare edge: the exact form")
+    out.append("        uint64_t " + ", ".join(slow_sgprs) + ";")
+    out.append('        asm volatile("{0}"'.format("\\n\\t".join(slow)))
+    out.append("                     : " + ", ".join(outs_c + [f'[{x}] "=&s"({x})' for x in slow_sgprs]))
+    out.append("                     : " + ins_c)
+    out.append('                     : "scc");')
+    out.append("        (void)" + "; (void)".join(slow_sgprs) + ";")
+    out.append("    }")
+    for k in range(len(outs) // 8):
+        out.append("    " + " ".join(f"o{k}[{i}] = {outs[8 * k + i]};" for i in range(8)))
+    out.append("    (void)" + "; (void)".join(fast_sgprs + vtemps) + ";")
+    out.append("}")
+    return out
+
+
+def add_chain(h, a="a", b="b", cy="scy", upto=8, start=0):
+    out = []
+    for i in range(start, upto):
+        if i == 0:
+            out.append(V(f"v_add_co_u32 %[{h[0]}], %[{cy}], %[{a}0], %[{b}0]", [cy]))
+        else:
+            out.append(V(f"v_addc_co_u32 %[{h[i]}], %[{cy}], %[{a}{i}], %[{b}{i}], %[{cy}]", [cy], [cy]))
+    return out
+
+
 def gen_add():
+    """Fast statement: the add chain with fix_test's compare placed as soon as h1 and h4 exist, then
+    m = carry | top and the fast fix-up.  Exact statement: the chain again and fix_seq."""
     h = [f"h{i}" for i in range(8)]
-    chain = [V("v_add_co_u32 %[h0], %[scy], %[a0], %[b0]", ["scy"])]
-    for i in range(1, 8):
-        chain.append(V(f"v_addc_co_u32 %[h{i}], %[scy], %[a{i}], %[b{i}], %[scy]", ["scy"], ["scy"]))
-    lines = two_way(chain + fix_test(h, "scy"), fix_fast(h), fix_seq(h, h, "scy"))
-    return emit("fe_add_asm", ["fe25519_add (curve25519_ops.cu:41-68) on limb halves: exact 257-bit sum, then",
-                               "one lossy \"- p\" when it carried out or is >= p (fast form unless a lane is",
-                               "on one of the fix-up's rare edges: fix_test)."],
-                [("fa", "a"), ("ga", "b")], [f"a{i}" for i in range(8)] + [f"b{i}" for i in range(8)],
-                h, ["vt1", "vt2", "vt3"], FIX_SGPRS + ["scy", "srare"], lines)
+    fast = add_chain(h, upto=5) + [V("v_max_u32 %[vt3], %[h1], %[h4]"),
+                                    V("v_cmp_eq_u32 %[srare], -1, %[vt3]", ["srare"])] + \
+        add_chain(h, start=5) + [V("v_cmp_gt_i32 %[stp], 0, %[h7]", ["stp"]),
+                                 S("s_or_b64 %[sm], %[scy], %[stp]", ["sm"])] + fix_fast(h)
+    lf, _ = schedule(fast)
+    ls, _ = schedule(add_chain(h) + fix_seq(h, h, "scy"))
+    return emit_split("fe_add_asm", ["fe25519_add (curve25519_ops.cu:41-68) on limb halves: exact 257-bit sum, then",
+                                     "one lossy \"- p\" when it carried out or is >= p (fast form unless a lane is",
+                                     "on one of the fix-up's rare edges: fix_test)."],
+                      [("fa", "a"), ("ga", "b")], h, ["vt1", "vt2", "vt3"],
+                      ["scy", "srare", "stp", "sm", "sk0", "sk2"], lf, FIX_SGPRS + ["scy"], ls)
 
 
 def gen_fold():
-    """One wave-uniform branch after the plain carry chain: if some x_i (i = 1..3) may be 2^64-1
-    (its low word is: the lossy carry can differ from the true one) or fix_test's edge words are
-    all ones, the exact chain (from the inputs again) + exact fix-up; else the fast fix-up."""
+    """One wave-uniform rare-edge test: if some x_i (i = 1..3) may be 2^64-1 (its low word is: the
+    lossy carry can differ from the true one) or fix_test's edge words are all ones, the exact chain
+    (from the inputs again) + exact fix-up; else the plain chain + the fast fix-up."""
     h = [f"h{i}" for i in range(8)]
-    test1 = [V("v_max3_u32 %[vt3], %[x2], %[x4], %[x6]"),
-             V("v_cmp_eq_u32 %[srare], -1, %[vt3]", ["srare"])]
     plain = [V("v_add_co_u32 %[h0], %[scy], %[a0], %[x0]", ["scy"])]
     for i in range(1, 8):
         plain.append(V(f"v_addc_co_u32 %[h{i}], %[scy], %[a{i}], %[x{i}], %[scy]", ["scy"], ["scy"]))
@@ -225,26 +274,22 @@ def gen_fold():
                        ["sk1"], ["sk0"]))
         exact.append(S(f"s_and_b64 %[sq{i}], %[sq{i}], %[scy]", [f"sq{i}"]))   # x_i == M & carry-in
         exact.append(S(f"s_andn2_b64 %[scy], %[sk1], %[sq{i}]", ["scy"]))      # the reference's carry
-    # one wave-uniform test for both rare edges: the plain chain runs first; max3 of the x words the
-    # lossy-carry test reads and of the words fix_test reads, then one compare.  Layout: plain chain,
-    # tests, branch -> 3; fast fix, s_branch 4; 3: exact chain (recomputed from the inputs) + exact
-    # fix; 4: end
-    both = [V("v_max3_u32 %[vt3], %[x2], %[x4], %[x6]"),
-            V(f"v_max3_u32 %[vt3], %[vt3], %[{h[1]}], %[{h[4]}]"),
-            V(f"v_cmp_gt_i32 %[stp], 0, %[{h[7]}]", ["stp"]),
-            V("v_cmp_eq_u32 %[srare], -1, %[vt3]", ["srare"]),
-            S(f"s_or_b64 %[sm], {cref('scy')}, %[stp]", ["sm"])]
-    l2, s2 = schedule(plain + both + branch_if_rare("3f"))
-    l3, _ = schedule(fix_fast(h), s2)
-    l5, s5 = schedule(exact, s2)
-    l6, _ = schedule(fix_seq(h, h, "scy"), s5)
-    lines = l2 + l3 + ["s_branch 4f", "3:"] + l5 + l6 + ["4:"]
-    return emit("fe_fold_asm", ["Fold of the exact 512-bit product (curve25519_ops.cu:114-145): t_lo as halves",
-                                "ta[0..7], x_i = lo64(19 t_{i+4}) as halves xa[0..7]; carry chain with the lossy",
-                                "carry cy_i = c_i & !(x_i == 2^64-1 & cy_{i-1}), then the fix-up.  The plain",
-                                "chain and the fast fix-up unless a lane is on a rare edge (wave-uniform tests)."],
-                [("ta", "a"), ("xa", "x")], [f"a{i}" for i in range(8)] + [f"x{i}" for i in range(8)],
-                h, ["vt1", "vt2", "vt3"], FIX_SGPRS + ["scy", "sq1", "sq2", "sq3", "srare"], lines)
+    # fast statement: the x words' max first, the chain, the h words' max and the one compare as soon
+    # as h1 and h4 exist, the rest of the chain, m = carry | top, the fast fix-up.  Exact statement:
+    # the exact chain from the inputs again and the exact fix-up.
+    fast = [V("v_max3_u32 %[vt3], %[x2], %[x4], %[x6]")] + plain[:5] + \
+        [V(f"v_max3_u32 %[vt3], %[vt3], %[{h[1]}], %[{h[4]}]"),
+         V("v_cmp_eq_u32 %[srare], -1, %[vt3]", ["srare"])] + plain[5:] + \
+        [V(f"v_cmp_gt_i32 %[stp], 0, %[{h[7]}]", ["stp"]),
+         S(f"s_or_b64 %[sm], {cref('scy')}, %[stp]", ["sm"])] + fix_fast(h)
+    lf, _ = schedule(fast)
+    ls, _ = schedule(exact + fix_seq(h, h, "scy"))
+    return emit_split("fe_fold_asm", ["Fold of the exact 512-bit product (curve25519_ops.cu:114-145): t_lo as halves",
+                                      "ta[0..7], x_i = lo64(19 t_{i+4}) as halves xa[0..7]; carry chain with the lossy",
+                                      "carry cy_i = c_i & !(x_i == 2^64-1 & cy_{i-1}), then the fix-up.  The plain",
+                                      "chain and the fast fix-up unless a lane is on a rare edge (wave-uniform test)."],
+                      [("ta", "a"), ("xa", "x")], h, ["vt1", "vt2", "vt3"],
+                      ["scy", "srare", "stp", "sm", "sk0", "sk2"], lf, FIX_SGPRS + ["scy", "sq1", "sq2", "sq3"], ls)
 
 
 def gen_sub():
@@ -256,14 +301,9 @@ def gen_sub():
     so the borrow chain is the plain one; and no lane has t0 < 19 (implies t0's high word is 0),
     t1 == M or t2 == M (their low words are 2^32-1), so the "+ p" pass is t + m (-19, 0, 0, 2^63)."""
     t = [f"h{i}" for i in range(8)]
-    test1 = [V("v_max3_u32 %[vt3], %[b2], %[b4], %[b6]"),
-             V("v_cmp_eq_u32 %[srare], -1, %[vt3]", ["srare"])]
     plain = [V("v_sub_co_u32 %[h0], %[scy], %[a0], %[b0]", ["scy"])]
     for i in range(1, 8):
         plain.append(V(f"v_subb_co_u32 %[h{i}], %[scy], %[a{i}], %[b{i}], %[scy]", ["scy"], ["scy"]))
-    test2 = [V("v_not_b32 %[vt3], %[h1]"),
-             V("v_max3_u32 %[vt3], %[vt3], %[h2], %[h4]"),
-             V("v_cmp_eq_u32 %[srare], -1, %[vt3]", ["srare"])]
     fastp = [V("v_cndmask_b32 %[vt1], 0, 19, %[scy]", [], ["scy"]),
              V("v_cndmask_b32 %[vt2], 0, %[c80], %[scy]", [], ["scy"]),
              V("v_sub_co_u32 %[h0], %[sk0], %[h0], %[vt1]", ["sk0"]),
@@ -298,19 +338,21 @@ def gen_sub():
               V("v_subb_co_u32 %[h6], %[sk3], %[h6], 0, %[sd3]", ["sk3"], ["sd3"]),
               V("v_subb_co_u32 %[h7], %[sk3], %[h7], 0, %[sk3]", ["sk3"], ["sk3"]),
               V("v_add_u32 %[h7], %[h7], %[vt2]")]                                         # + m 2^63
-    # layout: test1, branch -> 5 (exact chain); plain chain, test2, branch -> 3 (exact "+ p");
-    # fast "+ p", s_branch 4; 5: exact chain (falls through); 3: exact "+ p"; 4: end
-    l1, s1 = schedule(test1 + [S("s_cmp_lg_u64 %[srare], 0"), S("s_cbranch_scc1 5f")])
-    l2, s2 = schedule(plain + test2 + branch_if_rare("3f"), s1)
-    l3, _ = schedule(fastp, s2)
-    l5, s5 = schedule(exact, s1)
-    l6, _ = schedule(exactp, merge(s2, s5))
-    lines = l1 + l2 + l3 + ["s_branch 4f", "5:"] + l5 + ["3:"] + l6 + ["4:"]
-    return emit("fe_sub_asm", ["fe25519_sub (curve25519_ops.cu:71-90) on limb halves: lossy borrow chain, then the",
-                               "literal \"+ p\" pass on a final borrow (fast forms unless a lane is on a rare edge)."],
-                [("fa", "a"), ("ga", "b")], [f"a{i}" for i in range(8)] + [f"b{i}" for i in range(8)],
-                t, ["vt1", "vt2", "vt3"], ["sk0", "sk1", "sk2", "sk3", "sd1", "sd2", "sd3", "scy", "sq1", "sq2",
-                                           "sq3", "srare"], lines)
+    # fast statement: test 1's max of the g words first, the plain chain, test 2's words into the same
+    # max and the one compare as soon as t1, t2 and t4 exist, the rest of the chain, the fast "+ p".
+    # Exact statement (any rare lane): the exact chain from the inputs again and the exact "+ p"
+    # (the exact chain equals the plain one when test 1 finds no lane, so this covers test 2 alone).
+    fast = [V("v_max3_u32 %[vt3], %[b2], %[b4], %[b6]")] + plain[:5] + \
+        [V("v_not_b32 %[vt1], %[h1]"),
+         V("v_max3_u32 %[vt3], %[vt3], %[vt1], %[h2]"),
+         V("v_max_u32 %[vt3], %[vt3], %[h4]"),
+         V("v_cmp_eq_u32 %[srare], -1, %[vt3]", ["srare"])] + plain[5:] + fastp
+    lf, _ = schedule(fast)
+    ls, _ = schedule(exact + exactp)
+    return emit_split("fe_sub_asm", ["fe25519_sub (curve25519_ops.cu:71-90) on limb halves: lossy borrow chain, then the",
+                                     "literal \"+ p\" pass on a final borrow (fast forms unless a lane is on a rare edge)."],
+                      [("fa", "a"), ("ga", "b")], t, ["vt1", "vt2", "vt3"], ["scy", "srare", "sk0"], lf,
+                      ["sk0", "sk1", "sk2", "sk3", "sd1", "sd2", "sd3", "scy", "sq1", "sq2", "sq3"], ls)
 
 
 def renamed(ins, names):
@@ -333,22 +375,21 @@ def gen_addsub():
     the inputs again, exactly as fe_add_asm and fe_sub_asm do (add chain + fix_seq; sub's exact chain
     + exact "+ p").  Same bits as the two separate blocks."""
     h = [f"h{i}" for i in range(8)]   # a + b
-    pre = [V("v_max3_u32 %[vt3], %[b2], %[b4], %[b6]"),
-           V("v_cmp_eq_u32 %[sr1], -1, %[vt3]", ["sr1"]),
-           V("v_add_co_u32 %[h0], %[scy], %[a0], %[b0]", ["scy"]),
-           V("v_sub_co_u32 %[t0], %[sby], %[a0], %[b0]", ["sby"])]
+    chains = [V("v_add_co_u32 %[h0], %[scy], %[a0], %[b0]", ["scy"]),
+              V("v_sub_co_u32 %[t0], %[sby], %[a0], %[b0]", ["sby"])]
     for i in range(1, 8):
-        pre.append(V(f"v_addc_co_u32 %[h{i}], %[scy], %[a{i}], %[b{i}], %[scy]", ["scy"], ["scy"]))
-        pre.append(V(f"v_subb_co_u32 %[t{i}], %[sby], %[a{i}], %[b{i}], %[sby]", ["sby"], ["sby"]))
-    pre += [V("v_max_u32 %[vt3], %[h1], %[h4]"),                      # add: fix_test
-            V("v_not_b32 %[vt4], %[t1]"),                              # sub: test 2
-            V("v_cmp_gt_i32 %[stp], 0, %[h7]", ["stp"]),
-            V("v_max3_u32 %[vt4], %[vt4], %[t2], %[t4]"),
-            V("v_cmp_eq_u32 %[srare], -1, %[vt3]", ["srare"]),
-            V("v_cmp_eq_u32 %[sr2], -1, %[vt4]", ["sr2"]),
-            S("s_or_b64 %[sm], %[scy], %[stp]", ["sm"]),
-            S("s_or_b64 %[srare], %[srare], %[sr1]", ["srare"]),
-            S("s_or_b64 %[srare], %[srare], %[sr2]", ["srare"])]
+        chains.append(V(f"v_addc_co_u32 %[h{i}], %[scy], %[a{i}], %[b{i}], %[scy]", ["scy"], ["scy"]))
+        chains.append(V(f"v_subb_co_u32 %[t{i}], %[sby], %[a{i}], %[b{i}], %[sby]", ["sby"], ["sby"]))
+    # one max over every word the three tests read (sub's test 1: g words; add's fix_test: h1, h4;
+    # sub's test 2: ~t1, t2, t4), compared as soon as the chains have produced limb 4's words
+    pre = [V("v_max3_u32 %[vt3], %[b2], %[b4], %[b6]")] + chains[:10] + \
+        [V("v_not_b32 %[vt4], %[t1]"),
+         V("v_max3_u32 %[vt3], %[vt3], %[h1], %[h4]"),
+         V("v_max3_u32 %[vt3], %[vt3], %[vt4], %[t2]"),
+         V("v_max_u32 %[vt3], %[vt3], %[t4]"),
+         V("v_cmp_eq_u32 %[srare], -1, %[vt3]", ["srare"])] + chains[10:] + \
+        [V("v_cmp_gt_i32 %[stp], 0, %[h7]", ["stp"]),
+         S("s_or_b64 %[sm], %[scy], %[stp]", ["sm"])]
     fast = [V("v_cndmask_b32 %[vt1], 0, 19, %[sm]", [], ["sm"]),
             V("v_cndmask_b32 %[vt4], 0, 19, %[sby]", [], ["sby"]),
             V("v_cndmask_b32 %[vt2], 0, %[c80], %[sm]", [], ["sm"]),
@@ -396,34 +437,13 @@ def gen_addsub():
         V("v_subb_co_u32 %[h6], %[sk3], %[h6], 0, %[sd3]", ["sk3"], ["sd3"]),
         V("v_subb_co_u32 %[h7], %[sk3], %[h7], 0, %[sk3]", ["sk3"], ["sk3"]),
         V("v_add_u32 %[h7], %[h7], %[vt2]")], {**{f"h{i}": f"t{i}" for i in range(8)}, "scy": "sby"})
-    lp, sp = schedule(pre + branch_if_rare("3f"))
-    lf, _ = schedule(fast, sp)
-    ls, _ = schedule(add_exact + sub_exact, sp)
-    lines = lp + lf + ["s_branch 4f", "3:"] + ls + ["4:"]
-    t = [f"t{i}" for i in range(8)]
-    sgprs = FIX_SGPRS + ["scy", "sby", "sr1", "sr2", "srare", "sq1", "sq2", "sq3"]
-    ins = [f"a{i}" for i in range(8)] + [f"b{i}" for i in range(8)]
-    text = "\\n\\t".join(lines + GUARD)
-    out = ["// fe_add(a, b) and fe_sub(a, b) in one block (curve25519_ops.cu:41-90): the two carry chains",
-           "// interleaved, one rare-edge branch for both (tools/gen_field_asm.py gen_addsub).",
-           "__device__ __forceinline__ void fe_addsub_asm(uint32_t os[8], uint32_t od[8], const uint32_t fa[8], "
-           "const uint32_t ga[8]) {"]
-    for p, pre_ in (("fa", "a"), ("ga", "b")):
-        out.append("    const uint32_t " + ", ".join(f"{pre_}{i} = {p}[{i}]" for i in range(8)) + ";")
-    vt = ["vt1", "vt2", "vt3", "vt4", "vt5"]
-    out.append("    uint32_t " + ", ".join(h + t + vt) + ";")
-    out.append("    uint64_t " + ", ".join(sgprs) + ";")
-    out.append(f'    asm volatile("{text}"')
-    out.append("                 : " + ", ".join([f'[{x}] "=&v"({x})' for x in h + t + vt] +
-                                          [f'[{x}] "=&s"({x})' for x in sgprs]))
-    out.append("                 : " + ", ".join([f'[{x}] "v"({x})' for x in ins] +
-                                          ['[c80] "v"(0x80000000u)', '[p0l] "s"(0xFFFFFFEDu)']))
-    out.append('                 : "scc");')
-    for i in range(8):
-        out.append(f"    os[{i}] = h{i}; od[{i}] = t{i};")
-    out.append("    (void)" + "; (void)".join(sgprs + vt) + ";")
-    out.append("}")
-    return out
+    lf, _ = schedule(pre + fast)
+    ls, _ = schedule(add_exact + sub_exact)
+    return emit_split("fe_addsub_asm", ["fe_add(a, b) and fe_sub(a, b) in one block (curve25519_ops.cu:41-90): the two carry",
+                                        "chains interleaved, one rare-edge test for both (tools/gen_field_asm.py gen_addsub)."],
+                      [("fa", "a"), ("ga", "b")], h + [f"t{i}" for i in range(8)], ["vt1", "vt2", "vt3", "vt4", "vt5"],
+                      ["scy", "sby", "srare", "stp", "sm", "sk0", "sk1", "sk2"], lf,
+                      FIX_SGPRS + ["scy", "sby", "sq1", "sq2", "sq3"], ls)
 
 
 def gen_canon():
