@@ -304,6 +304,9 @@ __device__ __forceinline__ fe row_of_form(const ge& r) {
 __device__ __forceinline__ ge row_of_point(const fe& r3) {   // X3 | T3 | Z3 | Y3 by quad -> replicated
     return ge{fe_row_bcast<0>(r3), fe_row_bcast<12>(r3), fe_row_bcast<8>(r3), fe_row_bcast<4>(r3)};
 }
+#ifndef BP_ROW_CTRL
+#define BP_ROW_CTRL 1
+#endif
 __device__ __forceinline__ ge sm_row(const fe& s, const ge& P, const ge* __restrict__ dtab, const ge* ptab, int K) {
     const fe qs = row_of_form(P);
     const int lz = fe_clz256(s);
@@ -315,6 +318,36 @@ __device__ __forceinline__ ge sm_row(const fe& s, const ge& P, const ge* __restr
     uint32_t bit = bs_next(bs);
     bool add_phase = false;   // false: next op doubles; true: next op adds P
     fe o = row_of_form(r0), r3;
+#if BP_ROW_CTRL
+    // The same decisions as the branchy loop below, as selects: each 16-lane row has its own scalar,
+    // so every per-lane `if` there became an exec-mask save / branch / restore whose SALU half waits
+    // on the compare just before it (≈20 cycles each on one wave, tools/ubench_dep.hip).  Here the
+    // next op's phase, the bit index and the stream advance are computed before the step (off its
+    // critical path), the exit is the one divergent test, and the stream's refill (every 64 bits
+    // of a row) runs under a wave-uniform test.
+    while (true) {
+        const bool take = !add_phase && bit;   // the next op adds P
+        const int adv = take ? 0 : 1;           // else: the next bit
+        const bool done = i - adv < 0;
+        const uint32_t nbit = (uint32_t)(bs.cur >> 63);
+        r3 = ge_row_of_step(o, fe_sel(add_phase, qs, o));
+        if (done) break;
+        i -= adv;
+        add_phase = take;
+        bit = adv ? nbit : bit;
+        bs.cur = adv ? bs.cur << 1 : bs.cur;
+        bs.left -= adv;
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(bs.left == 0) != 0, 0)) {
+            const bool rf = bs.left == 0;
+            bs.cur = rf ? bs.n1 : bs.cur;
+            bs.n1 = rf ? bs.n2 : bs.n1;
+            bs.n2 = rf ? bs.n3 : bs.n2;
+            bs.n3 = rf ? 0 : bs.n3;
+            bs.left = rf ? 64 : bs.left;
+        }
+        o = row_of_next(r3);
+    }
+#else
     while (true) {
         r3 = ge_row_of_step(o, fe_sel(add_phase, qs, o));
         if (!add_phase && bit) {
@@ -326,6 +359,7 @@ __device__ __forceinline__ ge sm_row(const fe& s, const ge& P, const ge* __restr
         }
         o = row_of_next(r3);
     }
+#endif
     return row_of_point(r3);
 }
 
