@@ -74,6 +74,7 @@ __device__ __forceinline__ void q4_rows(const fe& x, uint32_t a[2]) {
 #ifndef BP_Q4_SUM_ASM
 #define BP_Q4_SUM_ASM 1
 #endif
+template <bool LAT = false>
 __device__ __forceinline__ fe fe_q4_sum_fold(const uint32_t w[10]) {
     uint32_t r[16];
 #if BP_Q4_SUM_ASM && defined(__HIP_DEVICE_COMPILE__)
@@ -107,8 +108,9 @@ __device__ __forceinline__ fe fe_q4_sum_fold(const uint32_t w[10]) {
     uint64_t t[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) t[i] = (uint64_t)r[2 * i] | ((uint64_t)r[2 * i + 1] << 32);
-    return fe_fold512(t);
+    return fe_fold512<LAT>(t);
 }
+template <bool LAT = false>
 __device__ __forceinline__ fe fe_mul_q4(const fe& x, const fe& y) {
     uint32_t a[2], b[8], w[10];
     q4_rows(x, a);
@@ -119,14 +121,15 @@ __device__ __forceinline__ fe fe_mul_q4(const fe& x, const fe& y) {
     }
     mul2x8_bounded_asm(w, a, b);   // the counting form when a lane's a[0] exceeds the bound (mul512_asm.h)
     if (__builtin_expect(__any(a[0] > MUL_BOUNDED_WORD), 0)) mul2x8_asm(w, a, b);
-    return fe_q4_sum_fold(w);
+    return fe_q4_sum_fold<LAT>(w);
 }
 // fe_mul_q4(x, k) for the curve constant k: the rows by k's SGPR words, one carry counted (mul2x8_k_asm)
+template <bool LAT = false>
 __device__ __forceinline__ fe fe_mul_q4_k(const fe& x) {
     uint32_t a[2], w[10];
     q4_rows(x, a);
     mul2x8_k_asm(w, a);
-    return fe_q4_sum_fold(w);
+    return fe_q4_sum_fold<LAT>(w);
 }
 // Stages 2 and 3 of ge25519_add from the quad's stage-1 products (lane qd holds product qd of
 // {A, B, T1 T2, Z1 Z2}); the result replicated over the quad.
@@ -280,22 +283,28 @@ __device__ __forceinline__ fe fe_row_bcast(const fe& a) {
     }
     return r;
 }
+// BP_ROW_LAT: the row step's field blocks in their latency forms (field_asm.h *_lat: m = carry | top in
+// VALU, no SALU OR waiting on a compare; 2 more VALU per block, which the one wave per SIMD of a row tick
+// does not feel)
+#ifndef BP_ROW_LAT
+#define BP_ROW_LAT 1
+#endif
 __device__ __forceinline__ fe ge_row_of_step(const fe& o, const fe& q) {
     const int qi = (threadIdx.x >> 2) & 3;
-    const fe p1 = fe_mul_q4(o, q);   // role qi's stage-1 product, on the quad's lane 0
+    const fe p1 = fe_mul_q4<BP_ROW_LAT>(o, q);   // role qi's stage-1 product, on the quad's lane 0
     const fe A = fe_row_bcast<0>(p1), CT = fe_row_bcast<4>(p1), D0 = fe_row_bcast<8>(p1), B = fe_row_bcast<12>(p1);
-    const fe C = fe_quad_bcast<0>(fe_mul_q4_k(CT));
-    const fe D = fe_add(D0, D0);
+    const fe C = fe_quad_bcast<0>(fe_mul_q4_k<BP_ROW_LAT>(CT));
+    const fe D = fe_add<BP_ROW_LAT>(D0, D0);
     fe E, F, G, H;
-    fe_addsub(B, A, H, E);   // H = B + A, E = B - A
-    fe_addsub(D, C, G, F);   // G = D + C, F = D - C
-    return fe_quad_bcast<0>(fe_mul_q4(fe_sel(qi & 2, G, E), fe_sel(qi & 1, H, F)));
+    fe_addsub<BP_ROW_LAT>(B, A, H, E);   // H = B + A, E = B - A
+    fe_addsub<BP_ROW_LAT>(D, C, G, F);   // G = D + C, F = D - C
+    return fe_quad_bcast<0>(fe_mul_q4<BP_ROW_LAT>(fe_sel(qi & 2, G, E), fe_sel(qi & 1, H, F)));
 }
 __device__ __forceinline__ fe row_of_next(const fe& r3) {   // quad 0: Y3 - X3, quad 3: X3 + Y3
     const int qi = (threadIdx.x >> 2) & 3;
     const fe sw = fe_dpp<0x140>(r3);   // row_mirror: quad q <- quad 3 - q
     fe s, d;
-    fe_addsub(sw, r3, s, d);
+    fe_addsub<BP_ROW_LAT>(sw, r3, s, d);
     return fe_sel(qi == 0, d, fe_sel(qi == 3, s, r3));
 }
 __device__ __forceinline__ fe row_of_form(const ge& r) {

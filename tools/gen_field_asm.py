@@ -140,6 +140,23 @@ def fix_fast(h):
             V(f"v_addc_co_u32 %[{h[5]}], %[sk2], %[{h[5]}], 0, %[sk2]", ["sk2"], ["sk2"])]
 
 
+def fix_fast_lat(h, carry="scy"):
+    """fix_fast for the latency forms (the 16-lane row step): m = carry | top as a VALU mask, 0 or
+    -1, instead of a compare and the SALU OR, which waits ≈16 cycles on that compare when one wave
+    runs alone (tools/ubench_dep.hip cmp_sor_add).  Two more VALU than fix_fast's compare and two
+    selects: a loss where many waves hide the wait (the throughput kernels keep fix_fast)."""
+    return [V(f"v_ashrrev_i32 %[vt2], 31, %[{h[7]}]"),
+            V(f"v_cndmask_b32 %[vt2], %[vt2], -1, %[{carry}]", [], [carry]),
+            V("v_and_b32 %[vt1], 19, %[vt2]"),
+            V("v_lshrrev_b32 %[vt3], 31, %[vt2]"),
+            V("v_and_b32 %[vt2], %[c80], %[vt2]"),
+            V(f"v_add_co_u32 %[{h[0]}], %[sk0], %[{h[0]}], %[vt1]", ["sk0"]),
+            V(f"v_add_co_u32 %[{h[4]}], %[sk2], %[{h[4]}], %[vt3]", ["sk2"]),
+            V(f"v_add_u32 %[{h[7]}], %[{h[7]}], %[vt2]"),
+            V(f"v_addc_co_u32 %[{h[1]}], %[sk0], %[{h[1]}], 0, %[sk0]", ["sk0"], ["sk0"]),
+            V(f"v_addc_co_u32 %[{h[5]}], %[sk2], %[{h[5]}], 0, %[sk2]", ["sk2"], ["sk2"])]
+
+
 def branch_if_rare(label):
     return [S("s_cmp_lg_u64 %[srare], 0"), S(f"s_cbranch_scc1 {label}")]
 
@@ -237,24 +254,27 @@ def add_chain(h, a="a", b="b", cy="scy", upto=8, start=0):
     return out
 
 
-def gen_add():
+def gen_add(lat=False):
     """Fast statement: the add chain with fix_test's compare placed as soon as h1 and h4 exist, then
-    m = carry | top and the fast fix-up.  Exact statement: the chain again and fix_seq."""
+    m = carry | top and the fast fix-up (lat: fix_fast_lat).  Exact statement: the chain again and
+    fix_seq."""
     h = [f"h{i}" for i in range(8)]
     fast = add_chain(h, upto=5) + [V("v_max_u32 %[vt3], %[h1], %[h4]"),
-                                    V("v_cmp_eq_u32 %[srare], -1, %[vt3]", ["srare"])] + \
-        add_chain(h, start=5) + [V("v_cmp_gt_i32 %[stp], 0, %[h7]", ["stp"]),
-                                 S("s_or_b64 %[sm], %[scy], %[stp]", ["sm"])] + fix_fast(h)
+                                    V("v_cmp_eq_u32 %[srare], -1, %[vt3]", ["srare"])] + add_chain(h, start=5)
+    if lat:
+        fast += fix_fast_lat(h)
+    else:
+        fast += [V("v_cmp_gt_i32 %[stp], 0, %[h7]", ["stp"]), S("s_or_b64 %[sm], %[scy], %[stp]", ["sm"])] + fix_fast(h)
     lf, _ = schedule(fast)
     ls, _ = schedule(add_chain(h) + fix_seq(h, h, "scy"))
-    return emit_split("fe_add_asm", ["fe25519_add (curve25519_ops.cu:41-68) on limb halves: exact 257-bit sum, then",
+    return emit_split("fe_add_asm" + ("_lat" if lat else ""), ["fe25519_add (curve25519_ops.cu:41-68) on limb halves: exact 257-bit sum, then",
                                      "one lossy \"- p\" when it carried out or is >= p (fast form unless a lane is",
                                      "on one of the fix-up's rare edges: fix_test)."],
                       [("fa", "a"), ("ga", "b")], h, ["vt1", "vt2", "vt3"],
-                      ["scy", "srare", "stp", "sm", "sk0", "sk2"], lf, FIX_SGPRS + ["scy"], ls)
+                      ["scy", "srare", "sk0", "sk2"] + ([] if lat else ["stp", "sm"]), lf, FIX_SGPRS + ["scy"], ls)
 
 
-def gen_fold():
+def gen_fold(lat=False):
     """One wave-uniform rare-edge test: if some x_i (i = 1..3) may be 2^64-1 (its low word is: the
     lossy carry can differ from the true one) or fix_test's edge words are all ones, the exact chain
     (from the inputs again) + exact fix-up; else the plain chain + the fast fix-up."""
@@ -279,17 +299,21 @@ def gen_fold():
     # the exact chain from the inputs again and the exact fix-up.
     fast = [V("v_max3_u32 %[vt3], %[x2], %[x4], %[x6]")] + plain[:5] + \
         [V(f"v_max3_u32 %[vt3], %[vt3], %[{h[1]}], %[{h[4]}]"),
-         V("v_cmp_eq_u32 %[srare], -1, %[vt3]", ["srare"])] + plain[5:] + \
-        [V(f"v_cmp_gt_i32 %[stp], 0, %[{h[7]}]", ["stp"]),
-         S(f"s_or_b64 %[sm], {cref('scy')}, %[stp]", ["sm"])] + fix_fast(h)
+         V("v_cmp_eq_u32 %[srare], -1, %[vt3]", ["srare"])] + plain[5:]
+    if lat:
+        fast += fix_fast_lat(h)
+    else:
+        fast += [V(f"v_cmp_gt_i32 %[stp], 0, %[{h[7]}]", ["stp"]),
+                 S(f"s_or_b64 %[sm], {cref('scy')}, %[stp]", ["sm"])] + fix_fast(h)
     lf, _ = schedule(fast)
     ls, _ = schedule(exact + fix_seq(h, h, "scy"))
-    return emit_split("fe_fold_asm", ["Fold of the exact 512-bit product (curve25519_ops.cu:114-145): t_lo as halves",
+    return emit_split("fe_fold_asm" + ("_lat" if lat else ""), ["Fold of the exact 512-bit product (curve25519_ops.cu:114-145): t_lo as halves",
                                       "ta[0..7], x_i = lo64(19 t_{i+4}) as halves xa[0..7]; carry chain with the lossy",
                                       "carry cy_i = c_i & !(x_i == 2^64-1 & cy_{i-1}), then the fix-up.  The plain",
                                       "chain and the fast fix-up unless a lane is on a rare edge (wave-uniform test)."],
                       [("ta", "a"), ("xa", "x")], h, ["vt1", "vt2", "vt3"],
-                      ["scy", "srare", "stp", "sm", "sk0", "sk2"], lf, FIX_SGPRS + ["scy", "sq1", "sq2", "sq3"], ls)
+                      ["scy", "srare", "sk0", "sk2"] + ([] if lat else ["stp", "sm"]), lf,
+                      FIX_SGPRS + ["scy", "sq1", "sq2", "sq3"], ls)
 
 
 def gen_sub():
@@ -365,7 +389,7 @@ def renamed(ins, names):
     return out
 
 
-def gen_addsub():
+def gen_addsub(lat=False):
     """fe_add(a, b) and fe_sub(a, b) of the same operands in one block (ge25519_add's E = B - A with
     H = B + A, and F = D - C with G = D + C; the lane-quad forms' next operands Y - X / Y + X), for
     the latency-bound drain chains: the two carry chains interleaved, so a link reads its carry two
@@ -387,9 +411,9 @@ def gen_addsub():
          V("v_max3_u32 %[vt3], %[vt3], %[h1], %[h4]"),
          V("v_max3_u32 %[vt3], %[vt3], %[vt4], %[t2]"),
          V("v_max_u32 %[vt3], %[vt3], %[t4]"),
-         V("v_cmp_eq_u32 %[srare], -1, %[vt3]", ["srare"])] + chains[10:] + \
-        [V("v_cmp_gt_i32 %[stp], 0, %[h7]", ["stp"]),
-         S("s_or_b64 %[sm], %[scy], %[stp]", ["sm"])]
+         V("v_cmp_eq_u32 %[srare], -1, %[vt3]", ["srare"])] + chains[10:]
+    if not lat:
+        pre += [V("v_cmp_gt_i32 %[stp], 0, %[h7]", ["stp"]), S("s_or_b64 %[sm], %[scy], %[stp]", ["sm"])]
     fast = [V("v_cndmask_b32 %[vt1], 0, 19, %[sm]", [], ["sm"]),
             V("v_cndmask_b32 %[vt4], 0, 19, %[sby]", [], ["sby"]),
             V("v_cndmask_b32 %[vt2], 0, %[c80], %[sm]", [], ["sm"]),
@@ -402,6 +426,22 @@ def gen_addsub():
             V("v_addc_co_u32 %[h1], %[sk0], %[h1], 0, %[sk0]", ["sk0"], ["sk0"]),
             V("v_subb_co_u32 %[t1], %[sk1], %[t1], 0, %[sk1]", ["sk1"], ["sk1"]),
             V("v_addc_co_u32 %[h5], %[sk2], %[h5], 0, %[sk2]", ["sk2"], ["sk2"])]
+    if lat:   # add's m = carry | top as a VALU mask (fix_fast_lat), sub's "+ p" as above, interleaved
+        fast = [V("v_ashrrev_i32 %[vt2], 31, %[h7]"),
+                V("v_cndmask_b32 %[vt4], 0, 19, %[sby]", [], ["sby"]),
+                V("v_cndmask_b32 %[vt2], %[vt2], -1, %[scy]", [], ["scy"]),
+                V("v_cndmask_b32 %[vt5], 0, %[c80], %[sby]", [], ["sby"]),
+                V("v_and_b32 %[vt1], 19, %[vt2]"),
+                V("v_lshrrev_b32 %[vt3], 31, %[vt2]"),
+                V("v_and_b32 %[vt2], %[c80], %[vt2]"),
+                V("v_add_co_u32 %[h0], %[sk0], %[h0], %[vt1]", ["sk0"]),
+                V("v_sub_co_u32 %[t0], %[sk1], %[t0], %[vt4]", ["sk1"]),
+                V("v_add_co_u32 %[h4], %[sk2], %[h4], %[vt3]", ["sk2"]),
+                V("v_add_u32 %[h7], %[h7], %[vt2]"),
+                V("v_add_u32 %[t7], %[t7], %[vt5]"),
+                V("v_addc_co_u32 %[h1], %[sk0], %[h1], 0, %[sk0]", ["sk0"], ["sk0"]),
+                V("v_subb_co_u32 %[t1], %[sk1], %[t1], 0, %[sk1]", ["sk1"], ["sk1"]),
+                V("v_addc_co_u32 %[h5], %[sk2], %[h5], 0, %[sk2]", ["sk2"], ["sk2"])]
     add_exact = [V("v_add_co_u32 %[h0], %[scy], %[a0], %[b0]", ["scy"])]
     for i in range(1, 8):
         add_exact.append(V(f"v_addc_co_u32 %[h{i}], %[scy], %[a{i}], %[b{i}], %[scy]", ["scy"], ["scy"]))
@@ -439,10 +479,10 @@ def gen_addsub():
         V("v_add_u32 %[h7], %[h7], %[vt2]")], {**{f"h{i}": f"t{i}" for i in range(8)}, "scy": "sby"})
     lf, _ = schedule(pre + fast)
     ls, _ = schedule(add_exact + sub_exact)
-    return emit_split("fe_addsub_asm", ["fe_add(a, b) and fe_sub(a, b) in one block (curve25519_ops.cu:41-90): the two carry",
+    return emit_split("fe_addsub_asm" + ("_lat" if lat else ""), ["fe_add(a, b) and fe_sub(a, b) in one block (curve25519_ops.cu:41-90): the two carry",
                                         "chains interleaved, one rare-edge test for both (tools/gen_field_asm.py gen_addsub)."],
                       [("fa", "a"), ("ga", "b")], h + [f"t{i}" for i in range(8)], ["vt1", "vt2", "vt3", "vt4", "vt5"],
-                      ["scy", "sby", "srare", "stp", "sm", "sk0", "sk1", "sk2"], lf,
+                      ["scy", "sby", "srare", "sk0", "sk1", "sk2"] + ([] if lat else ["stp", "sm"]), lf,
                       FIX_SGPRS + ["scy", "sby", "sq1", "sq2", "sq3"], ls)
 
 
@@ -529,7 +569,10 @@ def main(path=OUT):
            "// gfx950 inline-asm fe25519 add and product fold: the same bits as the C forms in fe25519_dev.h.",
            "#pragma once", "#include <stdint.h>", "namespace bp {"]
     out += gen_add() + [""] + gen_sub() + [""] + gen_fold() + [""] + gen_canon() + [""] + gen_addsub() + [""] + \
-        gen_q4_sum()
+        gen_q4_sum() + [""]
+    out += ["// Latency forms (the 16-lane row step, one wave per SIMD): the same blocks with m = carry | top",
+            "// computed in VALU (fix_fast_lat) instead of a compare + SALU OR; same bits."]
+    out += gen_add(lat=True) + [""] + gen_fold(lat=True) + [""] + gen_addsub(lat=True)
     out.append("}  // namespace bp")
     open(path, "w").write("\n".join(out) + "\n")
     print("wrote", path)
