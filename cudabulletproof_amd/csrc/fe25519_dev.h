@@ -126,9 +126,10 @@ BP_DEV uint64_t cat64(uint32_t lo, uint32_t hi) { return (uint64_t)lo | ((uint64
 
 // fe25519_add (curve25519_ops.cu:41-68): exact 257-bit sum (one 32-bit carry chain), then
 // one lossy "- p" when the sum carried out or is >= p.
-// LAT: the latency form of the generated block (field_asm.h fe_add_asm_lat, the 16-lane row step).
-template <bool LAT = false>
-BP_DEV fe fe_add(const fe& f, const fe& g) {
+// LAT 1: the latency form of the generated block (field_asm.h fe_add_asm_lat, the 16-lane row step);
+// LAT 2: its fast statement alone, the rare-edge test deferred into *acc (fe_add_asm_lat_acc).
+template <int LAT = 0>
+BP_DEV fe fe_add(const fe& f, const fe& g, uint32_t* acc = nullptr) {
 #if BP_FIELD_ASM && defined(__HIP_DEVICE_COMPILE__)   // generated gfx950 form (field_asm.h), same bits
     uint32_t a[8], b[8], o[8];
 #pragma unroll
@@ -136,7 +137,7 @@ BP_DEV fe fe_add(const fe& f, const fe& g) {
         a[2 * i] = lo32(f.v[i]); a[2 * i + 1] = hi32(f.v[i]);
         b[2 * i] = lo32(g.v[i]); b[2 * i + 1] = hi32(g.v[i]);
     }
-    if constexpr (LAT) fe_add_asm_lat(o, a, b); else fe_add_asm(o, a, b);
+    if constexpr (LAT == 2) fe_add_asm_lat_acc(o, a, b, *acc); else if constexpr (LAT == 1) fe_add_asm_lat(o, a, b); else fe_add_asm(o, a, b);
     return fe{{cat64(o[0], o[1]), cat64(o[2], o[3]), cat64(o[4], o[5]), cat64(o[6], o[7])}};
 #else
     fe h;
@@ -192,8 +193,8 @@ BP_DEV fe fe_sub(const fe& f, const fe& g) {
 
 // fe_add(f, g) and fe_sub(f, g) together (the generated block interleaves the two carry chains:
 // fewer wait states in the latency-bound lane-quad chains); the same bits as the two calls.
-template <bool LAT = false>
-BP_DEV void fe_addsub(const fe& f, const fe& g, fe& sum, fe& diff) {
+template <int LAT = 0>
+BP_DEV void fe_addsub(const fe& f, const fe& g, fe& sum, fe& diff, uint32_t* acc = nullptr) {
 #if BP_FIELD_ASM && defined(__HIP_DEVICE_COMPILE__)
     uint32_t a[8], b[8], os[8], od[8];
 #pragma unroll
@@ -201,7 +202,9 @@ BP_DEV void fe_addsub(const fe& f, const fe& g, fe& sum, fe& diff) {
         a[2 * i] = lo32(f.v[i]); a[2 * i + 1] = hi32(f.v[i]);
         b[2 * i] = lo32(g.v[i]); b[2 * i + 1] = hi32(g.v[i]);
     }
-    if constexpr (LAT) fe_addsub_asm_lat(os, od, a, b); else fe_addsub_asm(os, od, a, b);
+    if constexpr (LAT == 2) fe_addsub_asm_lat_acc(os, od, a, b, *acc);
+    else if constexpr (LAT == 1) fe_addsub_asm_lat(os, od, a, b);
+    else fe_addsub_asm(os, od, a, b);
     sum = fe{{cat64(os[0], os[1]), cat64(os[2], os[3]), cat64(os[4], os[5]), cat64(os[6], os[7])}};
     diff = fe{{cat64(od[0], od[1]), cat64(od[2], od[3]), cat64(od[4], od[5]), cat64(od[6], od[7])}};
 #else
@@ -216,8 +219,8 @@ BP_DEV void fe_addsub(const fe& f, const fe& g, fe& sum, fe& diff) {
 //   if (cy || t >= p) lossy "- p"
 // Computed as one carry chain t_i + x_i + cy (x_i = lo64(19 t_{i+4})): the same sum; the
 // carry differs only when x_i = 2^64-1 and cy = 1 (c wraps to 0, the reference carries 0).
-template <bool LAT = false>
-BP_DEV fe fe_fold512(const uint64_t t[8]) {
+template <int LAT = 0>
+BP_DEV fe fe_fold512(const uint64_t t[8], uint32_t* acc = nullptr) {
 #if BP_FIELD_ASM && defined(__HIP_DEVICE_COMPILE__)   // generated gfx950 form (field_asm.h), same bits
     uint32_t a[8], xh[8], o[8];
 #pragma unroll
@@ -226,7 +229,7 @@ BP_DEV fe fe_fold512(const uint64_t t[8]) {
         a[2 * i] = lo32(t[i]); a[2 * i + 1] = hi32(t[i]);
         xh[2 * i] = lo32(x); xh[2 * i + 1] = hi32(x);
     }
-    if constexpr (LAT) fe_fold_asm_lat(o, a, xh); else fe_fold_asm(o, a, xh);
+    if constexpr (LAT == 2) fe_fold_asm_lat_acc(o, a, xh, *acc); else if constexpr (LAT == 1) fe_fold_asm_lat(o, a, xh); else fe_fold_asm(o, a, xh);
     return fe{{cat64(o[0], o[1]), cat64(o[2], o[3]), cat64(o[4], o[5]), cat64(o[6], o[7])}};
 #else
     fe h;

@@ -74,8 +74,8 @@ __device__ __forceinline__ void q4_rows(const fe& x, uint32_t a[2]) {
 #ifndef BP_Q4_SUM_ASM
 #define BP_Q4_SUM_ASM 1
 #endif
-template <bool LAT = false>
-__device__ __forceinline__ fe fe_q4_sum_fold(const uint32_t w[10]) {
+template <int LAT = 0>
+__device__ __forceinline__ fe fe_q4_sum_fold(const uint32_t w[10], uint32_t* acc = nullptr) {
     uint32_t r[16];
 #if BP_Q4_SUM_ASM && defined(__HIP_DEVICE_COMPILE__)
     q4_sum_asm(r, w);
@@ -108,10 +108,10 @@ __device__ __forceinline__ fe fe_q4_sum_fold(const uint32_t w[10]) {
     uint64_t t[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) t[i] = (uint64_t)r[2 * i] | ((uint64_t)r[2 * i + 1] << 32);
-    return fe_fold512<LAT>(t);
+    return fe_fold512<LAT>(t, acc);
 }
-template <bool LAT = false>
-__device__ __forceinline__ fe fe_mul_q4(const fe& x, const fe& y) {
+template <int LAT = 0>
+__device__ __forceinline__ fe fe_mul_q4(const fe& x, const fe& y, uint32_t* acc = nullptr) {
     uint32_t a[2], b[8], w[10];
     q4_rows(x, a);
 #pragma unroll
@@ -121,15 +121,15 @@ __device__ __forceinline__ fe fe_mul_q4(const fe& x, const fe& y) {
     }
     mul2x8_bounded_asm(w, a, b);   // the counting form when a lane's a[0] exceeds the bound (mul512_asm.h)
     if (__builtin_expect(__any(a[0] > MUL_BOUNDED_WORD), 0)) mul2x8_asm(w, a, b);
-    return fe_q4_sum_fold<LAT>(w);
+    return fe_q4_sum_fold<LAT>(w, acc);
 }
 // fe_mul_q4(x, k) for the curve constant k: the rows by k's SGPR words, one carry counted (mul2x8_k_asm)
-template <bool LAT = false>
-__device__ __forceinline__ fe fe_mul_q4_k(const fe& x) {
+template <int LAT = 0>
+__device__ __forceinline__ fe fe_mul_q4_k(const fe& x, uint32_t* acc = nullptr) {
     uint32_t a[2], w[10];
     q4_rows(x, a);
     mul2x8_k_asm(w, a);
-    return fe_q4_sum_fold<LAT>(w);
+    return fe_q4_sum_fold<LAT>(w, acc);
 }
 // Stages 2 and 3 of ge25519_add from the quad's stage-1 products (lane qd holds product qd of
 // {A, B, T1 T2, Z1 Z2}); the result replicated over the quad.
@@ -289,16 +289,25 @@ __device__ __forceinline__ fe fe_row_bcast(const fe& a) {
 #ifndef BP_ROW_LAT
 #define BP_ROW_LAT 1
 #endif
-__device__ __forceinline__ fe ge_row_of_step(const fe& o, const fe& q) {
+#ifndef BP_ROW_DEFER
+#define BP_ROW_DEFER 1
+#endif
+#ifndef BP_ROW_DEFER_FORCE   // test builds only (tools/ubench_row.hip): every step takes the recompute path
+#define BP_ROW_DEFER_FORCE 0
+#endif
+// LAT 2 (BP_ROW_DEFER): the blocks' fast statements only, their rare-edge words into *acc (sm_row
+// recomputes the step with LAT = BP_ROW_LAT when some lane's acc is 2^32-1)
+template <int LAT = BP_ROW_LAT>
+__device__ __forceinline__ fe ge_row_of_step(const fe& o, const fe& q, uint32_t* acc = nullptr) {
     const int qi = (threadIdx.x >> 2) & 3;
-    const fe p1 = fe_mul_q4<BP_ROW_LAT>(o, q);   // role qi's stage-1 product, on the quad's lane 0
+    const fe p1 = fe_mul_q4<LAT>(o, q, acc);   // role qi's stage-1 product, on the quad's lane 0
     const fe A = fe_row_bcast<0>(p1), CT = fe_row_bcast<4>(p1), D0 = fe_row_bcast<8>(p1), B = fe_row_bcast<12>(p1);
-    const fe C = fe_quad_bcast<0>(fe_mul_q4_k<BP_ROW_LAT>(CT));
-    const fe D = fe_add<BP_ROW_LAT>(D0, D0);
+    const fe C = fe_quad_bcast<0>(fe_mul_q4_k<LAT>(CT, acc));
+    const fe D = fe_add<LAT>(D0, D0, acc);
     fe E, F, G, H;
-    fe_addsub<BP_ROW_LAT>(B, A, H, E);   // H = B + A, E = B - A
-    fe_addsub<BP_ROW_LAT>(D, C, G, F);   // G = D + C, F = D - C
-    return fe_quad_bcast<0>(fe_mul_q4<BP_ROW_LAT>(fe_sel(qi & 2, G, E), fe_sel(qi & 1, H, F)));
+    fe_addsub<LAT>(B, A, H, E, acc);   // H = B + A, E = B - A
+    fe_addsub<LAT>(D, C, G, F, acc);   // G = D + C, F = D - C
+    return fe_quad_bcast<0>(fe_mul_q4<LAT>(fe_sel(qi & 2, G, E), fe_sel(qi & 1, H, F), acc));
 }
 __device__ __forceinline__ fe row_of_next(const fe& r3) {   // quad 0: Y3 - X3, quad 3: X3 + Y3
     const int qi = (threadIdx.x >> 2) & 3;
@@ -339,7 +348,17 @@ __device__ __forceinline__ ge sm_row(const fe& s, const ge& P, const ge* __restr
         const int adv = take ? 0 : 1;           // else: the next bit
         const bool done = i - adv < 0;
         const uint32_t nbit = (uint32_t)(bs.cur >> 63);
+#if BP_ROW_DEFER
+        {   // one rare-edge test per step instead of one per field block (field_asm.h *_lat_acc)
+            const fe qq = fe_sel(add_phase, qs, o);
+            uint32_t acc = 0;
+            r3 = ge_row_of_step<2>(o, qq, &acc);
+            if (BP_ROW_DEFER_FORCE || __builtin_expect(__builtin_amdgcn_ballot_w64(acc == 0xFFFFFFFFu) != 0, 0))
+                r3 = ge_row_of_step<BP_ROW_LAT>(o, qq);
+        }
+#else
         r3 = ge_row_of_step(o, fe_sel(add_phase, qs, o));
+#endif
         if (done) break;
         i -= adv;
         add_phase = take;

@@ -244,6 +244,43 @@ def emit_split(name, doc, args, outs, vtemps, fast_sgprs, fast, slow_sgprs, slow
     return out
 
 
+def emit_acc(name, doc, args, outs, vtemps, sgprs, fast):
+    """The fast statement alone, for callers that defer the rare-edge test (the row step): the words
+    the test reads go into the caller's running max `acc` (v_max_u32 in place of the compare); a
+    rare lane shows as acc == 2^32-1 and the caller recomputes the whole step with the exact-capable
+    forms.  Same VALU count as the fast statement of emit_split, no SALU test, no branch."""
+    ins = [f"{pre}{i}" for _, pre in args for i in range(8)]
+    out = [f"// {d}" for d in doc]
+    out.append(f"__device__ __forceinline__ void {name}(" + ", ".join(f"uint32_t o{k}[8]" for k in range(len(outs) // 8)) +
+               ", " + ", ".join(f"const uint32_t {p}[8]" for p, _ in args) + ", uint32_t& acc) {")
+    for p, pre in args:
+        out.append("    const uint32_t " + ", ".join(f"{pre}{i} = {p}[{i}]" for i in range(8)) + ";")
+    out.append("    uint32_t " + ", ".join(outs + vtemps) + ";")
+    out.append("    uint64_t " + ", ".join(sgprs) + ";")
+    out.append('    asm volatile("{0}"'.format("\\n\\t".join(fast)))
+    out.append("                 : " + ", ".join([f'[{x}] "=&v"({x})' for x in outs + vtemps] + ['[acc] "+v"(acc)'] +
+                                          [f'[{x}] "=&s"({x})' for x in sgprs]))
+    out.append("                 : " + ", ".join([f'[{x}] "v"({x})' for x in ins] + ['[c80] "v"(0x80000000u)']))
+    out.append('                 : "scc");')
+    for k in range(len(outs) // 8):
+        out.append("    " + " ".join(f"o{k}[{i}] = {outs[8 * k + i]};" for i in range(8)))
+    out.append("    (void)" + "; (void)".join(sgprs + vtemps) + ";")
+    out.append("}")
+    return out
+
+
+def to_acc(fast):
+    """The fast statement with the rare-edge compare replaced by the running max into acc."""
+    out = []
+    for t in fast:
+        if t[0] == "v_cmp_eq_u32 %[srare], -1, %[vt3]":
+            out.append(V("v_max_u32 %[acc], %[acc], %[vt3]"))
+        else:
+            out.append(t)
+    assert len(out) == len(fast) and any(t[0].startswith("v_max_u32 %[acc]") for t in out)
+    return out
+
+
 def add_chain(h, a="a", b="b", cy="scy", upto=8, start=0):
     out = []
     for i in range(start, upto):
@@ -254,7 +291,7 @@ def add_chain(h, a="a", b="b", cy="scy", upto=8, start=0):
     return out
 
 
-def gen_add(lat=False):
+def gen_add(lat=False, acc=False):
     """Fast statement: the add chain with fix_test's compare placed as soon as h1 and h4 exist, then
     m = carry | top and the fast fix-up (lat: fix_fast_lat).  Exact statement: the chain again and
     fix_seq."""
@@ -266,6 +303,10 @@ def gen_add(lat=False):
     else:
         fast += [V("v_cmp_gt_i32 %[stp], 0, %[h7]", ["stp"]), S("s_or_b64 %[sm], %[scy], %[stp]", ["sm"])] + fix_fast(h)
     lf, _ = schedule(fast)
+    if acc:
+        return emit_acc("fe_add_asm_lat_acc", ["fe_add_asm_lat's fast statement, the rare-edge test deferred into acc (emit_acc)."],
+                        [("fa", "a"), ("ga", "b")], h, ["vt1", "vt2", "vt3"], ["scy", "sk0", "sk2"],
+                        schedule(to_acc(fast))[0])
     ls, _ = schedule(add_chain(h) + fix_seq(h, h, "scy"))
     return emit_split("fe_add_asm" + ("_lat" if lat else ""), ["fe25519_add (curve25519_ops.cu:41-68) on limb halves: exact 257-bit sum, then",
                                      "one lossy \"- p\" when it carried out or is >= p (fast form unless a lane is",
@@ -274,7 +315,7 @@ def gen_add(lat=False):
                       ["scy", "srare", "sk0", "sk2"] + ([] if lat else ["stp", "sm"]), lf, FIX_SGPRS + ["scy"], ls)
 
 
-def gen_fold(lat=False):
+def gen_fold(lat=False, acc=False):
     """One wave-uniform rare-edge test: if some x_i (i = 1..3) may be 2^64-1 (its low word is: the
     lossy carry can differ from the true one) or fix_test's edge words are all ones, the exact chain
     (from the inputs again) + exact fix-up; else the plain chain + the fast fix-up."""
@@ -306,6 +347,10 @@ def gen_fold(lat=False):
         fast += [V(f"v_cmp_gt_i32 %[stp], 0, %[{h[7]}]", ["stp"]),
                  S(f"s_or_b64 %[sm], {cref('scy')}, %[stp]", ["sm"])] + fix_fast(h)
     lf, _ = schedule(fast)
+    if acc:
+        return emit_acc("fe_fold_asm_lat_acc", ["fe_fold_asm_lat's fast statement, the rare-edge test deferred into acc (emit_acc)."],
+                        [("ta", "a"), ("xa", "x")], h, ["vt1", "vt2", "vt3"], ["scy", "sk0", "sk2"],
+                        schedule(to_acc(fast))[0])
     ls, _ = schedule(exact + fix_seq(h, h, "scy"))
     return emit_split("fe_fold_asm" + ("_lat" if lat else ""), ["Fold of the exact 512-bit product (curve25519_ops.cu:114-145): t_lo as halves",
                                       "ta[0..7], x_i = lo64(19 t_{i+4}) as halves xa[0..7]; carry chain with the lossy",
@@ -389,7 +434,7 @@ def renamed(ins, names):
     return out
 
 
-def gen_addsub(lat=False):
+def gen_addsub(lat=False, acc=False):
     """fe_add(a, b) and fe_sub(a, b) of the same operands in one block (ge25519_add's E = B - A with
     H = B + A, and F = D - C with G = D + C; the lane-quad forms' next operands Y - X / Y + X), for
     the latency-bound drain chains: the two carry chains interleaved, so a link reads its carry two
@@ -478,6 +523,11 @@ def gen_addsub(lat=False):
         V("v_subb_co_u32 %[h7], %[sk3], %[h7], 0, %[sk3]", ["sk3"], ["sk3"]),
         V("v_add_u32 %[h7], %[h7], %[vt2]")], {**{f"h{i}": f"t{i}" for i in range(8)}, "scy": "sby"})
     lf, _ = schedule(pre + fast)
+    if acc:
+        return emit_acc("fe_addsub_asm_lat_acc", ["fe_addsub_asm_lat's fast statement, the rare-edge test deferred into acc (emit_acc)."],
+                        [("fa", "a"), ("ga", "b")], h + [f"t{i}" for i in range(8)],
+                        ["vt1", "vt2", "vt3", "vt4", "vt5"], ["scy", "sby", "sk0", "sk1", "sk2"],
+                        schedule(to_acc(pre + fast))[0])
     ls, _ = schedule(add_exact + sub_exact)
     return emit_split("fe_addsub_asm" + ("_lat" if lat else ""), ["fe_add(a, b) and fe_sub(a, b) in one block (curve25519_ops.cu:41-90): the two carry",
                                         "chains interleaved, one rare-edge test for both (tools/gen_field_asm.py gen_addsub)."],
@@ -572,7 +622,9 @@ def main(path=OUT):
         gen_q4_sum() + [""]
     out += ["// Latency forms (the 16-lane row step, one wave per SIMD): the same blocks with m = carry | top",
             "// computed in VALU (fix_fast_lat) instead of a compare + SALU OR; same bits."]
-    out += gen_add(lat=True) + [""] + gen_fold(lat=True) + [""] + gen_addsub(lat=True)
+    out += gen_add(lat=True) + [""] + gen_fold(lat=True) + [""] + gen_addsub(lat=True) + [""]
+    out += ["// The row step's fast statements with the rare-edge test deferred (emit_acc; ge25519_quad.h sm_row)."]
+    out += gen_add(lat=True, acc=True) + [""] + gen_fold(lat=True, acc=True) + [""] + gen_addsub(lat=True, acc=True)
     out.append("}  // namespace bp")
     open(path, "w").write("\n".join(out) + "\n")
     print("wrote", path)
