@@ -153,3 +153,20 @@ def test_generated_asm_hazard_spacing():
                     sgpr_w, vgpr_w = {}, {}
                 pos += 1
     assert checked > 250, checked   # (315 reads checked at round 6)
+
+
+def test_deferred_forms_are_the_fast_statements():
+    """field_asm.h's *_lat_acc forms (the row step's deferred rare-edge test) are their *_lat block's
+    fast statement with the one rare-edge compare replaced by the running max into acc: the same
+    instructions otherwise, so the same results, and the same test words feed the deferred test."""
+    s = open(os.path.join(ROOT, "cudabulletproof_amd", "csrc", "field_asm.h")).read()
+
+    def statements(fn):
+        body = s[s.index(f"void {fn}("):]
+        body = body[:body.index("\n}\n")]
+        return [m.group(1) for m in re.finditer(r'asm volatile\("((?:[^"\\]|\\.)*)"', body)]
+    for fn in ("fe_add_asm_lat", "fe_fold_asm_lat", "fe_addsub_asm_lat"):
+        fast = statements(fn)[0]
+        acc = statements(fn + "_acc")
+        assert len(acc) == 1 and fast.count("v_cmp_eq_u32 %[srare], -1, %[vt3]") == 1
+        assert acc[0] == fast.replace("v_cmp_eq_u32 %[srare], -1, %[vt3]", "v_max_u32 %[acc], %[acc], %[vt3]")
