@@ -562,7 +562,10 @@ def field_op(op, r, a, b=None, stream=None):
            "addsub_add": 8, "addsub_sub": 9,   # 8/9: the fused add/sub block's sum / difference
            "mul_q4": 10,   # 10: fe25519_mul as the drain forms' quad-split product (fe_mul_q4)
            "mul_k": 11,    # 11: fe25519_mul(a, k), the point operations' product by the constant (fe_mul_k)
-           "mul_q4_k": 12}   # 12: the same split over a lane quad (fe_mul_q4_k, the drain forms' C)
+           "mul_q4_k": 12,   # 12: the same split over a lane quad (fe_mul_q4_k, the drain forms' C)
+           # the row step's latency forms (13, 15/16, 19) and deferred rare-edge forms (14, 17/18, 20)
+           "add_lat": 13, "add_defer": 14, "addsub_lat_add": 15, "addsub_lat_sub": 16,
+           "addsub_defer_add": 17, "addsub_defer_sub": 18, "fold_lat": 19, "fold_defer": 20}
     _chk(lib().hipbp_field_op(ops[op], _c(r.data_ptr()), _c(a.data_ptr()), _c(b.data_ptr()) if b is not None else None,
                               _sz(a.shape[0]), _stream_ptr(stream)))
 

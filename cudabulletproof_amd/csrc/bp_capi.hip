@@ -1336,7 +1336,7 @@ int hipbp_field_op(int op, fe25519* r, const fe25519* a, const fe25519* b, size_
     hipError_t err;
     Engine* e = engine_or_null(&err);
     BP_RET_ON(err);
-    if (op < 0 || op > 12) { g_err = "bad op"; return HIPBP_ERR_ARG; }
+    if (op < 0 || op > 20) { g_err = "bad op"; return HIPBP_ERR_ARG; }
     if (!a || (!b && op != 3 && op != 5 && op != 7 && op != 11 && op != 12)) { g_err = "null operand"; return HIPBP_ERR_ARG; }
     if (count == 0) return HIPBP_OK;
     hipStream_t s = pick(stream, *e);

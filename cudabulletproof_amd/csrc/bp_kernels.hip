@@ -361,6 +361,44 @@ __global__ __launch_bounds__(TPB) void k_field_op(int op, fe* r, const fe* __res
             z = op == 8 ? sm : df;
             break;
         }
+        // the row step's latency forms (LAT 1: field_asm.h *_lat) and its deferred forms (LAT 2:
+        // *_lat_acc, the fast statement alone; here per element, as sm_row does per step: when the
+        // running max of the test words is 2^32-1 the exact-capable form recomputes the result)
+        case 13: z = fe_add<1>(x, y); break;
+        case 14: {
+            uint32_t acc = 0;
+            z = fe_add<2>(x, y, &acc);
+            if (acc == 0xFFFFFFFFu) z = fe_add<1>(x, y);
+            break;
+        }
+        case 15:
+        case 16: {
+            fe sm, df;
+            fe_addsub<1>(x, y, sm, df);
+            z = op == 15 ? sm : df;
+            break;
+        }
+        case 17:
+        case 18: {
+            fe sm, df;
+            uint32_t acc = 0;
+            fe_addsub<2>(x, y, sm, df, &acc);
+            if (acc == 0xFFFFFFFFu) fe_addsub<1>(x, y, sm, df);
+            z = op == 17 ? sm : df;
+            break;
+        }
+        case 19:
+        case 20: {
+            uint64_t t[8] = {x.v[0], x.v[1], x.v[2], x.v[3], y.v[0], y.v[1], y.v[2], y.v[3]};
+            if (op == 19) {
+                z = fe_fold512<1>(t);
+            } else {
+                uint32_t acc = 0;
+                z = fe_fold512<2>(t, &acc);
+                if (acc == 0xFFFFFFFFu) z = fe_fold512<1>(t);
+            }
+            break;
+        }
         default:
 #pragma unroll
             for (int k = 0; k < 4; k++) z.v[k] = x.v[k] + y.v[k];

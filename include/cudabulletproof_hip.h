@@ -307,7 +307,10 @@ int hipbp_point_tree(ge25519* result, const ge25519* points, size_t n, void* str
  * values as ops 0 / 1), 10 fe25519_mul formed as the drain forms' quad-split product (fe_mul_q4:
  * four lanes per element, the same value as op 2), 11 fe25519_mul(a, k) for the curve constant k
  * (fe_mul_k: only provably possible carries counted; the same value as op 2 with b = k; b unused),
- * 12 the same split over a lane quad (fe_mul_q4_k, four lanes per element). */
+ * 12 the same split over a lane quad (fe_mul_q4_k, four lanes per element); the 16-lane row step's
+ * field blocks (same values as ops 0 / 8 / 9 / 6): 13 add, 15 / 16 add-sub, 19 fold in their latency
+ * forms, and 14, 17 / 18, 20 the same through their deferred rare-edge test (fast form, recomputed
+ * when the element's test words hit 2^32-1). */
 int hipbp_field_op(int op, fe25519* r, const fe25519* a, const fe25519* b, size_t count, void* stream);
 /* The verify path's SHA-256 message shapes on the device, item i over in[6i .. 6i+5] (device
  * pointers): kind 0 the y challenge (points (in0,in1), (in2,in3), (in4,in5) as X, Y), 1 z (in0),

@@ -918,16 +918,23 @@ def _edge_cases(op, rng):
     return out
 
 
-@pytest.mark.parametrize("op", ["add", "sub", "fold", "mul", "addsub_add", "addsub_sub"])
+@pytest.mark.parametrize("op", ["add", "sub", "fold", "mul", "addsub_add", "addsub_sub",
+                                "add_lat", "add_defer", "fold_lat", "fold_defer", "addsub_lat_add", "addsub_lat_sub",
+                                "addsub_defer_add", "addsub_defer_sub"])
 def test_field_fast_forms_one_edge_lane_per_wave(bp, oracle, op):
     """The field asm runs a short form unless some lane of the wave sits on one of the rare edges
     (a limb or word equal to 2^64-1 / 2^32-1, t0 >= p0, t0 < 19): the exact form then runs for the
     whole wave.  Here each edge case sits alone in its own wave, at a rotating lane, among 63
     common lanes (the exact form must give those the same bits); further waves hold edge limbs at
     random, and the last ones near-edge values only (words 2^32-2, high words all ones with low
-    words not) that the short form must get right."""
+    words not) that the short form must get right.  The *_lat / *_defer ops run the 16-lane row
+    step's latency forms and its deferred rare-edge test (a missed edge would leave a fast result
+    the oracle rejects)."""
     import torch
-    rng = np.random.default_rng({"add": 1, "sub": 2, "fold": 3, "mul": 4, "addsub_add": 5, "addsub_sub": 6}[op])
+    kind = op
+    op = op.replace("_lat", "").replace("_defer", "")   # the operation the oracle checks
+    rng = np.random.default_rng({"add": 1, "sub": 2, "fold": 3, "mul": 4, "addsub_add": 5, "addsub_sub": 6}[op] +
+                                (10 if "_lat" in kind else 20 if "_defer" in kind else 0))
     # the fused add/sub block (fe_addsub_asm) takes its exact path when either op's edge fires, so
     # it gets both ops' edge cases whichever of its outputs is checked
     cases = _edge_cases(op, rng) if not op.startswith("addsub") else _edge_cases("add", rng) + _edge_cases("sub", rng)
@@ -957,7 +964,7 @@ def test_field_fast_forms_one_edge_lane_per_wave(bp, oracle, op):
     dev = torch.device("cuda:0")
     T = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(np.int64)).to(dev)
     r = torch.empty(N, 4, dtype=torch.int64, device=dev)
-    bp.field_op(op, r, T(a), T(b))
+    bp.field_op(kind, r, T(a), T(b))
     torch.cuda.synchronize()
     got = r.cpu().numpy().view(np.uint64)
     for i in range(N):
@@ -965,7 +972,7 @@ def test_field_fast_forms_one_edge_lane_per_wave(bp, oracle, op):
             want = _ref_fold([int(x) for x in a[i]] + [int(x) for x in b[i]])
         else:
             want = [int(x) for x in getattr(oracle, "fe_" + op.replace("addsub_", ""))(a[i], b[i])]
-        assert [int(x) for x in got[i]] == want, (op, i, [hex(int(x)) for x in a[i]], [hex(int(x)) for x in b[i]])
+        assert [int(x) for x in got[i]] == want, (kind, i, [hex(int(x)) for x in a[i]], [hex(int(x)) for x in b[i]])
 
 
 def test_sq_matches_mul(bp, oracle):
